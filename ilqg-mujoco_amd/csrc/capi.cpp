@@ -1,0 +1,589 @@
+// C ABI (include/ilqg_amd.h): model lifecycle, solver context, host<->device
+// state exchange and the asynchronous hot-path launches.  No CPU physics:
+// every mj_forward / mj_step / FD evaluation runs in the HIP kernels; when no
+// GPU is present the device entry points fail with ILQG_ERR_NODEVICE.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "device/dmodel.h"
+#include "device/kernels.h"
+#include "ilqg_amd.h"
+#include "model/model.h"
+
+using namespace ilqg;
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const std::string& msg) {
+  g_err = msg;
+  return code;
+}
+int hip_fail(hipError_t e, const char* what) {
+  return fail(e == hipErrorNoDevice ? ILQG_ERR_NODEVICE : ILQG_ERR_HIP,
+              std::string(what) + ": " + hipGetErrorName(e) + " (" + hipGetErrorString(e) + ")");
+}
+#define HIPCHK(expr)                                  \
+  do {                                                \
+    hipError_t e_ = (expr);                           \
+    if (e_ != hipSuccess) return hip_fail(e_, #expr); \
+  } while (0)
+
+struct DevBuf {
+  void* p = nullptr;
+  size_t n = 0;
+  ~DevBuf() { release(); }
+  void release() {
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    n = 0;
+  }
+  hipError_t alloc(size_t bytes) {
+    release();
+    n = bytes;
+    if (!bytes) return hipSuccess;
+    hipError_t e = hipMalloc(&p, bytes);
+    if (e != hipSuccess) { p = nullptr; return e; }
+    return hipMemset(p, 0, bytes);
+  }
+  template <typename T>
+  T* as() const { return static_cast<T*>(p); }
+};
+
+int check_device_support(const HostModel& m, bool solver, std::string& why) {
+  for (int j = 0; j < m.njnt; j++)
+    if ((m.jnt_type[j] == 0 || m.jnt_type[j] == 1) && m.jnt_stiffness[j] != 0) {
+      why = "stiffness on ball/free joints is not supported";
+      return ILQG_ERR_UNSUPPORTED;
+    }
+  auto power_ok = [](double p) { return p == (double)(int)p && p >= 1 && p <= 8; };
+  for (int j = 0; j < m.njnt; j++)
+    if (!power_ok(m.jnt_solimp[5 * j + 4])) { why = "solimp power must be an integer in [1,8]"; return ILQG_ERR_UNSUPPORTED; }
+  for (int g = 0; g < m.ngeom; g++)
+    if (!power_ok(m.geom_solimp[5 * g + 4])) { why = "solimp power must be an integer in [1,8]"; return ILQG_ERR_UNSUPPORTED; }
+  if (m.opt_disableflags != 0) { why = "disableflags are not supported"; return ILQG_ERR_UNSUPPORTED; }
+  if (solver) {
+    if (m.nq != m.nv) {
+      why = "ILQR state x = [qpos; qvel] assumes nq == nv (inc/ilqr.h:90, quirk Q21)";
+      return ILQG_ERR_UNSUPPORTED;
+    }
+    if (m.nu > 32 || m.nu < 1) { why = "nu must be in [1, 32]"; return ILQG_ERR_UNSUPPORTED; }
+  }
+  return ILQG_OK;
+}
+
+}  // namespace
+
+struct ilqg_model {
+  HostModel host;
+  std::vector<unsigned char> blob;
+  // device copy (per device ordinal)
+  int dev = -1;
+  DevBuf buf;
+  DevModel dm{};
+  WsLayout L{};
+  hipStream_t stream = nullptr;
+
+  int upload(int device) {
+    if (dev == device && buf.p) return ILQG_OK;
+    HIPCHK(hipSetDevice(device));
+    size_t total = 0;
+#define ILQG_SZ_F(nm, cnt) total += ((host.nm.size() * 8 + 255) & ~(size_t)255);
+#define ILQG_SZ_I(nm, cnt) total += ((host.nm.size() * 4 + 255) & ~(size_t)255);
+    ILQG_MODEL_F64_ARRAYS(ILQG_SZ_F)
+    ILQG_MODEL_I32_ARRAYS(ILQG_SZ_I)
+    std::vector<unsigned char> img(total + 256, 0);
+    size_t off = 0;
+    std::vector<std::pair<size_t, const void**>> fix;
+#define ILQG_CP_F(nm, cnt)                                                     \
+  {                                                                            \
+    if (!host.nm.empty()) memcpy(img.data() + off, host.nm.data(), host.nm.size() * 8); \
+    fix.emplace_back(off, (const void**)&dm.nm);                               \
+    off += ((host.nm.size() * 8 + 255) & ~(size_t)255);                        \
+  }
+#define ILQG_CP_I(nm, cnt)                                                     \
+  {                                                                            \
+    std::vector<int> v_(host.nm.begin(), host.nm.end());                       \
+    if (!v_.empty()) memcpy(img.data() + off, v_.data(), v_.size() * 4);       \
+    fix.emplace_back(off, (const void**)&dm.nm);                               \
+    off += ((host.nm.size() * 4 + 255) & ~(size_t)255);                        \
+  }
+    ILQG_MODEL_F64_ARRAYS(ILQG_CP_F)
+    ILQG_MODEL_I32_ARRAYS(ILQG_CP_I)
+    HIPCHK(buf.alloc(img.size()));
+    HIPCHK(hipMemcpy(buf.p, img.data(), img.size(), hipMemcpyHostToDevice));
+    for (auto& f : fix) *f.second = static_cast<unsigned char*>(buf.p) + f.first;
+#define ILQG_SC_I(nm) dm.nm = host.nm;
+#define ILQG_SC_F(nm) dm.nm = host.nm;
+    ILQG_MODEL_I32_SCALARS(ILQG_SC_I)
+    ILQG_MODEL_F64_SCALARS(ILQG_SC_F)
+    dm.maxcon = host.maxcon;
+    dm.maxefc = host.maxefc;
+    L = make_layout(dm);
+    if (!stream) HIPCHK(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
+    dev = device;
+    return ILQG_OK;
+  }
+  ~ilqg_model() {
+    if (stream) (void)hipStreamDestroy(stream);
+  }
+};
+
+struct ilqg_solver {
+  const ilqg_model* model = nullptr;
+  ilqg_solver_opts opts{};
+  int S = 0, A = 0, P = 0, D = 0, nx = 0, ncol = 0;
+  hipStream_t stream = nullptr;
+  DevBuf traj[5], cand[5], dinit[5];
+  DevBuf qfrc_applied, xfrc_applied, K, k, deriv, warm_c, cost_c, V, v, cost_cand, cost_sel, sel, alphas, cost;
+  DevBuf wsd, wsi;
+  int nlanes = 0;
+  std::vector<double> host_alphas;
+  bool initialized = false;
+
+  TrajDev tview(DevBuf* b) const {
+    return TrajDev{b[0].as<double>(), b[1].as<double>(), b[2].as<double>(), b[3].as<double>(), b[4].as<double>()};
+  }
+  CostDev cview() const {
+    const double* c = cost.as<double>();
+    const int nq = model->host.nq, nv = model->host.nv, nu = model->host.nu;
+    return CostDev{c, c + nq, c + 2 * nq, c + 3 * nq, c + 3 * nq + nv, c + 3 * nq + 2 * nv,
+                   c + 3 * nq + 3 * nv, c + 3 * nq + 3 * nv + nu, c + 3 * nq + 3 * nv + 2 * nu};
+  }
+  WsDev ws() const { return WsDev{wsd.as<double>(), wsi.as<int>(), nlanes}; }
+  ~ilqg_solver() {
+    if (stream) (void)hipStreamDestroy(stream);
+  }
+};
+
+static std::vector<double> pack_cost(const HostModel& m, const ilqg_cost* c) {
+  const int nq = m.nq, nv = m.nv, nu = m.nu;
+  std::vector<double> out(3 * nq + 3 * nv + 3 * nu, 0.0);
+  if (!c) return out;
+  auto put = [&](const double* src, int n, size_t at) {
+    if (src) std::copy(src, src + n, out.begin() + at);
+  };
+  put(c->wq, nq, 0); put(c->tq, nq, nq); put(c->lq, nq, 2 * nq);
+  put(c->wv, nv, 3 * nq); put(c->tv, nv, 3 * nq + nv); put(c->lv, nv, 3 * nq + 2 * nv);
+  put(c->wu, nu, 3 * nq + 3 * nv); put(c->tu, nu, 3 * nq + 3 * nv + nu); put(c->lu, nu, 3 * nq + 3 * nv + 2 * nu);
+  return out;
+}
+
+extern "C" {
+
+const char* ilqg_last_error(void) { return g_err.c_str(); }
+int ilqg_version(void) { return 100; }
+
+int ilqg_device_count(int* count) {
+  if (!count) return fail(ILQG_ERR_ARG, "null count");
+  int n = 0;
+  hipError_t e = hipGetDeviceCount(&n);
+  if (e != hipSuccess) { *count = 0; return hip_fail(e, "hipGetDeviceCount"); }
+  *count = n;
+  return ILQG_OK;
+}
+
+// ---------------------------------------------------------------- model --
+static int finish_model(ilqg_model* m, ilqg_model** out) {
+  m->blob = write_blob(m->host);
+  *out = m;
+  return ILQG_OK;
+}
+
+int ilqg_model_load_xml(const char* path, ilqg_model** out) {
+  if (!path || !out) return fail(ILQG_ERR_ARG, "null argument");
+  auto* m = new ilqg_model();
+  std::string err;
+  if (!compile_mjcf_file(path, m->host, err)) {
+    delete m;
+    return fail(ILQG_ERR_MODEL, err);
+  }
+  return finish_model(m, out);
+}
+
+int ilqg_model_load_xml_string(const char* xml, ilqg_model** out) {
+  if (!xml || !out) return fail(ILQG_ERR_ARG, "null argument");
+  auto* m = new ilqg_model();
+  std::string err;
+  if (!compile_mjcf_string(xml, m->host, err)) {
+    delete m;
+    return fail(ILQG_ERR_MODEL, err);
+  }
+  return finish_model(m, out);
+}
+
+void ilqg_model_free(ilqg_model* m) { delete m; }
+
+int ilqg_model_sizes(const ilqg_model* m, int* s) {
+  if (!m || !s) return fail(ILQG_ERR_ARG, "null argument");
+  const HostModel& h = m->host;
+  int v[10] = {h.nq, h.nv, h.nu, h.nbody, h.njnt, h.ngeom, h.maxcon, h.maxefc, h.nconmax, h.njmax};
+  memcpy(s, v, sizeof(v));
+  return ILQG_OK;
+}
+
+int ilqg_model_timestep(const ilqg_model* m, double* dt) {
+  if (!m || !dt) return fail(ILQG_ERR_ARG, "null argument");
+  *dt = m->host.opt_timestep;
+  return ILQG_OK;
+}
+
+int ilqg_model_qpos0(const ilqg_model* m, double* q) {
+  if (!m || !q) return fail(ILQG_ERR_ARG, "null argument");
+  std::copy(m->host.qpos0.begin(), m->host.qpos0.end(), q);
+  return ILQG_OK;
+}
+
+int ilqg_model_blob(const ilqg_model* m, void* buf, size_t cap, size_t* needed) {
+  if (!m) return fail(ILQG_ERR_ARG, "null model");
+  if (needed) *needed = m->blob.size();
+  if (buf) {
+    if (cap < m->blob.size()) return fail(ILQG_ERR_ARG, "buffer too small");
+    memcpy(buf, m->blob.data(), m->blob.size());
+  }
+  return ILQG_OK;
+}
+
+// ------------------------------------------------------ batched physics --
+namespace {
+struct Scratch {
+  DevBuf time, qpos, qvel, warm, ctrl, qa, xf, out, wsd, wsi, warm_c, cost_c, cost;
+};
+int prep_batch(ilqg_model* m, int n, int lanes, Scratch& s, const double* time, const double* qpos,
+               const double* qvel, const double* warm, const double* ctrl, const double* qfrc_applied,
+               const double* xfrc_applied) {
+  std::string why;
+  int rc = check_device_support(m->host, false, why);
+  if (rc) return fail(rc, why);
+  rc = m->upload(0);
+  if (rc) return rc;
+  const HostModel& h = m->host;
+  HIPCHK(s.time.alloc(n * 8));
+  HIPCHK(s.qpos.alloc((size_t)n * h.nq * 8));
+  HIPCHK(s.qvel.alloc((size_t)n * h.nv * 8));
+  HIPCHK(s.warm.alloc((size_t)n * h.nv * 8));
+  HIPCHK(s.ctrl.alloc((size_t)n * h.nu * 8));
+  HIPCHK(s.qa.alloc((size_t)n * h.nv * 8));
+  HIPCHK(s.xf.alloc((size_t)n * 6 * h.nbody * 8));
+  HIPCHK(s.wsd.alloc((size_t)lanes * m->L.nd * 8));
+  HIPCHK(s.wsi.alloc((size_t)lanes * m->L.ni * 4));
+  auto up = [&](DevBuf& b, const double* src, size_t cnt) -> hipError_t {
+    if (!src) return hipSuccess;
+    return hipMemcpy(b.p, src, cnt * 8, hipMemcpyHostToDevice);
+  };
+  HIPCHK(up(s.time, time, n));
+  HIPCHK(up(s.qpos, qpos, (size_t)n * h.nq));
+  HIPCHK(up(s.qvel, qvel, (size_t)n * h.nv));
+  HIPCHK(up(s.warm, warm, (size_t)n * h.nv));
+  HIPCHK(up(s.ctrl, ctrl, (size_t)n * h.nu));
+  HIPCHK(up(s.qa, qfrc_applied, (size_t)n * h.nv));
+  HIPCHK(up(s.xf, xfrc_applied, (size_t)n * 6 * h.nbody));
+  return ILQG_OK;
+}
+}  // namespace
+
+int ilqg_step_batch(const ilqg_model* mc, int n, int nstep, double* time, double* qpos, double* qvel, double* warm,
+                    const double* ctrl, const double* qfrc_applied, const double* xfrc_applied) {
+  auto* m = const_cast<ilqg_model*>(mc);
+  if (!m || n <= 0 || nstep < 0 || !qpos || !qvel || !warm || !ctrl) return fail(ILQG_ERR_ARG, "bad argument");
+  Scratch s;
+  std::vector<double> t0(n, 0.0);
+  int rc = prep_batch(m, n, n, s, time ? time : t0.data(), qpos, qvel, warm, ctrl, qfrc_applied, xfrc_applied);
+  if (rc) return rc;
+  TrajDev st{s.time.as<double>(), s.qpos.as<double>(), s.qvel.as<double>(), s.warm.as<double>(), s.ctrl.as<double>()};
+  HIPCHK(launch_step(m->dm, m->L, WsDev{s.wsd.as<double>(), s.wsi.as<int>(), n}, st, n, nstep, s.qa.as<double>(),
+                     s.xf.as<double>(), m->stream));
+  HIPCHK(hipStreamSynchronize(m->stream));
+  const HostModel& h = m->host;
+  if (time) HIPCHK(hipMemcpy(time, s.time.p, n * 8, hipMemcpyDeviceToHost));
+  HIPCHK(hipMemcpy(qpos, s.qpos.p, (size_t)n * h.nq * 8, hipMemcpyDeviceToHost));
+  HIPCHK(hipMemcpy(qvel, s.qvel.p, (size_t)n * h.nv * 8, hipMemcpyDeviceToHost));
+  HIPCHK(hipMemcpy(warm, s.warm.p, (size_t)n * h.nv * 8, hipMemcpyDeviceToHost));
+  return ILQG_OK;
+}
+
+int ilqg_forward_batch(const ilqg_model* mc, int n, const double* qpos, const double* qvel, double* warm,
+                       const double* ctrl, const double* qfrc_applied, const double* xfrc_applied, double* qacc) {
+  auto* m = const_cast<ilqg_model*>(mc);
+  if (!m || n <= 0 || !qpos || !qvel || !warm || !ctrl || !qacc) return fail(ILQG_ERR_ARG, "bad argument");
+  Scratch s;
+  std::vector<double> t0(n, 0.0);
+  int rc = prep_batch(m, n, n, s, t0.data(), qpos, qvel, warm, ctrl, qfrc_applied, xfrc_applied);
+  if (rc) return rc;
+  const HostModel& h = m->host;
+  HIPCHK(s.out.alloc((size_t)n * h.nv * 8));
+  TrajDev st{s.time.as<double>(), s.qpos.as<double>(), s.qvel.as<double>(), s.warm.as<double>(), s.ctrl.as<double>()};
+  HIPCHK(launch_forward(m->dm, m->L, WsDev{s.wsd.as<double>(), s.wsi.as<int>(), n}, st, n, s.qa.as<double>(),
+                        s.xf.as<double>(), s.out.as<double>(), m->stream));
+  HIPCHK(hipStreamSynchronize(m->stream));
+  HIPCHK(hipMemcpy(qacc, s.out.p, (size_t)n * h.nv * 8, hipMemcpyDeviceToHost));
+  HIPCHK(hipMemcpy(warm, s.warm.p, (size_t)n * h.nv * 8, hipMemcpyDeviceToHost));
+  return ILQG_OK;
+}
+
+int ilqg_fd_batch(const ilqg_model* mc, int n, const double* qpos, const double* qvel, const double* warm,
+                  const double* ctrl, const double* qfrc_applied, const double* xfrc_applied, const ilqg_cost* cost,
+                  double* deriv) {
+  auto* m = const_cast<ilqg_model*>(mc);
+  if (!m || n <= 0 || !qpos || !qvel || !warm || !ctrl || !deriv) return fail(ILQG_ERR_ARG, "bad argument");
+  const HostModel& h = m->host;
+  const int nctrl = std::min(h.nu, h.nv), ncol = nctrl + 2 * h.nv;
+  const int D = h.nv * (2 * h.nv + h.nu) + 2 * h.nv + h.nu;
+  Scratch s;
+  std::vector<double> t0(n, 0.0);
+  int lanes = n * ncol;
+  int rc = prep_batch(m, n, lanes, s, t0.data(), qpos, qvel, warm, ctrl, qfrc_applied, xfrc_applied);
+  if (rc) return rc;
+  std::vector<double> cp = pack_cost(h, cost);
+  HIPCHK(s.cost.alloc(cp.size() * 8));
+  HIPCHK(hipMemcpy(s.cost.p, cp.data(), cp.size() * 8, hipMemcpyHostToDevice));
+  HIPCHK(s.warm_c.alloc((size_t)n * h.nv * 8));
+  HIPCHK(s.cost_c.alloc((size_t)n * 8));
+  HIPCHK(s.out.alloc((size_t)n * D * 8));
+  const double* c = s.cost.as<double>();
+  const int nq = h.nq, nv = h.nv, nu = h.nu;
+  CostDev cd{c, c + nq, c + 2 * nq, c + 3 * nq, c + 3 * nq + nv, c + 3 * nq + 2 * nv,
+             c + 3 * nq + 3 * nv, c + 3 * nq + 3 * nv + nu, c + 3 * nq + 3 * nv + 2 * nu};
+  TrajDev st{s.time.as<double>(), s.qpos.as<double>(), s.qvel.as<double>(), s.warm.as<double>(), s.ctrl.as<double>()};
+  WsDev ws{s.wsd.as<double>(), s.wsi.as<int>(), lanes};
+  HIPCHK(launch_fd_centre(m->dm, m->L, ws, st, n, 1, s.qa.as<double>(), s.xf.as<double>(), cd,
+                          s.warm_c.as<double>(), s.cost_c.as<double>(), m->stream));
+  HIPCHK(launch_fd_cols(m->dm, m->L, ws, st, n, 1, s.qa.as<double>(), s.xf.as<double>(), cd, s.warm_c.as<double>(),
+                        s.cost_c.as<double>(), s.out.as<double>(), m->stream));
+  HIPCHK(hipStreamSynchronize(m->stream));
+  HIPCHK(hipMemcpy(deriv, s.out.p, (size_t)n * D * 8, hipMemcpyDeviceToHost));
+  return ILQG_OK;
+}
+
+// --------------------------------------------------------------- solver --
+int ilqg_solver_create(const ilqg_model* mc, const ilqg_solver_opts* o, const ilqg_cost* cost, ilqg_solver** out) {
+  auto* m = const_cast<ilqg_model*>(mc);
+  if (!m || !o || !out) return fail(ILQG_ERR_ARG, "null argument");
+  if (o->horizon < 1 || o->nseed < 1 || o->nalpha < 1) return fail(ILQG_ERR_ARG, "horizon, nseed, nalpha must be >= 1");
+  std::string why;
+  int rc = check_device_support(m->host, true, why);
+  if (rc) return fail(rc, why);
+  rc = m->upload(o->device);
+  if (rc) return rc;
+  const HostModel& h = m->host;
+  auto* s = new ilqg_solver();
+  s->model = m;
+  s->opts = *o;
+  s->S = o->nseed;
+  s->A = o->nalpha;
+  s->P = o->horizon + 1;
+  s->nx = 2 * h.nv;
+  s->D = h.nv * (2 * h.nv + h.nu) + 2 * h.nv + h.nu;
+  s->ncol = std::min(h.nu, h.nv) + 2 * h.nv;
+  s->host_alphas.assign(o->nalpha, 1.0);
+  if (o->alphas) std::copy(o->alphas, o->alphas + o->nalpha, s->host_alphas.begin());
+  s->opts.alphas = nullptr;
+  const size_t S = s->S, A = s->A, P = s->P;
+  auto fail_free = [&](hipError_t e, const char* w) {
+    delete s;
+    return hip_fail(e, w);
+  };
+#define ALLOC(b, bytes) do { hipError_t e_ = (b).alloc(bytes); if (e_ != hipSuccess) return fail_free(e_, #b); } while (0)
+  hipError_t e = hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking);
+  if (e != hipSuccess) return fail_free(e, "hipStreamCreate");
+  const size_t fld[5] = {1, (size_t)h.nq, (size_t)h.nv, (size_t)h.nv, (size_t)h.nu};
+  for (int f = 0; f < 5; f++) {
+    ALLOC(s->traj[f], S * P * fld[f] * 8);
+    ALLOC(s->dinit[f], S * fld[f] * 8);
+    if (A > 1) ALLOC(s->cand[f], S * A * P * fld[f] * 8);
+  }
+  ALLOC(s->qfrc_applied, S * h.nv * 8);
+  ALLOC(s->xfrc_applied, S * 6 * h.nbody * 8);
+  ALLOC(s->K, S * P * h.nu * s->nx * 8);  // zero-initialised gains (quirk Q12)
+  ALLOC(s->k, S * P * h.nu * 8);
+  ALLOC(s->deriv, S * P * s->D * 8);
+  ALLOC(s->warm_c, S * P * h.nv * 8);
+  ALLOC(s->cost_c, S * P * 8);
+  ALLOC(s->V, S * s->nx * s->nx * 8);
+  ALLOC(s->v, S * s->nx * 8);
+  ALLOC(s->cost_cand, S * A * 8);
+  ALLOC(s->cost_sel, S * 8);
+  ALLOC(s->sel, S * 4);
+  ALLOC(s->alphas, A * 8);
+  std::vector<double> cp = pack_cost(h, cost);
+  ALLOC(s->cost, cp.size() * 8);
+  s->nlanes = (int)std::max({S * P * (size_t)s->ncol, S * A, S * P});
+  ALLOC(s->wsd, (size_t)s->nlanes * m->L.nd * 8);
+  ALLOC(s->wsi, (size_t)s->nlanes * m->L.ni * 4);
+  e = hipMemcpy(s->alphas.p, s->host_alphas.data(), A * 8, hipMemcpyHostToDevice);
+  if (e != hipSuccess) return fail_free(e, "alphas");
+  e = hipMemcpy(s->cost.p, cp.data(), cp.size() * 8, hipMemcpyHostToDevice);
+  if (e != hipSuccess) return fail_free(e, "cost");
+  size_t lds = backward_lds_bytes(h.nv, h.nu);
+  if (lds > 160 * 1024) {
+    delete s;
+    return fail(ILQG_ERR_UNSUPPORTED, "backward pass LDS footprint exceeds 160 KiB (nx too large)");
+  }
+  *out = s;
+  return ILQG_OK;
+#undef ALLOC
+}
+
+void ilqg_solver_free(ilqg_solver* s) { delete s; }
+
+static int upload_state(ilqg_solver* s, DevBuf* dst, size_t npts, const double* time, const double* qpos,
+                        const double* qvel, const double* warm, const double* ctrl) {
+  const HostModel& h = s->model->host;
+  const double* src[5] = {time, qpos, qvel, warm, ctrl};
+  const size_t fld[5] = {1, (size_t)h.nq, (size_t)h.nv, (size_t)h.nv, (size_t)h.nu};
+  for (int f = 0; f < 5; f++)
+    if (src[f]) HIPCHK(hipMemcpyAsync(dst[f].p, src[f], npts * fld[f] * 8, hipMemcpyHostToDevice, s->stream));
+    else HIPCHK(hipMemsetAsync(dst[f].p, 0, npts * fld[f] * 8, s->stream));
+  HIPCHK(hipStreamSynchronize(s->stream));
+  return ILQG_OK;
+}
+
+int ilqg_solver_init(ilqg_solver* s, const double* time, const double* qpos, const double* qvel, const double* warm,
+                     const double* ctrl, const double* qfrc_applied, const double* xfrc_applied) {
+  if (!s || !qpos || !qvel) return fail(ILQG_ERR_ARG, "bad argument");
+  const ilqg_model* m = s->model;
+  const HostModel& h = m->host;
+  int rc = upload_state(s, s->dinit, s->S, time, qpos, qvel, warm, ctrl);
+  if (rc) return rc;
+  if (qfrc_applied)
+    HIPCHK(hipMemcpy(s->qfrc_applied.p, qfrc_applied, (size_t)s->S * h.nv * 8, hipMemcpyHostToDevice));
+  if (xfrc_applied)
+    HIPCHK(hipMemcpy(s->xfrc_applied.p, xfrc_applied, (size_t)s->S * 6 * h.nbody * 8, hipMemcpyHostToDevice));
+  // ILQR ctor: passive rollout with constant ctrl into dArray[N..0]
+  TrajDev nom = s->tview(s->traj), di = s->tview(s->dinit);
+  HIPCHK(launch_rollout(m->dm, m->L, s->ws(), s->S, 1, s->P, nom, nom, 0, s->K.as<double>(), s->k.as<double>(),
+                        nullptr, di, s->qfrc_applied.as<double>(), s->xfrc_applied.as<double>(), 1, s->cview(),
+                        nullptr, s->stream));
+  HIPCHK(hipStreamSynchronize(s->stream));
+  // setDInit(dmain) as the MPC driver does before iterating (src/inverted_pendulum/inverted_pendulum.cpp:21)
+  s->initialized = true;
+  return upload_state(s, s->dinit, s->S, time, qpos, qvel, warm, ctrl);
+}
+
+int ilqg_solver_set_dinit(ilqg_solver* s, const double* time, const double* qpos, const double* qvel,
+                          const double* warm, const double* ctrl) {
+  if (!s) return fail(ILQG_ERR_ARG, "null solver");
+  return upload_state(s, s->dinit, s->S, time, qpos, qvel, warm, ctrl);
+}
+
+int ilqg_solver_set_traj(ilqg_solver* s, const double* time, const double* qpos, const double* qvel,
+                         const double* warm, const double* ctrl) {
+  if (!s) return fail(ILQG_ERR_ARG, "null solver");
+  s->initialized = true;
+  return upload_state(s, s->traj, (size_t)s->S * s->P, time, qpos, qvel, warm, ctrl);
+}
+
+int ilqg_solver_get_traj(ilqg_solver* s, double* time, double* qpos, double* qvel, double* warm, double* ctrl) {
+  if (!s) return fail(ILQG_ERR_ARG, "null solver");
+  const HostModel& h = s->model->host;
+  double* dst[5] = {time, qpos, qvel, warm, ctrl};
+  const size_t fld[5] = {1, (size_t)h.nq, (size_t)h.nv, (size_t)h.nv, (size_t)h.nu};
+  HIPCHK(hipStreamSynchronize(s->stream));
+  for (int f = 0; f < 5; f++)
+    if (dst[f]) HIPCHK(hipMemcpy(dst[f], s->traj[f].p, (size_t)s->S * s->P * fld[f] * 8, hipMemcpyDeviceToHost));
+  return ILQG_OK;
+}
+
+int ilqg_solver_set_gains(ilqg_solver* s, const double* K, const double* k) {
+  if (!s) return fail(ILQG_ERR_ARG, "null solver");
+  HIPCHK(hipStreamSynchronize(s->stream));
+  if (K) HIPCHK(hipMemcpy(s->K.p, K, s->K.n, hipMemcpyHostToDevice));
+  if (k) HIPCHK(hipMemcpy(s->k.p, k, s->k.n, hipMemcpyHostToDevice));
+  return ILQG_OK;
+}
+
+int ilqg_solver_get_gains(ilqg_solver* s, double* K, double* k) {
+  if (!s) return fail(ILQG_ERR_ARG, "null solver");
+  HIPCHK(hipStreamSynchronize(s->stream));
+  if (K) HIPCHK(hipMemcpy(K, s->K.p, s->K.n, hipMemcpyDeviceToHost));
+  if (k) HIPCHK(hipMemcpy(k, s->k.p, s->k.n, hipMemcpyDeviceToHost));
+  return ILQG_OK;
+}
+
+int ilqg_solver_get_deriv(ilqg_solver* s, double* deriv) {
+  if (!s || !deriv) return fail(ILQG_ERR_ARG, "bad argument");
+  HIPCHK(hipStreamSynchronize(s->stream));
+  HIPCHK(hipMemcpy(deriv, s->deriv.p, s->deriv.n, hipMemcpyDeviceToHost));
+  return ILQG_OK;
+}
+
+int ilqg_solver_get_value(ilqg_solver* s, double* V, double* v) {
+  if (!s) return fail(ILQG_ERR_ARG, "null solver");
+  HIPCHK(hipStreamSynchronize(s->stream));
+  if (V) HIPCHK(hipMemcpy(V, s->V.p, s->V.n, hipMemcpyDeviceToHost));
+  if (v) HIPCHK(hipMemcpy(v, s->v.p, s->v.n, hipMemcpyDeviceToHost));
+  return ILQG_OK;
+}
+
+int ilqg_solver_get_costs(ilqg_solver* s, double* cost, int* selected) {
+  if (!s) return fail(ILQG_ERR_ARG, "null solver");
+  HIPCHK(hipStreamSynchronize(s->stream));
+  if (cost) HIPCHK(hipMemcpy(cost, s->cost_cand.p, s->cost_cand.n, hipMemcpyDeviceToHost));
+  if (selected) HIPCHK(hipMemcpy(selected, s->sel.p, s->sel.n, hipMemcpyDeviceToHost));
+  return ILQG_OK;
+}
+
+int ilqg_forward(ilqg_solver* s) {
+  if (!s || !s->initialized) return fail(ILQG_ERR_ARG, "solver not initialised");
+  const ilqg_model* m = s->model;
+  TrajDev nom = s->tview(s->traj), di = s->tview(s->dinit);
+  const bool multi = s->A > 1;
+  TrajDev outv = multi ? s->tview(s->cand) : nom;
+  HIPCHK(launch_rollout(m->dm, m->L, s->ws(), s->S, s->A, s->P, nom, outv, multi ? 1 : 0, s->K.as<double>(),
+                        s->k.as<double>(), s->alphas.as<double>(), di, s->qfrc_applied.as<double>(),
+                        s->xfrc_applied.as<double>(), 0, s->cview(), s->cost_cand.as<double>(), s->stream));
+  HIPCHK(launch_select(m->dm, s->S, s->A, s->P, s->opts.select_mode, multi ? 1 : 0, s->cost_cand.as<double>(),
+                       s->sel.as<int>(), s->cost_sel.as<double>(), outv, nom, di, s->stream));
+  return ILQG_OK;
+}
+
+int ilqg_fd_sweep(ilqg_solver* s) {
+  if (!s || !s->initialized) return fail(ILQG_ERR_ARG, "solver not initialised");
+  const ilqg_model* m = s->model;
+  TrajDev nom = s->tview(s->traj);
+  const int npts = s->S * s->P;
+  HIPCHK(launch_fd_centre(m->dm, m->L, s->ws(), nom, npts, s->P, s->qfrc_applied.as<double>(),
+                          s->xfrc_applied.as<double>(), s->cview(), s->warm_c.as<double>(), s->cost_c.as<double>(),
+                          s->stream));
+  HIPCHK(launch_fd_cols(m->dm, m->L, s->ws(), nom, npts, s->P, s->qfrc_applied.as<double>(),
+                        s->xfrc_applied.as<double>(), s->cview(), s->warm_c.as<double>(), s->cost_c.as<double>(),
+                        s->deriv.as<double>(), s->stream));
+  return ILQG_OK;
+}
+
+int ilqg_backward(ilqg_solver* s) {
+  if (!s || !s->initialized) return fail(ILQG_ERR_ARG, "solver not initialised");
+  const ilqg_model* m = s->model;
+  HIPCHK(launch_backward(m->dm, s->S, s->P, s->opts.mu, s->deriv.as<double>(), s->tview(s->traj),
+                         s->K.as<double>(), s->k.as<double>(), s->V.as<double>(), s->v.as<double>(), s->stream));
+  return ILQG_OK;
+}
+
+int ilqg_iterate(ilqg_solver* s) {
+  int rc = ilqg_forward(s);
+  if (rc) return rc;
+  rc = ilqg_fd_sweep(s);
+  if (rc) return rc;
+  return ilqg_backward(s);
+}
+
+int ilqg_synchronize(ilqg_solver* s) {
+  if (!s) return fail(ILQG_ERR_ARG, "null solver");
+  HIPCHK(hipStreamSynchronize(s->stream));
+  return ILQG_OK;
+}
+
+void* ilqg_solver_stream(ilqg_solver* s) { return s ? (void*)s->stream : nullptr; }
+
+int ilqg_solver_device_costs(ilqg_solver* s, double** dptr) {
+  if (!s || !dptr) return fail(ILQG_ERR_ARG, "bad argument");
+  *dptr = s->cost_sel.as<double>();
+  return ILQG_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,93 @@
+// Device-side model and per-evaluation workspace layout.
+//
+// The compiled model lives in ONE device allocation; DevModel carries the
+// sizes by value (kernel argument -> SGPRs) and pointers into that allocation
+// (wave-uniform, so model reads become scalar loads).
+//
+// Each physics evaluation ("lane") owns a slice of a workspace laid out
+// structure-of-arrays ACROSS lanes: element e of lane l lives at
+// ws[e * stride + l], so a wave's 64 lanes touching the same field hit 64
+// consecutive doubles (512 B, fully coalesced).
+#pragma once
+
+#include <cstddef>
+
+#include "ilqg_model_fields.h"
+
+namespace ilqg {
+
+struct DevModel {
+#define ILQG_DM_I(nm) int nm;
+#define ILQG_DM_F(nm) double nm;
+#define ILQG_DM_FA(nm, cnt) const double* nm;
+#define ILQG_DM_IA(nm, cnt) const int* nm;
+  ILQG_MODEL_I32_SCALARS(ILQG_DM_I)
+  ILQG_MODEL_F64_SCALARS(ILQG_DM_F)
+  ILQG_MODEL_F64_ARRAYS(ILQG_DM_FA)
+  ILQG_MODEL_I32_ARRAYS(ILQG_DM_IA)
+#undef ILQG_DM_I
+#undef ILQG_DM_F
+#undef ILQG_DM_FA
+#undef ILQG_DM_IA
+  int maxcon, maxefc;
+};
+
+// contact record inside the workspace (doubles, then ints)
+enum {
+  CON_DIST = 0, CON_POS = 1, CON_FRAME = 4, CON_INCLM = 13, CON_FRIC = 14,
+  CON_SOLREF = 19, CON_SOLIMP = 21, CON_ND = 26
+};
+enum { CONI_DIM = 0, CONI_G1 = 1, CONI_G2 = 2, CONI_EFCADR = 3, CON_NI = 4 };
+
+struct WsLayout {
+  int qpos, qvel, ctrl, qacc, warm, qfrc_applied, xfrc_applied, time;
+  int xpos, xquat, xmat, xipos, ximat, xanchor, xaxis, gxpos, gxmat, scom, cdof, cinert, crb;
+  int qM, qLD, qLDinv, amom;
+  int con;
+  int efc_J, efc_pos, efc_margin, efc_D, efc_KBIP, efc_aref, efc_vel, efc_force, efc_b;
+  int cvel, cdof_dot, qfrc_passive, qfrc_bias, afrc, qfrc_act, qfrc_smooth, qacc_smooth, qfrc_con;
+  int s_rne, s_con, s_newton, s_euler, s_rk4, s_fd;
+  int nd;
+  int coni, efc_type, efc_id, efc_state, ncon, nefc;
+  int ni;
+};
+
+inline WsLayout make_layout(const DevModel& m) {
+  WsLayout L{};
+  int o = 0;
+  const int nq = m.nq, nv = m.nv, nu = m.nu, nb = m.nbody, nj = m.njnt, ng = m.ngeom;
+  const int nc = m.maxcon > 0 ? m.maxcon : 1, ne = m.maxefc > 0 ? m.maxefc : 1;
+  auto take = [&](int n) { int r = o; o += n; return r; };
+  L.qpos = take(nq); L.qvel = take(nv); L.ctrl = take(nu); L.qacc = take(nv); L.warm = take(nv);
+  L.qfrc_applied = take(nv); L.xfrc_applied = take(6 * nb); L.time = take(1);
+  L.xpos = take(3 * nb); L.xquat = take(4 * nb); L.xmat = take(9 * nb); L.xipos = take(3 * nb);
+  L.ximat = take(9 * nb); L.xanchor = take(3 * nj); L.xaxis = take(3 * nj); L.gxpos = take(3 * ng);
+  L.gxmat = take(9 * ng); L.scom = take(3 * nb); L.cdof = take(6 * nv); L.cinert = take(10 * nb);
+  L.crb = take(10 * nb); L.qM = take(nv * nv); L.qLD = take(nv * nv); L.qLDinv = take(nv);
+  L.amom = take(nu * nv);
+  L.con = take(CON_ND * nc);
+  L.efc_J = take(ne * nv); L.efc_pos = take(ne); L.efc_margin = take(ne); L.efc_D = take(ne);
+  L.efc_KBIP = take(4 * ne); L.efc_aref = take(ne); L.efc_vel = take(ne); L.efc_force = take(ne);
+  L.efc_b = take(ne);
+  L.cvel = take(6 * nb); L.cdof_dot = take(6 * nv); L.qfrc_passive = take(nv); L.qfrc_bias = take(nv);
+  L.afrc = take(nu); L.qfrc_act = take(nv); L.qfrc_smooth = take(nv); L.qacc_smooth = take(nv);
+  L.qfrc_con = take(nv);
+  L.s_rne = take(12 * nb);
+  L.s_con = take(10 * nv);
+  L.s_newton = take(4 * nv + nv * nv + 2 * ne);
+  L.s_euler = take(2 * nv + 2 * nv * nv);
+  L.s_rk4 = take(2 * nv + 4 * (nq + nv) + 4 * nv);
+  L.s_fd = take(2 * nv);
+  L.nd = o;
+  int oi = 0;
+  L.coni = oi; oi += CON_NI * nc;
+  L.efc_type = oi; oi += ne;
+  L.efc_id = oi; oi += ne;
+  L.efc_state = oi; oi += ne;
+  L.ncon = oi; oi += 1;
+  L.nefc = oi; oi += 1;
+  L.ni = oi;
+  return L;
+}
+
+}  // namespace ilqg

@@ -1,0 +1,59 @@
+// Launch interface of the hot-path kernels (implemented in kernels.hip).
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include "dmodel.h"
+
+namespace ilqg {
+
+// trajectory / state arrays on the device, [point][field]
+struct TrajDev {
+  double* time;
+  double* qpos;
+  double* qvel;
+  double* warm;
+  double* ctrl;
+};
+
+// device cost descriptor (all 9 arrays present, zero where unused)
+struct CostDev {
+  const double *wq, *tq, *lq, *wv, *tv, *lv, *wu, *tu, *lu;
+};
+
+// per-evaluation workspace
+struct WsDev {
+  double* d;
+  int* i;
+  int nlanes;
+};
+
+// FD centre: npts points (point -> seed = point / P), 1 lane each
+hipError_t launch_fd_centre(const DevModel& m, const WsLayout& L, WsDev ws, TrajDev tr, int npts, int P,
+                            const double* qfrc_applied, const double* xfrc_applied, CostDev cost,
+                            double* warm_c, double* cost_c, hipStream_t st);
+// FD columns: npts * (nctrl + 2nv) lanes, writes deriv[npts][D]
+hipError_t launch_fd_cols(const DevModel& m, const WsLayout& L, WsDev ws, TrajDev tr, int npts, int P,
+                          const double* qfrc_applied, const double* xfrc_applied, CostDev cost,
+                          const double* warm_c, const double* cost_c, double* deriv, hipStream_t st);
+// rollout: S*A lanes; passive=1 keeps ctrl (ILQR ctor), else u = K dx + alpha k + u*
+hipError_t launch_rollout(const DevModel& m, const WsLayout& L, WsDev ws, int S, int A, int P, TrajDev nominal,
+                          TrajDev out, int out_is_cand, const double* K, const double* k, const double* alphas,
+                          TrajDev dinit, const double* qfrc_applied, const double* xfrc_applied, int passive,
+                          CostDev cost, double* cost_cand, hipStream_t st);
+// candidate selection + setDInit(dArray[N])
+hipError_t launch_select(const DevModel& m, int S, int A, int P, int mode, int copy_cand, const double* cost_cand,
+                         int* sel, double* cost_sel, TrajDev cand, TrajDev nominal, TrajDev dinit, hipStream_t st);
+// Riccati backward pass, one workgroup per seed
+hipError_t launch_backward(const DevModel& m, int S, int P, double mu, const double* deriv, TrajDev tr, double* K,
+                           double* k, double* V, double* v, hipStream_t st);
+// n independent states: nstep mj_step each (in place)
+hipError_t launch_step(const DevModel& m, const WsLayout& L, WsDev ws, TrajDev st_, int n, int nstep,
+                       const double* qfrc_applied, const double* xfrc_applied, hipStream_t st);
+// n independent states: mj_forward -> qacc
+hipError_t launch_forward(const DevModel& m, const WsLayout& L, WsDev ws, TrajDev st_, int n,
+                          const double* qfrc_applied, const double* xfrc_applied, double* qacc, hipStream_t st);
+
+size_t backward_lds_bytes(int nv, int nu);
+
+}  // namespace ilqg

@@ -1,0 +1,353 @@
+"""Python host binding of the MI355X iLQR hot path (ctypes over the C ABI in
+include/ilqg_amd.h, library lib/libilqg_amd.so built by this directory's
+Makefile).
+
+The reference's host side is C++ (inc/ilqr.h, inc/differentiator.h,
+src/mjderivative.cpp); this module mirrors its operator surface for tests,
+the bench and Python callers:
+
+  Model.load(path)                      mj_loadXML            cmd/basic.cpp:123
+  Model.step(...) / Model.forward(...)  mj_step / mj_forward  inc/ilqr.h:86,128
+  Model.calc_derivatives(...)           calcMJDerivatives     inc/mjderivative.h:7
+  ILQR(model, dmain, N, cost)           ILQR<nv,nu,N> ctor    inc/ilqr.h:69-97
+  ILQR.set_dinit / forward_pass / backward_pass / iterate     inc/ilqr.h:110-186
+
+There is no CPU fallback: a missing library or missing GPU raises.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from dataclasses import dataclass
+from typing import Optional, Sequence
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "lib", "libilqg_amd.so")
+
+_c_double_p = ctypes.POINTER(ctypes.c_double)
+_c_int_p = ctypes.POINTER(ctypes.c_int)
+
+
+class IlqgError(RuntimeError):
+    pass
+
+
+class _Cost(ctypes.Structure):
+    _fields_ = [(n, _c_double_p) for n in ("wq", "tq", "lq", "wv", "tv", "lv", "wu", "tu", "lu")]
+
+
+class _Opts(ctypes.Structure):
+    _fields_ = [
+        ("horizon", ctypes.c_int),
+        ("nseed", ctypes.c_int),
+        ("nalpha", ctypes.c_int),
+        ("alphas", _c_double_p),
+        ("select_mode", ctypes.c_int),
+        ("mu", ctypes.c_double),
+        ("device", ctypes.c_int),
+    ]
+
+
+EXPORTS = [
+    "ilqg_last_error", "ilqg_version", "ilqg_device_count",
+    "ilqg_model_load_xml", "ilqg_model_load_xml_string", "ilqg_model_free", "ilqg_model_sizes",
+    "ilqg_model_timestep", "ilqg_model_qpos0", "ilqg_model_blob",
+    "ilqg_step_batch", "ilqg_forward_batch", "ilqg_fd_batch",
+    "ilqg_solver_create", "ilqg_solver_free", "ilqg_solver_init", "ilqg_solver_set_dinit",
+    "ilqg_solver_set_traj", "ilqg_solver_get_traj", "ilqg_solver_set_gains", "ilqg_solver_get_gains",
+    "ilqg_solver_get_deriv", "ilqg_solver_get_value", "ilqg_solver_get_costs",
+    "ilqg_forward", "ilqg_fd_sweep", "ilqg_backward", "ilqg_iterate", "ilqg_synchronize",
+    "ilqg_solver_stream", "ilqg_solver_device_costs",
+]
+
+_lib = None
+
+
+def lib() -> ctypes.CDLL:
+    """Load the HIP library (fails loudly if it was not built)."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise IlqgError(f"{LIB_PATH} missing: run `make -C ilqg-mujoco_amd` (hipcc, gfx950)")
+        L = ctypes.CDLL(LIB_PATH)
+        L.ilqg_last_error.restype = ctypes.c_char_p
+        L.ilqg_solver_stream.restype = ctypes.c_void_p
+        _lib = L
+    return _lib
+
+
+def _check(rc: int, what: str = ""):
+    if rc != 0:
+        msg = lib().ilqg_last_error().decode(errors="replace")
+        raise IlqgError(f"{what} failed (code {rc}): {msg}")
+
+
+def _ptr(a: Optional[np.ndarray]):
+    if a is None:
+        return None
+    assert a.dtype == np.float64 and a.flags.c_contiguous
+    return a.ctypes.data_as(_c_double_p)
+
+
+def _f64(a, shape=None) -> Optional[np.ndarray]:
+    if a is None:
+        return None
+    a = np.ascontiguousarray(np.asarray(a, dtype=np.float64))
+    if shape is not None:
+        a = a.reshape(shape)
+    return a
+
+
+def device_count() -> int:
+    n = ctypes.c_int(0)
+    rc = lib().ilqg_device_count(ctypes.byref(n))
+    return n.value if rc == 0 else 0
+
+
+@dataclass
+class Cost:
+    """Diagonal-quadratic + linear step cost (ilqg_cost in include/ilqg_amd.h)."""
+    wq: Sequence[float] = ()
+    tq: Sequence[float] = ()
+    lq: Sequence[float] = ()
+    wv: Sequence[float] = ()
+    tv: Sequence[float] = ()
+    lv: Sequence[float] = ()
+    wu: Sequence[float] = ()
+    tu: Sequence[float] = ()
+    lu: Sequence[float] = ()
+
+    def packed(self, nq, nv, nu):
+        def arr(x, n):
+            a = np.zeros(n)
+            x = np.asarray(x, dtype=np.float64).ravel()
+            a[: len(x)] = x
+            return a
+        return {k: arr(getattr(self, k), n) for k, n in
+                (("wq", nq), ("tq", nq), ("lq", nq), ("wv", nv), ("tv", nv), ("lv", nv),
+                 ("wu", nu), ("tu", nu), ("lu", nu))}
+
+    def struct(self, nq, nv, nu):
+        p = self.packed(nq, nv, nu)
+        c = _Cost(**{k: _ptr(v) for k, v in p.items()})
+        c._keep = p
+        return c
+
+
+# inc/inverted_pendulum/cost.h:7-17
+PENDULUM_COST = Cost(wq=[1.0, 10.0], wv=[1.0, 10.0], wu=[1.0])
+# build-defined hopper cost (the reference has none):
+# keep the torso up (rootz -> 1.25) and level, damp velocities, small effort
+HOPPER_COST = Cost(wq=[0.0, 10.0, 1.0, 0.1, 0.1, 0.1], tq=[0.0, 1.25, 0.0, 0.0, 0.0, 0.0],
+                   wv=[0.1] * 6, wu=[0.01] * 3)
+
+
+class Model:
+    """Compiled MJCF model (mjModel equivalent), host + lazily uploaded device copy."""
+
+    def __init__(self, handle):
+        self._h = handle
+        s = (ctypes.c_int * 10)()
+        _check(lib().ilqg_model_sizes(self._h, s), "ilqg_model_sizes")
+        (self.nq, self.nv, self.nu, self.nbody, self.njnt, self.ngeom,
+         self.maxcon, self.maxefc, self.nconmax, self.njmax) = list(s)
+        dt = ctypes.c_double()
+        _check(lib().ilqg_model_timestep(self._h, ctypes.byref(dt)))
+        self.timestep = dt.value
+        q0 = np.zeros(self.nq)
+        _check(lib().ilqg_model_qpos0(self._h, _ptr(q0)))
+        self.qpos0 = q0
+        self.D = self.nv * (2 * self.nv + self.nu) + 2 * self.nv + self.nu
+
+    @classmethod
+    def load(cls, path: str) -> "Model":
+        h = ctypes.c_void_p()
+        _check(lib().ilqg_model_load_xml(path.encode(), ctypes.byref(h)), f"load {path}")
+        return cls(h)
+
+    @classmethod
+    def from_string(cls, xml: str) -> "Model":
+        h = ctypes.c_void_p()
+        _check(lib().ilqg_model_load_xml_string(xml.encode(), ctypes.byref(h)), "load xml string")
+        return cls(h)
+
+    def __del__(self):
+        if getattr(self, "_h", None) and _lib is not None:
+            _lib.ilqg_model_free(self._h)
+            self._h = None
+
+    def blob(self) -> bytes:
+        n = ctypes.c_size_t()
+        _check(lib().ilqg_model_blob(self._h, None, 0, ctypes.byref(n)))
+        buf = ctypes.create_string_buffer(n.value)
+        _check(lib().ilqg_model_blob(self._h, buf, n.value, ctypes.byref(n)))
+        return buf.raw
+
+    def reset_state(self, n=1):
+        """mj_resetData: qpos0, zero velocity/warmstart/ctrl/time."""
+        return State(time=np.zeros(n), qpos=np.tile(self.qpos0, (n, 1)), qvel=np.zeros((n, self.nv)),
+                     warm=np.zeros((n, self.nv)), ctrl=np.zeros((n, self.nu)))
+
+    # ---- batched single-point physics on the GPU ----
+    def step(self, st: "State", nstep: int = 1, qfrc_applied=None, xfrc_applied=None):
+        n = st.qpos.shape[0]
+        _check(lib().ilqg_step_batch(self._h, n, nstep, _ptr(st.time), _ptr(st.qpos), _ptr(st.qvel),
+                                     _ptr(st.warm), _ptr(st.ctrl), _ptr(_f64(qfrc_applied)),
+                                     _ptr(_f64(xfrc_applied))), "ilqg_step_batch")
+        return st
+
+    def forward(self, st: "State", qfrc_applied=None, xfrc_applied=None):
+        n = st.qpos.shape[0]
+        qacc = np.zeros((n, self.nv))
+        _check(lib().ilqg_forward_batch(self._h, n, _ptr(st.qpos), _ptr(st.qvel), _ptr(st.warm),
+                                        _ptr(st.ctrl), _ptr(_f64(qfrc_applied)), _ptr(_f64(xfrc_applied)),
+                                        _ptr(qacc)), "ilqg_forward_batch")
+        return qacc
+
+    def calc_derivatives(self, st: "State", cost: Optional[Cost] = None, qfrc_applied=None, xfrc_applied=None):
+        """calcMJDerivatives at every state of `st` -> (n, D) reference-layout records."""
+        n = st.qpos.shape[0]
+        deriv = np.zeros((n, self.D))
+        cs = cost.struct(self.nq, self.nv, self.nu) if cost is not None else None
+        _check(lib().ilqg_fd_batch(self._h, n, _ptr(st.qpos), _ptr(st.qvel), _ptr(st.warm), _ptr(st.ctrl),
+                                   _ptr(_f64(qfrc_applied)), _ptr(_f64(xfrc_applied)),
+                                   ctypes.byref(cs) if cs is not None else None, _ptr(deriv)), "ilqg_fd_batch")
+        return deriv
+
+
+@dataclass
+class State:
+    """Batch of mjData state records (cpMjData fields, src/util.cpp:4-14)."""
+    time: np.ndarray
+    qpos: np.ndarray
+    qvel: np.ndarray
+    warm: np.ndarray
+    ctrl: np.ndarray
+
+    def __post_init__(self):
+        for k in ("time", "qpos", "qvel", "warm", "ctrl"):
+            setattr(self, k, np.ascontiguousarray(np.asarray(getattr(self, k), dtype=np.float64)))
+        n = self.qpos.shape[0]
+        self.time = self.time.reshape(n)
+
+    def copy(self):
+        return State(self.time.copy(), self.qpos.copy(), self.qvel.copy(), self.warm.copy(), self.ctrl.copy())
+
+
+def assemble_AB(deriv: np.ndarray, nv: int, nu: int, dt: float):
+    """Differentiator::updateDerivatives (inc/differentiator.h:66-71,89-92),
+    reproducing the column-major Map of the row-major record (quirk Q1)."""
+    nx = 2 * nv
+    A = np.zeros((nx, nx))
+    A[:nv, :nv] = np.eye(nv)
+    A[:nv, nv:] = np.eye(nv) * dt
+    A[nv:, :nv] = deriv[: nv * nv].reshape(nv, nv, order="F") * dt
+    A[nv:, nv:] = np.eye(nv) + deriv[nv * nv: 2 * nv * nv].reshape(nv, nv, order="F") * dt
+    B = np.zeros((nx, nu))
+    B[nv:, :] = deriv[2 * nv * nv: 2 * nv * nv + nv * nu].reshape(nv, nu, order="F") * dt
+    return A, B
+
+
+class ILQR:
+    """ILQR<nv,nu,N> (inc/ilqr.h:14-188) over `nseed` independent seeds and
+    `alphas` rollout candidates, all on one GPU.  alphas[0] == 1 with
+    select='reference' reproduces the reference's forwardPass exactly."""
+
+    def __init__(self, model: Model, dmain: State, horizon: int, cost: Cost, alphas=(1.0,),
+                 select: str = "reference", mu: float = 1000.0, device: int = 0,
+                 qfrc_applied=None, xfrc_applied=None):
+        self.model = model
+        self.N = horizon
+        self.P = horizon + 1
+        self.S = dmain.qpos.shape[0]
+        self.alphas = np.ascontiguousarray(np.asarray(alphas, dtype=np.float64))
+        self.A = len(self.alphas)
+        self.nx = 2 * model.nv
+        o = _Opts(horizon=horizon, nseed=self.S, nalpha=self.A, alphas=_ptr(self.alphas),
+                  select_mode=0 if select == "reference" else 1, mu=mu, device=device)
+        cs = cost.struct(model.nq, model.nv, model.nu)
+        h = ctypes.c_void_p()
+        _check(lib().ilqg_solver_create(model._h, ctypes.byref(o), ctypes.byref(cs), ctypes.byref(h)),
+               "ilqg_solver_create")
+        self._h = h
+        self._cost = cs
+        _check(lib().ilqg_solver_init(self._h, _ptr(dmain.time), _ptr(dmain.qpos), _ptr(dmain.qvel),
+                                      _ptr(dmain.warm), _ptr(dmain.ctrl), _ptr(_f64(qfrc_applied)),
+                                      _ptr(_f64(xfrc_applied))), "ilqg_solver_init")
+
+    def __del__(self):
+        if getattr(self, "_h", None) and _lib is not None:
+            _lib.ilqg_solver_free(self._h)
+            self._h = None
+
+    def set_dinit(self, d: State):
+        _check(lib().ilqg_solver_set_dinit(self._h, _ptr(d.time), _ptr(d.qpos), _ptr(d.qvel), _ptr(d.warm),
+                                           _ptr(d.ctrl)), "set_dinit")
+
+    def set_traj(self, t: State):
+        _check(lib().ilqg_solver_set_traj(self._h, _ptr(t.time), _ptr(t.qpos), _ptr(t.qvel), _ptr(t.warm),
+                                          _ptr(t.ctrl)), "set_traj")
+
+    def traj(self) -> State:
+        m, S, P = self.model, self.S, self.P
+        t = State(np.zeros(S * P), np.zeros((S * P, m.nq)), np.zeros((S * P, m.nv)),
+                  np.zeros((S * P, m.nv)), np.zeros((S * P, m.nu)))
+        _check(lib().ilqg_solver_get_traj(self._h, _ptr(t.time), _ptr(t.qpos), _ptr(t.qvel), _ptr(t.warm),
+                                          _ptr(t.ctrl)), "get_traj")
+        return t
+
+    def gains(self):
+        m = self.model
+        K = np.zeros((self.S, self.P, m.nu * self.nx))
+        k = np.zeros((self.S, self.P, m.nu))
+        _check(lib().ilqg_solver_get_gains(self._h, _ptr(K), _ptr(k)), "get_gains")
+        return K, k
+
+    def set_gains(self, K, k):
+        K = _f64(K); k = _f64(k)
+        _check(lib().ilqg_solver_set_gains(self._h, _ptr(K), _ptr(k)), "set_gains")
+
+    def deriv(self):
+        d = np.zeros((self.S, self.P, self.model.D))
+        _check(lib().ilqg_solver_get_deriv(self._h, _ptr(d)), "get_deriv")
+        return d
+
+    def value(self):
+        V = np.zeros((self.S, self.nx * self.nx))
+        v = np.zeros((self.S, self.nx))
+        _check(lib().ilqg_solver_get_value(self._h, _ptr(V), _ptr(v)), "get_value")
+        return V, v
+
+    def costs(self):
+        c = np.zeros((self.S, self.A))
+        sel = np.zeros(self.S, dtype=np.int32)
+        _check(lib().ilqg_solver_get_costs(self._h, _ptr(c), sel.ctypes.data_as(_c_int_p)), "get_costs")
+        return c, sel
+
+    def forward_pass(self):
+        _check(lib().ilqg_forward(self._h), "ilqg_forward")
+
+    def fd_sweep(self):
+        _check(lib().ilqg_fd_sweep(self._h), "ilqg_fd_sweep")
+
+    def backward_pass(self):
+        """initV + Riccati; the FD sweep it depends on is ilqg_fd_sweep."""
+        _check(lib().ilqg_fd_sweep(self._h), "ilqg_fd_sweep")
+        _check(lib().ilqg_backward(self._h), "ilqg_backward")
+
+    def iterate(self):
+        _check(lib().ilqg_iterate(self._h), "ilqg_iterate")
+
+    def synchronize(self):
+        _check(lib().ilqg_synchronize(self._h), "ilqg_synchronize")
+
+    @property
+    def stream(self) -> int:
+        return lib().ilqg_solver_stream(self._h)
+
+    def device_costs_ptr(self) -> int:
+        p = ctypes.POINTER(ctypes.c_double)()
+        _check(lib().ilqg_solver_device_costs(self._h, ctypes.byref(p)), "device_costs")
+        return ctypes.cast(p, ctypes.c_void_p).value

@@ -1,0 +1,136 @@
+/*
+ * ilqg_amd -- MI355X-native iLQR hot path (FD derivative sweep, Riccati
+ * backward pass, forward rollout) behind a plain C ABI.
+ *
+ * Every entry point takes plain pointers and sizes and returns an int status
+ * (ILQG_OK == 0).  Host buffers are row-major float64.  Each entry point names
+ * the reference interface it replaces (paths under /root/reference).
+ *
+ * Trajectory record (the per-point state contract of cpMjData, src/util.cpp:4-14),
+ * per seed s and point p = 0..N (p = N is the initial state, p = 0 the terminal
+ * one, inc/ilqr.h:52):
+ *   time[s][p], qpos[s][p][nq], qvel[s][p][nv], warm[s][p][nv] (qacc_warmstart),
+ *   ctrl[s][p][nu]
+ * qfrc_applied / xfrc_applied are per-seed constants (the reference never
+ * changes them along a trajectory).
+ *
+ * FD record per point (src/mjderivative.cpp:88,107,120,138,174,202), D =
+ * nv*(2nv+nu) + 2nv + nu doubles, written exactly as the reference writes it:
+ *   [i + j*nv]            d qacc_j / d qpos_i
+ *   [nv^2 + i + j*nv]     d qacc_j / d qvel_i
+ *   [2nv^2 + i + j*nu]    d qacc_j / d ctrl_i
+ *   [2nv^2+nv*nu + i]     d cost / d qpos_i   (then qvel, then ctrl)
+ * Gains: K[s][p] is nu x 2nv column-major (Eigen layout, inc/ilqr.h:130),
+ * k[s][p] is nu.
+ */
+#ifndef ILQG_AMD_H
+#define ILQG_AMD_H
+
+#include <stddef.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define ILQG_OK 0
+#define ILQG_ERR_ARG 1
+#define ILQG_ERR_MODEL 2
+#define ILQG_ERR_HIP 3
+#define ILQG_ERR_UNSUPPORTED 4
+#define ILQG_ERR_NODEVICE 5
+
+typedef struct ilqg_model ilqg_model;
+typedef struct ilqg_solver ilqg_solver;
+
+/* Diagonal-quadratic + linear step cost over (qpos, qvel, ctrl), evaluated on
+   the device inside the sweep and the rollout.  Replaces the host callback
+   stepCostFn_t (inc/mjderivative.h:5) on the batched path:
+     c = sum_i wq_i (qpos_i - tq_i)^2 + lq_i qpos_i  + (same for qvel, ctrl)
+   accumulated in (q, v, u) order, index ascending.  inc/inverted_pendulum/
+   cost.h:7-17 is wq = {1,10}, wv = {1,10}, wu = {1}.  NULL arrays mean 0. */
+typedef struct ilqg_cost {
+  const double *wq, *tq, *lq;
+  const double *wv, *tv, *lv;
+  const double *wu, *tu, *lu;
+} ilqg_cost;
+
+typedef struct ilqg_solver_opts {
+  int horizon;          /* N; N+1 trajectory points (inc/ilqr.h:14 template N) */
+  int nseed;            /* independent trajectories (MPC seeds) on this device */
+  int nalpha;           /* rollout candidates per seed; alphas[0] == 1 is the reference rollout */
+  const double* alphas; /* feed-forward scales: u = K(x - x*) + alpha*k + u* */
+  int select_mode;      /* 0: keep alphas[0] (reference semantics); 1: lowest trajectory cost */
+  double mu;            /* Levenberg-Marquardt constant, 1000 in inc/ilqr.h:65 */
+  int device;           /* HIP device ordinal */
+} ilqg_solver_opts;
+
+const char* ilqg_last_error(void);
+int ilqg_version(void);
+int ilqg_device_count(int* count);
+
+/* ---- model: replaces mj_loadXML / mj_deleteModel (cmd/basic.cpp:123) ---- */
+int ilqg_model_load_xml(const char* path, ilqg_model** out);
+int ilqg_model_load_xml_string(const char* xml, ilqg_model** out);
+void ilqg_model_free(ilqg_model* m);
+/* sizes[10] = nq nv nu nbody njnt ngeom maxcon maxefc nconmax njmax */
+int ilqg_model_sizes(const ilqg_model* m, int* sizes);
+int ilqg_model_timestep(const ilqg_model* m, double* dt);
+int ilqg_model_qpos0(const ilqg_model* m, double* qpos0);
+/* compiled-model record (include/ilqg_model_blob.h); needed = bytes required */
+int ilqg_model_blob(const ilqg_model* m, void* buf, size_t cap, size_t* needed);
+
+/* ---- batched single-point physics (device) ----
+   n independent states; host buffers (n x nq etc.).  step: mj_step
+   (inc/ilqr.h:86,128, src/update.cpp:8-11) -- advances time/qpos/qvel/warm in
+   place; forward: mj_forward -> qacc (n x nv), warm updated in place. */
+int ilqg_step_batch(const ilqg_model* m, int n, int nstep, double* time, double* qpos, double* qvel,
+                    double* warm, const double* ctrl, const double* qfrc_applied,
+                    const double* xfrc_applied);
+int ilqg_forward_batch(const ilqg_model* m, int n, const double* qpos, const double* qvel,
+                       double* warm, const double* ctrl, const double* qfrc_applied,
+                       const double* xfrc_applied, double* qacc);
+/* calcMJDerivatives (src/mjderivative.cpp:212-255) at n independent points;
+   deriv is n x D.  cost may be NULL (cost-gradient entries then 0). */
+int ilqg_fd_batch(const ilqg_model* m, int n, const double* qpos, const double* qvel,
+                  const double* warm, const double* ctrl, const double* qfrc_applied,
+                  const double* xfrc_applied, const ilqg_cost* cost, double* deriv);
+
+/* ---- the iLQR solver context (ILQR<nv,nu,N>, inc/ilqr.h:14-188) ---- */
+int ilqg_solver_create(const ilqg_model* m, const ilqg_solver_opts* opts, const ilqg_cost* cost,
+                       ilqg_solver** out);
+void ilqg_solver_free(ilqg_solver* s);
+/* ILQR ctor (inc/ilqr.h:69-97): per seed, d = dmain; initial passive rollout
+   with constant ctrl fills the trajectory; then setDInit(dmain).  dmain
+   arrays are nseed x {1, nq, nv, nv, nu}; applied forces may be NULL (zero). */
+int ilqg_solver_init(ilqg_solver* s, const double* time, const double* qpos, const double* qvel,
+                     const double* warm, const double* ctrl, const double* qfrc_applied,
+                     const double* xfrc_applied);
+/* setDInit (inc/ilqr.h:110-113) per seed */
+int ilqg_solver_set_dinit(ilqg_solver* s, const double* time, const double* qpos, const double* qvel,
+                          const double* warm, const double* ctrl);
+int ilqg_solver_set_traj(ilqg_solver* s, const double* time, const double* qpos, const double* qvel,
+                         const double* warm, const double* ctrl);
+int ilqg_solver_get_traj(ilqg_solver* s, double* time, double* qpos, double* qvel, double* warm,
+                         double* ctrl);
+int ilqg_solver_set_gains(ilqg_solver* s, const double* K, const double* k);
+int ilqg_solver_get_gains(ilqg_solver* s, double* K, double* k);
+int ilqg_solver_get_deriv(ilqg_solver* s, double* deriv);     /* nseed x (N+1) x D */
+int ilqg_solver_get_value(ilqg_solver* s, double* V, double* v); /* nseed x nx x nx (col-major), nseed x nx */
+/* per-seed trajectory cost of every candidate (nseed x nalpha) and the selected index */
+int ilqg_solver_get_costs(ilqg_solver* s, double* cost, int* selected);
+
+/* hot path, enqueued on the solver's stream (asynchronous) */
+int ilqg_forward(ilqg_solver* s);   /* forwardPass over all candidates + selection (inc/ilqr.h:116-130) */
+int ilqg_fd_sweep(ilqg_solver* s);  /* calcMJDerivatives at every point of every seed */
+int ilqg_backward(ilqg_solver* s);  /* initV + Riccati n = 1..N (inc/ilqr.h:100-107,133-176) */
+int ilqg_iterate(ilqg_solver* s);   /* forwardPass; setDInit(dArray[N]); backwardPass (inc/ilqr.h:179-186) */
+int ilqg_synchronize(ilqg_solver* s);
+void* ilqg_solver_stream(ilqg_solver* s); /* hipStream_t */
+/* device pointer to the per-seed selected-candidate cost (nseed doubles), for
+   an in-stream collective (RCCL all-gather) without a host round trip */
+int ilqg_solver_device_costs(ilqg_solver* s, double** dptr);
+
+#ifdef __cplusplus
+}
+#endif
+#endif
