@@ -145,6 +145,35 @@ struct ilqg_solver {
   int nlanes = 0;
   std::vector<double> host_alphas;
   bool initialized = false;
+  hipStream_t own_stream = nullptr;
+  bool timing = false;
+  std::vector<std::pair<hipEvent_t, hipEvent_t>> ev[ILQG_NKERNEL];
+  std::vector<hipEvent_t> event_pool;
+
+  hipEvent_t get_event() {
+    if (!event_pool.empty()) {
+      hipEvent_t e = event_pool.back();
+      event_pool.pop_back();
+      return e;
+    }
+    hipEvent_t e = nullptr;
+    if (hipEventCreate(&e) != hipSuccess) return nullptr;
+    return e;
+  }
+  // record an event pair around a launch when timing is on
+  template <typename F>
+  hipError_t timed(int kind, F&& launch) {
+    if (!timing) return launch();
+    hipEvent_t a = get_event(), b = get_event();
+    if (!a || !b) return hipErrorOutOfMemory;
+    hipError_t e = hipEventRecord(a, stream);
+    if (e != hipSuccess) return e;
+    e = launch();
+    if (e != hipSuccess) return e;
+    e = hipEventRecord(b, stream);
+    ev[kind].emplace_back(a, b);
+    return e;
+  }
 
   TrajDev tview(DevBuf* b) const {
     return TrajDev{b[0].as<double>(), b[1].as<double>(), b[2].as<double>(), b[3].as<double>(), b[4].as<double>()};
@@ -157,7 +186,13 @@ struct ilqg_solver {
   }
   WsDev ws() const { return WsDev{wsd.as<double>(), wsi.as<int>(), nlanes}; }
   ~ilqg_solver() {
-    if (stream) (void)hipStreamDestroy(stream);
+    for (auto& v : ev)
+      for (auto& p : v) {
+        (void)hipEventDestroy(p.first);
+        (void)hipEventDestroy(p.second);
+      }
+    for (auto e : event_pool) (void)hipEventDestroy(e);
+    if (own_stream) (void)hipStreamDestroy(own_stream);
   }
 };
 
@@ -389,8 +424,9 @@ int ilqg_solver_create(const ilqg_model* mc, const ilqg_solver_opts* o, const il
     return hip_fail(e, w);
   };
 #define ALLOC(b, bytes) do { hipError_t e_ = (b).alloc(bytes); if (e_ != hipSuccess) return fail_free(e_, #b); } while (0)
-  hipError_t e = hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking);
+  hipError_t e = hipStreamCreateWithFlags(&s->own_stream, hipStreamNonBlocking);
   if (e != hipSuccess) return fail_free(e, "hipStreamCreate");
+  s->stream = s->own_stream;
   const size_t fld[5] = {1, (size_t)h.nq, (size_t)h.nv, (size_t)h.nv, (size_t)h.nu};
   for (int f = 0; f < 5; f++) {
     ALLOC(s->traj[f], S * P * fld[f] * 8);
@@ -534,11 +570,15 @@ int ilqg_forward(ilqg_solver* s) {
   TrajDev nom = s->tview(s->traj), di = s->tview(s->dinit);
   const bool multi = s->A > 1;
   TrajDev outv = multi ? s->tview(s->cand) : nom;
-  HIPCHK(launch_rollout(m->dm, m->L, s->ws(), s->S, s->A, s->P, nom, outv, multi ? 1 : 0, s->K.as<double>(),
-                        s->k.as<double>(), s->alphas.as<double>(), di, s->qfrc_applied.as<double>(),
-                        s->xfrc_applied.as<double>(), 0, s->cview(), s->cost_cand.as<double>(), s->stream));
-  HIPCHK(launch_select(m->dm, s->S, s->A, s->P, s->opts.select_mode, multi ? 1 : 0, s->cost_cand.as<double>(),
-                       s->sel.as<int>(), s->cost_sel.as<double>(), outv, nom, di, s->stream));
+  HIPCHK(s->timed(0, [&] {
+    return launch_rollout(m->dm, m->L, s->ws(), s->S, s->A, s->P, nom, outv, multi ? 1 : 0, s->K.as<double>(),
+                          s->k.as<double>(), s->alphas.as<double>(), di, s->qfrc_applied.as<double>(),
+                          s->xfrc_applied.as<double>(), 0, s->cview(), s->cost_cand.as<double>(), s->stream);
+  }));
+  HIPCHK(s->timed(1, [&] {
+    return launch_select(m->dm, s->S, s->A, s->P, s->opts.select_mode, multi ? 1 : 0, s->cost_cand.as<double>(),
+                         s->sel.as<int>(), s->cost_sel.as<double>(), outv, nom, di, s->stream);
+  }));
   return ILQG_OK;
 }
 
@@ -547,20 +587,26 @@ int ilqg_fd_sweep(ilqg_solver* s) {
   const ilqg_model* m = s->model;
   TrajDev nom = s->tview(s->traj);
   const int npts = s->S * s->P;
-  HIPCHK(launch_fd_centre(m->dm, m->L, s->ws(), nom, npts, s->P, s->qfrc_applied.as<double>(),
+  HIPCHK(s->timed(2, [&] {
+    return launch_fd_centre(m->dm, m->L, s->ws(), nom, npts, s->P, s->qfrc_applied.as<double>(),
+                            s->xfrc_applied.as<double>(), s->cview(), s->warm_c.as<double>(),
+                            s->cost_c.as<double>(), s->stream);
+  }));
+  HIPCHK(s->timed(3, [&] {
+    return launch_fd_cols(m->dm, m->L, s->ws(), nom, npts, s->P, s->qfrc_applied.as<double>(),
                           s->xfrc_applied.as<double>(), s->cview(), s->warm_c.as<double>(), s->cost_c.as<double>(),
-                          s->stream));
-  HIPCHK(launch_fd_cols(m->dm, m->L, s->ws(), nom, npts, s->P, s->qfrc_applied.as<double>(),
-                        s->xfrc_applied.as<double>(), s->cview(), s->warm_c.as<double>(), s->cost_c.as<double>(),
-                        s->deriv.as<double>(), s->stream));
+                          s->deriv.as<double>(), s->stream);
+  }));
   return ILQG_OK;
 }
 
 int ilqg_backward(ilqg_solver* s) {
   if (!s || !s->initialized) return fail(ILQG_ERR_ARG, "solver not initialised");
   const ilqg_model* m = s->model;
-  HIPCHK(launch_backward(m->dm, s->S, s->P, s->opts.mu, s->deriv.as<double>(), s->tview(s->traj),
-                         s->K.as<double>(), s->k.as<double>(), s->V.as<double>(), s->v.as<double>(), s->stream));
+  HIPCHK(s->timed(4, [&] {
+    return launch_backward(m->dm, s->S, s->P, s->opts.mu, s->deriv.as<double>(), s->tview(s->traj),
+                           s->K.as<double>(), s->k.as<double>(), s->V.as<double>(), s->v.as<double>(), s->stream);
+  }));
   return ILQG_OK;
 }
 
@@ -579,6 +625,38 @@ int ilqg_synchronize(ilqg_solver* s) {
 }
 
 void* ilqg_solver_stream(ilqg_solver* s) { return s ? (void*)s->stream : nullptr; }
+
+int ilqg_solver_set_stream(ilqg_solver* s, void* stream) {
+  if (!s) return fail(ILQG_ERR_ARG, "null solver");
+  HIPCHK(hipStreamSynchronize(s->stream));
+  s->stream = stream ? (hipStream_t)stream : s->own_stream;
+  return ILQG_OK;
+}
+
+int ilqg_solver_set_timing(ilqg_solver* s, int enable) {
+  if (!s) return fail(ILQG_ERR_ARG, "null solver");
+  s->timing = enable != 0;
+  return ILQG_OK;
+}
+
+int ilqg_solver_get_timing(ilqg_solver* s, double* ms, int* launches) {
+  if (!s) return fail(ILQG_ERR_ARG, "null solver");
+  HIPCHK(hipStreamSynchronize(s->stream));
+  for (int k = 0; k < ILQG_NKERNEL; k++) {
+    double tot = 0;
+    for (auto& p : s->ev[k]) {
+      float t = 0;
+      HIPCHK(hipEventElapsedTime(&t, p.first, p.second));
+      tot += t;
+      s->event_pool.push_back(p.first);
+      s->event_pool.push_back(p.second);
+    }
+    if (ms) ms[k] = tot;
+    if (launches) launches[k] = (int)s->ev[k].size();
+    s->ev[k].clear();
+  }
+  return ILQG_OK;
+}
 
 int ilqg_solver_device_costs(ilqg_solver* s, double** dptr) {
   if (!s || !dptr) return fail(ILQG_ERR_ARG, "bad argument");

@@ -59,8 +59,10 @@ EXPORTS = [
     "ilqg_solver_set_traj", "ilqg_solver_get_traj", "ilqg_solver_set_gains", "ilqg_solver_get_gains",
     "ilqg_solver_get_deriv", "ilqg_solver_get_value", "ilqg_solver_get_costs",
     "ilqg_forward", "ilqg_fd_sweep", "ilqg_backward", "ilqg_iterate", "ilqg_synchronize",
-    "ilqg_solver_stream", "ilqg_solver_device_costs",
+    "ilqg_solver_stream", "ilqg_solver_device_costs", "ilqg_solver_set_stream", "ilqg_solver_set_timing",
+    "ilqg_solver_get_timing",
 ]
+KERNELS = ("rollout", "select", "fd_centre", "fd_cols", "backward")
 
 _lib = None
 
@@ -346,6 +348,20 @@ class ILQR:
     @property
     def stream(self) -> int:
         return lib().ilqg_solver_stream(self._h)
+
+    def set_stream(self, stream: Optional[int]):
+        """enqueue on an external hipStream_t (e.g. torch.cuda.current_stream().cuda_stream)"""
+        _check(lib().ilqg_solver_set_stream(self._h, ctypes.c_void_p(stream) if stream else None), "set_stream")
+
+    def set_timing(self, enable: bool):
+        _check(lib().ilqg_solver_set_timing(self._h, int(enable)), "set_timing")
+
+    def timing(self):
+        """{kernel: (total_ms, launches)} since the last call (HIP events on the launch stream)"""
+        ms = (ctypes.c_double * 5)()
+        n = (ctypes.c_int * 5)()
+        _check(lib().ilqg_solver_get_timing(self._h, ms, n), "get_timing")
+        return {k: (ms[i], n[i]) for i, k in enumerate(KERNELS)}
 
     def device_costs_ptr(self) -> int:
         p = ctypes.POINTER(ctypes.c_double)()

@@ -126,6 +126,15 @@ int ilqg_backward(ilqg_solver* s);  /* initV + Riccati n = 1..N (inc/ilqr.h:100-
 int ilqg_iterate(ilqg_solver* s);   /* forwardPass; setDInit(dArray[N]); backwardPass (inc/ilqr.h:179-186) */
 int ilqg_synchronize(ilqg_solver* s);
 void* ilqg_solver_stream(ilqg_solver* s); /* hipStream_t */
+/* enqueue subsequent hot-path launches on an external stream (hipStream_t,
+   e.g. torch's current stream) instead of the solver's own; NULL restores it */
+int ilqg_solver_set_stream(ilqg_solver* s, void* stream);
+/* per-kernel HIP-event timing of the hot path, recorded on the launch stream:
+   index 0 rollout, 1 select, 2 fd_centre, 3 fd_cols, 4 backward */
+#define ILQG_NKERNEL 5
+int ilqg_solver_set_timing(ilqg_solver* s, int enable);
+/* synchronises; returns summed device ms and launch counts per kernel, then resets */
+int ilqg_solver_get_timing(ilqg_solver* s, double* ms, int* launches);
 /* device pointer to the per-seed selected-candidate cost (nseed doubles), for
    an in-stream collective (RCCL all-gather) without a host round trip */
 int ilqg_solver_device_costs(ilqg_solver* s, double** dptr);

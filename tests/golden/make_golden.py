@@ -1,0 +1,78 @@
+"""Generate tests/golden/*.npz from the REFERENCE's own FD driver.
+
+Run in the build container (needs /root/reference for oracle/_ref):
+    python tests/golden/make_golden.py
+
+Each fixture holds inputs (state record at a linearisation point) and the
+`deriv` record that /root/reference/src/mjderivative.cpp (calcMJDerivatives,
+compiled unmodified by oracle/Makefile against the restated physics) writes
+for it.  The model inputs are the reference's own res/*.xml, kept as data
+under tests/golden/models/.  Scenarios follow the reference's call sites:
+  pendulum: 10 passive steps from reset (src/inverted_pendulum/inverted_pendulum.cpp:12-13),
+            then a few more points of the passive trajectory
+  hopper:   500 passive steps, ctrl -= 0.1 (tst/test_derivatives.cpp:38-47), with the
+            test's dummy cost qpos[0] (tst/test_derivatives.cpp:16-20) and the
+            build-defined hopper cost
+"""
+import os
+import sys
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(os.path.dirname(HERE))
+sys.path.insert(0, os.path.join(ROOT, "ilqg-mujoco_amd"))
+sys.path.insert(0, os.path.join(ROOT, "oracle"))
+
+import ilqg_amd as ia  # noqa: E402  (host-only model compile)
+import oracle as ora  # noqa: E402
+
+MODELS = os.path.join(HERE, "models")
+
+
+def state_of(d):
+    s = d.state()
+    return dict(time=np.array([s["time"]]), qpos=s["qpos"], qvel=s["qvel"], warm=s["warm"], ctrl=s["ctrl"])
+
+
+def fd_points(mname, steps_before, ctrl_shift, n_points, gap, cost, cost_fn):
+    m = ia.Model.load(os.path.join(MODELS, mname + ".xml"))
+    rm = ora.OModel(m.blob(), ora.ref_lib())
+    if cost is not None:
+        rm.lib.L.ora_set_cost_desc(ora.CostDesc.from_cost(cost, m.nq, m.nv, m.nu))
+    d = rm.make_data()
+    d.step(steps_before)
+    d.arr("ctrl")[:] += ctrl_shift
+    rec = {k: [] for k in ("time", "qpos", "qvel", "warm", "ctrl", "deriv")}
+    for p in range(n_points):
+        dd = rm.make_data()
+        dd.set_state(**d.state())
+        deriv = ora.calc_derivatives(rm, dd, cost_fn=cost_fn, use_ref=True, nthread=4)
+        for k, v in state_of(d).items():
+            rec[k].append(v)
+        rec["deriv"].append(deriv)
+        d.step(gap)
+    out = {k: np.array(v) for k, v in rec.items()}
+    out["time"] = out["time"].reshape(-1)
+    return out
+
+
+def main():
+    if not os.path.exists("/root/reference/src/mjderivative.cpp"):
+        raise SystemExit("needs /root/reference (build container only)")
+    ora.build(ref=True)
+    dummy = ia.Cost(lq=[1.0])  # tst/test_derivatives.cpp:16-20: cost = qpos[0]
+    specs = {
+        "fd_pendulum.npz": ("inverted_pendulum", 10, 0.0, 8, 5, None, "ora_cost_pendulum"),
+        "fd_hopper_dummycost.npz": ("hopper", 500, -0.1, 4, 25, dummy, "ora_cost_desc_fn"),
+        "fd_hopper.npz": ("hopper", 500, -0.1, 4, 25, ia.HOPPER_COST, "ora_cost_desc_fn"),
+    }
+    for fname, (mname, steps, shift, npt, gap, cost, cfn) in specs.items():
+        out = fd_points(mname, steps, shift, npt, gap, cost, cfn)
+        out["model"] = np.array(mname)
+        np.savez(os.path.join(HERE, fname), **out)
+        print(fname, {k: v.shape for k, v in out.items()})
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,172 @@
+"""Physics sanity of the restated MuJoCo subset (parity with MuJoCo 2.0 itself is
+unpinned; these check the restatement is physically consistent) and the
+Riccati/LDLT restatement against an independent numpy formulation of
+inc/ilqr.h:150-174."""
+import ctypes
+
+import numpy as np
+import pytest
+
+from conftest import model_path
+
+PENDULUM_NODAMP = (open(model_path("inverted_pendulum")).read().replace('damping="1"', 'damping="0"')
+                   .replace('limited="true"', 'limited="false"'))
+
+
+def _energy(om, d, lib):
+    """E = 1/2 qdot' M qdot + sum_b m_b g z_com,b using the oracle's own M and xipos"""
+    nv = om.nv
+    M = np.ctypeslib.as_array(lib.ora_d_field(d.d, 9), shape=(nv * nv,)).reshape(nv, nv).copy()
+    qd = d.arr("qvel").copy()
+    return 0.5 * qd @ M @ qd
+
+
+def test_pendulum_energy_conservation(ia, ora):
+    """undamped, unactuated cart-pole under RK4: kinetic + potential energy is conserved"""
+    m = ia.Model.from_string(PENDULUM_NODAMP)
+    om = ora.OModel(m.blob())
+    blob_mass = None
+    d = om.make_data()
+    d.arr("qpos")[:] = [0.0, 2.5]  # pole hanging near the bottom, swings freely (limits removed)
+    L = om.lib.L
+    # pole COM height: body 2 inertial frame; use the xpos/xipos-free formula z = ipos_z rotated
+    from test_model_compile import _fields
+    b = _fields(m.blob())
+    mp = b["body_mass"][2]
+    ipos = b["body_ipos"].reshape(-1, 3)[2]
+
+    def potential():
+        th = d.arr("qpos")[1]
+        # hinge about +y: z' = -x sin + z cos
+        z = -ipos[0] * np.sin(th) + ipos[2] * np.cos(th)
+        return mp * 9.81 * z
+
+    d.forward()
+    E0 = _energy(om, d, L) + potential()
+    for _ in range(50):  # 1 s
+        d.step()
+        d.forward()
+        assert d.nefc() == 0
+    E1 = _energy(om, d, L) + potential()
+    assert abs(E1 - E0) < 1e-6 * max(1.0, abs(E0)), (E0, E1)
+
+
+def test_pendulum_gravity_torque(ia, ora):
+    """at rest, qacc = M^-1 * generalized gravity from the pole COM offset"""
+    m = ia.Model.from_string(PENDULUM_NODAMP)
+    om = ora.OModel(m.blob())
+    from test_model_compile import _fields
+    b = _fields(m.blob())
+    d = om.make_data()
+    th = 0.2
+    d.arr("qpos")[:] = [0.0, th]
+    d.forward()
+    nv = 2
+    M = np.ctypeslib.as_array(om.lib.L.ora_d_field(d.d, 9), shape=(4,)).reshape(2, 2).copy()
+    mp = b["body_mass"][2]
+    ix, iz = b["body_ipos"].reshape(-1, 3)[2][[0, 2]]
+    # potential V = mp g (-ix sin th + iz cos th); generalized force = -dV/dth on the hinge
+    tau = -mp * 9.81 * (-ix * np.cos(th) - iz * np.sin(th))
+    qacc = np.linalg.solve(M, np.array([0.0, tau]))
+    assert np.allclose(d.arr("qacc"), qacc, rtol=1e-10, atol=1e-12)
+
+
+def test_hopper_settles_on_floor(ia, ora):
+    m = ia.Model.load(model_path("hopper"))
+    om = ora.OModel(m.blob())
+    d = om.make_data()
+    d.step(250)
+    d.forward()
+    assert d.ncon() >= 1 and d.nefc() == 4 * d.ncon()
+    # foot capsule bottom (z 0.1 - r 0.06) rests on the plane: torso dropped ~0.04
+    assert abs(d.arr("qpos")[1] - 1.21) < 5e-3
+    assert np.all(np.isfinite(d.arr("qacc")))
+
+
+def test_limit_constraint_engages(ia, ora):
+    """pendulum pushed past the hinge limit creates a limit row and is pushed back"""
+    m = ia.Model.load(model_path("inverted_pendulum"))
+    om = ora.OModel(m.blob())
+    d = om.make_data()
+    d.arr("qpos")[:] = [0.0, np.pi / 2 + 0.01]
+    d.forward()
+    assert d.nefc() == 1
+    assert d.arr("qacc")[1] < 0  # restoring
+
+
+def _np_riccati(nv, nu, dt, mu, deriv, xprev, xcur, V, v):
+    nx = 2 * nv
+    import ilqg_amd as ia
+    A, B = ia.assemble_AB(deriv, nv, nu, dt)
+    q = deriv[2 * nv * nv + nv * nu: 2 * nv * nv + nv * nu + nx]
+    r = deriv[2 * nv * nv + nv * nu + nx:]
+    V = (V + V.T) / 2
+    Q, R = np.outer(q, q), np.outer(r, r)
+    c = xprev - xcur
+    V = V + mu * np.eye(nx)
+    H = -2 * B.T @ V @ B - 2 * R
+    K = np.linalg.solve(H, 2 * B.T @ V @ A)
+    k = np.linalg.solve(H, B.T @ (v + 2 * V @ c) + r)
+    ABK = A + B @ K
+    Vn = ABK.T @ V @ ABK + Q + K.T @ R @ K
+    vn = 2 * (k @ B.T + c) @ Vn @ ABK + v @ ABK + q + 2 * k @ R @ K
+    return K, k, Vn, vn
+
+
+@pytest.mark.parametrize("nv,nu", [(2, 1), (6, 3), (4, 4)])
+def test_riccati_step_vs_numpy(ora, nv, nu):
+    rng = np.random.default_rng(7 * nv + nu)
+    nx = 2 * nv
+    D = nv * (2 * nv + nu) + 2 * nv + nu
+    dp = ctypes.POINTER(ctypes.c_double)
+    for _ in range(5):
+        deriv = rng.normal(0, 1, D)
+        xp, xc = rng.normal(0, 1, nx), rng.normal(0, 1, nx)
+        G = rng.normal(0, 1, (nx, nx))
+        V0 = G @ G.T + np.eye(nx)
+        v0 = rng.normal(0, 1, nx)
+        K, k, Vn, vn = _np_riccati(nv, nu, 0.01, 1000.0, deriv, xp, xc, V0, v0)
+        Vc = np.asfortranarray(V0).ravel(order="F").copy()
+        vc = v0.copy()
+        Ko, ko = np.zeros(nu * nx), np.zeros(nu)
+        ora.oracle_lib().L.ora_riccati_step(nv, nu, 0.01, 1000.0, *(a.ctypes.data_as(dp) for a in (
+            deriv, xp, xc, Vc, vc, Ko, ko)))
+        assert np.allclose(Ko.reshape(nx, nu).T, K, rtol=1e-9, atol=1e-9)
+        assert np.allclose(ko, k, rtol=1e-9, atol=1e-9)
+        assert np.allclose(Vc.reshape(nx, nx).T, Vn, rtol=1e-9, atol=1e-6)
+        assert np.allclose(vc, vn, rtol=1e-9, atol=1e-6)
+
+
+def test_ldlt_pivoting_restatement(ora):
+    """Eigen-style pivoted LDLT restatement solves indefinite / negative definite systems"""
+    L = ora.oracle_lib().L
+    L.ora_ldlt_factor.argtypes = [ctypes.c_int, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_int)]
+    L.ora_ldlt_solve.argtypes = [ctypes.c_int, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_int),
+                                 ctypes.POINTER(ctypes.c_double)]
+    rng = np.random.default_rng(3)
+    for n in (1, 2, 3, 5, 8):
+        G = rng.normal(0, 1, (n, n))
+        M = -(G @ G.T) - 0.5 * np.eye(n)
+        if n > 2:
+            M[0, 0] = 1e-3  # force pivoting
+        b = rng.normal(0, 1, n)
+        mat = np.asfortranarray(M).ravel(order="F").copy()
+        tr = np.zeros(n, dtype=np.int32)
+        L.ora_ldlt_factor(n, mat.ctypes.data_as(ctypes.POINTER(ctypes.c_double)),
+                          tr.ctypes.data_as(ctypes.POINTER(ctypes.c_int)))
+        x = b.copy()
+        L.ora_ldlt_solve(n, mat.ctypes.data_as(ctypes.POINTER(ctypes.c_double)),
+                         tr.ctypes.data_as(ctypes.POINTER(ctypes.c_int)), x.ctypes.data_as(ctypes.POINTER(ctypes.c_double)))
+        assert np.allclose(M @ x, b, atol=1e-9)
+
+
+def test_iterate_counts_cout_sink(ia, ora):
+    """backwardPass prints 2 lines per step (ilqr.h:146-147) -> counted sink"""
+    m = ia.Model.load(model_path("inverted_pendulum"))
+    om = ora.OModel(m.blob())
+    d = om.make_data()
+    d.step(10)
+    il = ora.OILQR(om, d, 20)
+    il.set_dinit(d)
+    il.iterate()
+    assert il.arrays()["cout_lines"] == 40
