@@ -5,6 +5,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -55,6 +56,18 @@ struct DevBuf {
   T* as() const { return static_cast<T*>(p); }
 };
 
+// kernel family: cooperative (one wavefront per evaluation, LDS workspace,
+// default) or lane-per-evaluation (ILQG_PATH=lane; kept for A/B comparison)
+bool use_coop() {
+  static int v = -1;
+  if (v < 0) {
+    const char* e = getenv("ILQG_PATH");
+    v = (e && !strcmp(e, "lane")) ? 0 : 1;
+  }
+  return v == 1;
+}
+constexpr size_t kMaxLds = 160 * 1024;
+
 int check_device_support(const HostModel& m, bool solver, std::string& why) {
   for (int j = 0; j < m.njnt; j++)
     if ((m.jnt_type[j] == 0 || m.jnt_type[j] == 1) && m.jnt_stiffness[j] != 0) {
@@ -87,6 +100,10 @@ struct ilqg_model {
   DevBuf buf;
   DevModel dm{};
   WsLayout L{};
+  DevBuf auxbuf;
+  coop::CoopAux X{};
+  coop::CoopLayout C{};
+  int npair = 0;
   hipStream_t stream = nullptr;
 
   int upload(int device) {
@@ -125,6 +142,37 @@ struct ilqg_model {
     dm.maxcon = host.maxcon;
     dm.maxefc = host.maxefc;
     L = make_layout(dm);
+    // cooperative-kernel aux data: dof ancestor matrix and the statically
+    // admissible geom pairs in the oracle's (g1 < g2) enumeration order
+    {
+      const HostModel& h = host;
+      std::vector<int> aux(h.nv * h.nv, 0), pairs;
+      for (int i = 0; i < h.nv; i++)
+        for (int j = i; j >= 0; j = h.dof_parentid[j]) aux[i * h.nv + j] = 1;
+      for (int g1 = 0; g1 < h.ngeom; g1++)
+        for (int g2 = g1 + 1; g2 < h.ngeom; g2++) {
+          int b1 = h.geom_bodyid[g1], b2 = h.geom_bodyid[g2];
+          int w1 = h.body_weldid[b1], w2 = h.body_weldid[b2];
+          int wp1 = h.body_weldid[h.body_parentid[w1]], wp2 = h.body_weldid[h.body_parentid[w2]];
+          if (w1 == w2) continue;
+          if (w1 != 0 && w2 != 0 && (w1 == wp2 || w2 == wp1)) continue;
+          if (!((h.geom_contype[g1] & h.geom_conaffinity[g2]) || (h.geom_contype[g2] & h.geom_conaffinity[g1])))
+            continue;
+          pairs.push_back(g1);
+          pairs.push_back(g2);
+        }
+      npair = (int)pairs.size() / 2;
+      size_t na = aux.size(), np = pairs.size();
+      std::vector<int> all(na + np + 2, 0);
+      std::copy(aux.begin(), aux.end(), all.begin());
+      std::copy(pairs.begin(), pairs.end(), all.begin() + na);
+      HIPCHK(auxbuf.alloc(all.size() * 4));
+      HIPCHK(hipMemcpy(auxbuf.p, all.data(), all.size() * 4, hipMemcpyHostToDevice));
+      X.isanc = auxbuf.as<int>();
+      X.pair = auxbuf.as<int>() + na;
+      X.npair = npair;
+      C = coop::make_coop_layout(dm, npair);
+    }
     if (!stream) HIPCHK(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
     dev = device;
     return ILQG_OK;
@@ -386,10 +434,17 @@ int ilqg_fd_batch(const ilqg_model* mc, int n, const double* qpos, const double*
              c + 3 * nq + 3 * nv, c + 3 * nq + 3 * nv + nu, c + 3 * nq + 3 * nv + 2 * nu};
   TrajDev st{s.time.as<double>(), s.qpos.as<double>(), s.qvel.as<double>(), s.warm.as<double>(), s.ctrl.as<double>()};
   WsDev ws{s.wsd.as<double>(), s.wsi.as<int>(), lanes};
-  HIPCHK(launch_fd_centre(m->dm, m->L, ws, st, n, 1, s.qa.as<double>(), s.xf.as<double>(), cd,
-                          s.warm_c.as<double>(), s.cost_c.as<double>(), m->stream));
-  HIPCHK(launch_fd_cols(m->dm, m->L, ws, st, n, 1, s.qa.as<double>(), s.xf.as<double>(), cd, s.warm_c.as<double>(),
-                        s.cost_c.as<double>(), s.out.as<double>(), m->stream));
+  if (use_coop() && coop_lds_bytes(m->L, m->C) <= kMaxLds) {
+    HIPCHK(launch_fd_centre_coop(m->dm, m->L, m->C, m->X, st, n, 1, s.qa.as<double>(), s.xf.as<double>(), cd,
+                                 s.warm_c.as<double>(), s.cost_c.as<double>(), m->stream));
+    HIPCHK(launch_fd_cols_coop(m->dm, m->L, m->C, m->X, st, n, 1, s.qa.as<double>(), s.xf.as<double>(), cd,
+                               s.warm_c.as<double>(), s.cost_c.as<double>(), s.out.as<double>(), m->stream));
+  } else {
+    HIPCHK(launch_fd_centre(m->dm, m->L, ws, st, n, 1, s.qa.as<double>(), s.xf.as<double>(), cd,
+                            s.warm_c.as<double>(), s.cost_c.as<double>(), m->stream));
+    HIPCHK(launch_fd_cols(m->dm, m->L, ws, st, n, 1, s.qa.as<double>(), s.xf.as<double>(), cd,
+                          s.warm_c.as<double>(), s.cost_c.as<double>(), s.out.as<double>(), m->stream));
+  }
   HIPCHK(hipStreamSynchronize(m->stream));
   HIPCHK(hipMemcpy(deriv, s.out.p, (size_t)n * D * 8, hipMemcpyDeviceToHost));
   return ILQG_OK;
@@ -571,6 +626,11 @@ int ilqg_forward(ilqg_solver* s) {
   const bool multi = s->A > 1;
   TrajDev outv = multi ? s->tview(s->cand) : nom;
   HIPCHK(s->timed(0, [&] {
+    if (use_coop() && coop_lds_bytes(m->L, m->C) <= kMaxLds)
+      return launch_rollout_coop(m->dm, m->L, m->C, m->X, s->S, s->A, s->P, nom, outv, multi ? 1 : 0,
+                                 s->K.as<double>(), s->k.as<double>(), s->alphas.as<double>(), di,
+                                 s->qfrc_applied.as<double>(), s->xfrc_applied.as<double>(), 0, s->cview(),
+                                 s->cost_cand.as<double>(), s->stream);
     return launch_rollout(m->dm, m->L, s->ws(), s->S, s->A, s->P, nom, outv, multi ? 1 : 0, s->K.as<double>(),
                           s->k.as<double>(), s->alphas.as<double>(), di, s->qfrc_applied.as<double>(),
                           s->xfrc_applied.as<double>(), 0, s->cview(), s->cost_cand.as<double>(), s->stream);
@@ -588,11 +648,19 @@ int ilqg_fd_sweep(ilqg_solver* s) {
   TrajDev nom = s->tview(s->traj);
   const int npts = s->S * s->P;
   HIPCHK(s->timed(2, [&] {
+    if (use_coop() && coop_lds_bytes(m->L, m->C) <= kMaxLds)
+      return launch_fd_centre_coop(m->dm, m->L, m->C, m->X, nom, npts, s->P, s->qfrc_applied.as<double>(),
+                                   s->xfrc_applied.as<double>(), s->cview(), s->warm_c.as<double>(),
+                                   s->cost_c.as<double>(), s->stream);
     return launch_fd_centre(m->dm, m->L, s->ws(), nom, npts, s->P, s->qfrc_applied.as<double>(),
                             s->xfrc_applied.as<double>(), s->cview(), s->warm_c.as<double>(),
                             s->cost_c.as<double>(), s->stream);
   }));
   HIPCHK(s->timed(3, [&] {
+    if (use_coop() && coop_lds_bytes(m->L, m->C) <= kMaxLds)
+      return launch_fd_cols_coop(m->dm, m->L, m->C, m->X, nom, npts, s->P, s->qfrc_applied.as<double>(),
+                                 s->xfrc_applied.as<double>(), s->cview(), s->warm_c.as<double>(),
+                                 s->cost_c.as<double>(), s->deriv.as<double>(), s->stream);
     return launch_fd_cols(m->dm, m->L, s->ws(), nom, npts, s->P, s->qfrc_applied.as<double>(),
                           s->xfrc_applied.as<double>(), s->cview(), s->warm_c.as<double>(), s->cost_c.as<double>(),
                           s->deriv.as<double>(), s->stream);

@@ -1,0 +1,1188 @@
+// Cooperative device physics: ONE WAVEFRONT PER EVALUATION, workspace in LDS.
+//
+// The same MuJoCo-2.0 pipeline as dphys.h (and oracle/mjsub.c), re-mapped for
+// latency: the 64 lanes of a workgroup split every stage over its independent
+// outputs -- bodies, joints, dofs, geom pairs, constraint rows, matrix entries
+// -- while each scalar is still produced by exactly one lane with the oracle's
+// expression and summation order, so results stay bit-identical.  Inherently
+// serial recursions (kinematic chain, com velocities, triangular solves,
+// ordered reductions) run on lane 0 out of LDS.  All control flow that
+// reaches a barrier is uniform across the workgroup (broadcast through LDS).
+#pragma once
+
+#include "dphys.h"
+
+namespace ilqg {
+namespace coop {
+
+using namespace dev;
+
+struct Team {
+  double* w;   // WsLayout doubles (stride 1)
+  int* iw;     // WsLayout ints
+  double* c;   // CoopLayout doubles
+  int* ci;     // CoopLayout ints
+  int tid, nt;
+};
+
+#define TSYNC() __syncthreads()
+#define FOR_T(v, n) for (int v = T.tid; v < (n); v += T.nt)
+
+__device__ __forceinline__ double tdot(const double* a, const double* b, int n) {
+  double r = 0;
+  for (int i = 0; i < n; i++) r += a[i] * b[i];
+  return r;
+}
+
+// ------------------------------------------------------ position stage ---
+__device__ inline void kinematics(const DevModel& m, const WsLayout& L, const CoopLayout& C, const Team& T) {
+  double* qpos = T.w + L.qpos;
+  double* xpos = T.w + L.xpos;
+  double* xquat = T.w + L.xquat;
+  double* xmat = T.w + L.xmat;
+  double* xipos = T.w + L.xipos;
+  double* ximat = T.w + L.ximat;
+  double* xanchor = T.w + L.xanchor;
+  double* xaxis = T.w + L.xaxis;
+  double* qloc = T.c + C.qloc;
+  // joint-local rotations depend on qpos only: all joints at once
+  FOR_T(j, m.njnt) {
+    int type = m.jnt_type[j], qadr = m.jnt_qposadr[j];
+    double q[4], ja[3];
+    if (type == JNT_HINGE) {
+      ldm<3>(ja, m.jnt_axis + 3 * j);
+      axis_angle2quat(q, ja, qpos[qadr] - m.qpos0[qadr]);
+      for (int k = 0; k < 4; k++) qloc[4 * j + k] = q[k];
+    } else if (type == JNT_BALL) {
+      q[0] = qpos[qadr]; q[1] = qpos[qadr + 1]; q[2] = qpos[qadr + 2]; q[3] = qpos[qadr + 3];
+      normalize4(q);
+      for (int k = 0; k < 4; k++) qloc[4 * j + k] = q[k];
+    }
+  }
+  TSYNC();
+  // the kinematic chain: lane 0
+  if (T.tid == 0) {
+    xpos[0] = xpos[1] = xpos[2] = 0;
+    xquat[0] = 1; xquat[1] = xquat[2] = xquat[3] = 0;
+    for (int i = 1; i < m.nbody; i++) {
+      int pid = m.body_parentid[i];
+      double xp[3], xq[4], tmp[3], pq[4], bp[3], bq[4];
+      ldm<4>(pq, xquat + 4 * pid);
+      ldm<3>(bp, m.body_pos + 3 * i);
+      ldm<4>(bq, m.body_quat + 4 * i);
+      rot_vec_quat(tmp, bp, pq);
+      xp[0] = xpos[3 * pid] + tmp[0];
+      xp[1] = xpos[3 * pid + 1] + tmp[1];
+      xp[2] = xpos[3 * pid + 2] + tmp[2];
+      quat_mul(xq, pq, bq);
+      for (int j = 0; j < m.body_jntnum[i]; j++) {
+        int jid = m.body_jntadr[i] + j;
+        int qadr = m.jnt_qposadr[jid];
+        int type = m.jnt_type[jid];
+        double anc[3], ax[3], jp[3], ja[3];
+        ldm<3>(jp, m.jnt_pos + 3 * jid);
+        ldm<3>(ja, m.jnt_axis + 3 * jid);
+        if (type == JNT_FREE) {
+          xp[0] = qpos[qadr]; xp[1] = qpos[qadr + 1]; xp[2] = qpos[qadr + 2];
+          xq[0] = qpos[qadr + 3]; xq[1] = qpos[qadr + 4]; xq[2] = qpos[qadr + 5]; xq[3] = qpos[qadr + 6];
+          normalize4(xq);
+          for (int k = 0; k < 3; k++) { xanchor[3 * jid + k] = xp[k]; xaxis[3 * jid + k] = ja[k]; }
+          continue;
+        }
+        rot_vec_quat(anc, jp, xq);
+        anc[0] += xp[0]; anc[1] += xp[1]; anc[2] += xp[2];
+        rot_vec_quat(ax, ja, xq);
+        if (type == JNT_SLIDE) {
+          double dq = qpos[qadr] - m.qpos0[qadr];
+          xp[0] += ax[0] * dq; xp[1] += ax[1] * dq; xp[2] += ax[2] * dq;
+        } else {
+          double ql[4];
+          ldm<4>(ql, qloc + 4 * jid);
+          quat_mul(xq, xq, ql);
+          rot_vec_quat(tmp, jp, xq);
+          xp[0] = anc[0] - tmp[0];
+          xp[1] = anc[1] - tmp[1];
+          xp[2] = anc[2] - tmp[2];
+        }
+        for (int k = 0; k < 3; k++) { xanchor[3 * jid + k] = anc[k]; xaxis[3 * jid + k] = ax[k]; }
+      }
+      normalize4(xq);
+      for (int k = 0; k < 3; k++) xpos[3 * i + k] = xp[k];
+      for (int k = 0; k < 4; k++) xquat[4 * i + k] = xq[k];
+    }
+  }
+  TSYNC();
+  // body frames and inertial frames: one lane per body
+  FOR_T(i, m.nbody) {
+    double xq[4], mat[9], tmp[3], ip[3], iq[4], q2[4];
+    ldm<4>(xq, xquat + 4 * i);
+    quat2mat(mat, xq);
+    for (int k = 0; k < 9; k++) xmat[9 * i + k] = mat[k];
+    if (i == 0) {
+      xipos[0] = xipos[1] = xipos[2] = 0;
+      for (int k = 0; k < 9; k++) ximat[k] = mat[k];
+    } else {
+      ldm<3>(ip, m.body_ipos + 3 * i);
+      ldm<4>(iq, m.body_iquat + 4 * i);
+      rot_vec_mat(tmp, ip, mat);
+      xipos[3 * i] = tmp[0] + xpos[3 * i];
+      xipos[3 * i + 1] = tmp[1] + xpos[3 * i + 1];
+      xipos[3 * i + 2] = tmp[2] + xpos[3 * i + 2];
+      quat_mul(q2, xq, iq);
+      quat2mat(mat, q2);
+      for (int k = 0; k < 9; k++) ximat[9 * i + k] = mat[k];
+    }
+  }
+  TSYNC();
+  double* gxpos = T.w + L.gxpos;
+  double* gxmat = T.w + L.gxmat;
+  FOR_T(g, m.ngeom) {
+    int b = m.geom_bodyid[g];
+    double tmp[3], q[4], bm[9], bq[4], gp[3], gq[4], mat[9];
+    ldm<9>(bm, xmat + 9 * b);
+    ldm<4>(bq, xquat + 4 * b);
+    ldm<3>(gp, m.geom_pos + 3 * g);
+    ldm<4>(gq, m.geom_quat + 4 * g);
+    rot_vec_mat(tmp, gp, bm);
+    gxpos[3 * g] = tmp[0] + xpos[3 * b];
+    gxpos[3 * g + 1] = tmp[1] + xpos[3 * b + 1];
+    gxpos[3 * g + 2] = tmp[2] + xpos[3 * b + 2];
+    quat_mul(q, bq, gq);
+    quat2mat(mat, q);
+    for (int k = 0; k < 9; k++) gxmat[9 * g + k] = mat[k];
+  }
+  TSYNC();
+}
+
+__device__ inline void com_pos(const DevModel& m, const WsLayout& L, const Team& T) {
+  const int nb = m.nbody;
+  double* xipos = T.w + L.xipos;
+  double* scom = T.w + L.scom;
+  double* cinert = T.w + L.cinert;
+  double* ximat = T.w + L.ximat;
+  double* cdof = T.w + L.cdof;
+  double* xanchor = T.w + L.xanchor;
+  double* xaxis = T.w + L.xaxis;
+  double* xmat = T.w + L.xmat;
+  FOR_T(i, nb) {
+    double ms = m.body_mass[i];
+    scom[3 * i] = xipos[3 * i] * ms;
+    scom[3 * i + 1] = xipos[3 * i + 1] * ms;
+    scom[3 * i + 2] = xipos[3 * i + 2] * ms;
+  }
+  TSYNC();
+  FOR_T(k, 3) {
+    for (int i = nb - 1; i > 0; i--) scom[3 * m.body_parentid[i] + k] += scom[3 * i + k];
+  }
+  TSYNC();
+  FOR_T(i, nb) {
+    if (m.body_subtreemass[i] < MINVAL) {
+      scom[3 * i] = xipos[3 * i];
+      scom[3 * i + 1] = xipos[3 * i + 1];
+      scom[3 * i + 2] = xipos[3 * i + 2];
+    } else {
+      double inv = 1 / m.body_subtreemass[i];
+      scom[3 * i] *= inv;
+      scom[3 * i + 1] *= inv;
+      scom[3 * i + 2] *= inv;
+    }
+  }
+  TSYNC();
+  FOR_T(i, nb) {
+    if (i == 0) {
+      for (int k = 0; k < 10; k++) cinert[k] = 0;
+    } else {
+      double off[3], mat[9], in[3], res[10];
+      const double* rc = scom + 3 * m.body_rootid[i];
+      off[0] = xipos[3 * i] - rc[0];
+      off[1] = xipos[3 * i + 1] - rc[1];
+      off[2] = xipos[3 * i + 2] - rc[2];
+      ldm<9>(mat, ximat + 9 * i);
+      ldm<3>(in, m.body_inertia + 3 * i);
+      inert_com(res, in, mat, off, m.body_mass[i]);
+      for (int k = 0; k < 10; k++) cinert[10 * i + k] = res[k];
+    }
+  }
+  FOR_T(j, m.njnt) {
+    int da = 6 * m.jnt_dofadr[j];
+    int bi = m.jnt_bodyid[j];
+    const double* rc = scom + 3 * m.body_rootid[bi];
+    double off[3] = {rc[0] - xanchor[3 * j], rc[1] - xanchor[3 * j + 1], rc[2] - xanchor[3 * j + 2]};
+    double out[6];
+    int type = m.jnt_type[j];
+    int skip = 0;
+    if (type == JNT_FREE) {
+      for (int k = 0; k < 18; k++) cdof[da + k] = 0;
+      for (int i = 0; i < 3; i++) cdof[da + 3 + 7 * i] = 1;
+      skip = 18;
+    }
+    if (type == JNT_FREE || type == JNT_BALL) {
+      for (int i = 0; i < 3; i++) {
+        double axis[3] = {xmat[9 * bi + i], xmat[9 * bi + i + 3], xmat[9 * bi + i + 6]};
+        out[0] = axis[0]; out[1] = axis[1]; out[2] = axis[2];
+        cross3(out + 3, axis, off);
+        for (int k = 0; k < 6; k++) cdof[da + skip + 6 * i + k] = out[k];
+      }
+    } else if (type == JNT_SLIDE) {
+      out[0] = out[1] = out[2] = 0;
+      out[3] = xaxis[3 * j]; out[4] = xaxis[3 * j + 1]; out[5] = xaxis[3 * j + 2];
+      for (int k = 0; k < 6; k++) cdof[da + k] = out[k];
+    } else {
+      double ax[3] = {xaxis[3 * j], xaxis[3 * j + 1], xaxis[3 * j + 2]};
+      out[0] = ax[0]; out[1] = ax[1]; out[2] = ax[2];
+      cross3(out + 3, ax, off);
+      for (int k = 0; k < 6; k++) cdof[da + k] = out[k];
+    }
+  }
+  TSYNC();
+}
+
+__device__ inline void crb(const DevModel& m, const WsLayout& L, const CoopLayout& C, const CoopAux& X,
+                           const Team& T) {
+  const int nv = m.nv, nb = m.nbody;
+  double* crbv = T.w + L.crb;
+  double* cinert = T.w + L.cinert;
+  double* qM = T.w + L.qM;
+  double* cdof = T.w + L.cdof;
+  double* buf = T.c + C.buf6;
+  FOR_T(e, 10 * nb) crbv[e] = cinert[e];
+  TSYNC();
+  FOR_T(k, 10) {
+    for (int i = nb - 1; i > 0; i--) {
+      int p = m.body_parentid[i];
+      if (p > 0) crbv[10 * p + k] += crbv[10 * i + k];
+    }
+  }
+  TSYNC();
+  FOR_T(i, nv) {
+    double ci[10], cd[6], r[6];
+    ldm<10>(ci, crbv + 10 * m.dof_bodyid[i]);
+    ldm<6>(cd, cdof + 6 * i);
+    mul_inert_vec(r, ci, cd);
+    for (int k = 0; k < 6; k++) buf[6 * i + k] = r[k];
+  }
+  TSYNC();
+  FOR_T(e, nv * nv) {
+    int i = e / nv, j = e % nv;
+    if (j <= i) {
+      double v = (i == j) ? m.dof_armature[i] : 0.0;
+      if (X.isanc[e]) v += tdot(cdof + 6 * j, buf + 6 * i, 6);
+      qM[e] = v;
+      qM[j * nv + i] = v;
+    }
+  }
+  TSYNC();
+}
+
+// tree L'DL (oracle factor_ld), parallel over ancestor pairs for each k
+__device__ inline void factor_ld(const DevModel& m, const CoopAux& X, const Team& T, const double* mat, double* LD,
+                                 double* diaginv, double* tmpv) {
+  const int nv = m.nv;
+  FOR_T(e, nv * nv) {
+    int i = e / nv, j = e % nv;
+    LD[e] = (j <= i) ? mat[e] : 0;
+  }
+  TSYNC();
+  for (int k = nv - 1; k >= 0; k--) {
+    if (T.tid == 0 && LD[k * nv + k] < MINVAL) LD[k * nv + k] = MINVAL;
+    TSYNC();
+    FOR_T(i, nv) {
+      if (i != k && X.isanc[k * nv + i]) tmpv[i] = LD[k * nv + i] / LD[k * nv + k];
+    }
+    TSYNC();
+    FOR_T(e, nv * nv) {
+      int i = e / nv, j = e % nv;
+      if (i != k && X.isanc[k * nv + i] && X.isanc[i * nv + j]) LD[e] -= tmpv[i] * LD[k * nv + j];
+    }
+    TSYNC();
+    FOR_T(i, nv) {
+      if (i != k && X.isanc[k * nv + i]) LD[k * nv + i] = tmpv[i];
+    }
+    TSYNC();
+  }
+  FOR_T(i, nv) diaginv[i] = 1 / LD[i * nv + i];
+  TSYNC();
+}
+
+// oracle solve_ld on lane 0 (ends with a barrier)
+__device__ inline void solve_ld(const DevModel& m, const Team& T, const double* LD, const double* diaginv, double* x) {
+  const int nv = m.nv;
+  if (T.tid == 0) {
+    for (int i = nv - 1; i >= 0; i--) {
+      double tmp = x[i];
+      if (tmp != 0)
+        for (int j = m.dof_parentid[i]; j >= 0; j = m.dof_parentid[j]) x[j] -= LD[i * nv + j] * tmp;
+    }
+    for (int i = 0; i < nv; i++) x[i] *= diaginv[i];
+    for (int i = 0; i < nv; i++)
+      for (int j = m.dof_parentid[i]; j >= 0; j = m.dof_parentid[j]) x[i] -= LD[i * nv + j] * x[j];
+  }
+  TSYNC();
+}
+
+__device__ inline void jac_col(const DevModel& m, const CoopAux& X, const double* scom, const double* cdof,
+                               const double* point, int body, int k, double* out3) {
+  // one dof column of jac_point (oracle): zero unless dof k lies on the chain of `body`
+  const int nv = m.nv;
+  out3[0] = out3[1] = out3[2] = 0;
+  const double* rc = scom + 3 * m.body_rootid[body];
+  double off[3] = {point[0] - rc[0], point[1] - rc[1], point[2] - rc[2]};
+  while (body && !m.body_dofnum[body]) body = m.body_parentid[body];
+  if (!body) return;
+  int last = m.body_dofadr[body] + m.body_dofnum[body] - 1;
+  if (!X.isanc[last * nv + k]) return;
+  double tmp[3], cd[6];
+  ldm<6>(cd, cdof + 6 * k);
+  cross3(tmp, cd, off);
+  out3[0] = cd[3] + tmp[0];
+  out3[1] = cd[4] + tmp[1];
+  out3[2] = cd[5] + tmp[2];
+}
+
+__device__ inline void collision(const DevModel& m, const WsLayout& L, const CoopLayout& C, const CoopAux& X,
+                                 const Team& T) {
+  double* gxpos = T.w + L.gxpos;
+  double* gxmat = T.w + L.gxmat;
+  double* con = T.w + L.con;
+  int* coni = T.iw + L.coni;
+  double* pcon = T.c + C.pcon;
+  int* pcnt = T.ci + C.pcnt;
+  FOR_T(p, X.npair) {
+    int g1 = X.pair[2 * p], g2 = X.pair[2 * p + 1];
+    int n = 0;
+    double margin = maxd(m.geom_margin[g1], m.geom_margin[g2]);
+    bool ok = true;
+    if (m.geom_rbound[g1] > 0 && m.geom_rbound[g2] > 0) {
+      double dd[3] = {gxpos[3 * g1] - gxpos[3 * g2], gxpos[3 * g1 + 1] - gxpos[3 * g2 + 1],
+                      gxpos[3 * g1 + 2] - gxpos[3 * g2 + 2]};
+      if (sqrt(dot3(dd, dd)) > m.geom_rbound[g1] + m.geom_rbound[g2] + margin) ok = false;
+    }
+    if (ok) {
+      int ga = g1, gb = g2;
+      if (m.geom_type[g1] > m.geom_type[g2]) { ga = g2; gb = g1; }
+      double pos1[3], mat1[9], sz1[3], pos2[3], mat2[9], sz2[3];
+      ldm<3>(pos1, gxpos + 3 * ga);
+      ldm<9>(mat1, gxmat + 9 * ga);
+      ldm<3>(sz1, m.geom_size + 3 * ga);
+      ldm<3>(pos2, gxpos + 3 * gb);
+      ldm<9>(mat2, gxmat + 9 * gb);
+      ldm<3>(sz2, m.geom_size + 3 * gb);
+      RCon tmp[2];
+      n = narrow(m, m.geom_type[ga], m.geom_type[gb], pos1, mat1, sz1, pos2, mat2, sz2, margin, tmp);
+      for (int k = 0; k < n; k++) {
+        double* pc = pcon + 14 * p + 7 * k;
+        pc[0] = tmp[k].dist;
+        pc[1] = tmp[k].pos[0]; pc[2] = tmp[k].pos[1]; pc[3] = tmp[k].pos[2];
+        pc[4] = tmp[k].n[0]; pc[5] = tmp[k].n[1]; pc[6] = tmp[k].n[2];
+      }
+    }
+    pcnt[p] = n;
+  }
+  TSYNC();
+  // ordered compaction with the oracle's truncation at nconmax
+  if (T.tid == 0) {
+    int ncon = 0;
+    const int lim = m.nconmax < m.maxcon ? m.nconmax : m.maxcon;
+    for (int p = 0; p < X.npair; p++) {
+      int n = pcnt[p];
+      int take = 0;
+      for (int k = 0; k < n; k++)
+        if (ncon + take < lim) take++;
+      pcnt[p] = (ncon << 8) | take;  // offset, count
+      ncon += take;
+    }
+    T.iw[L.ncon] = ncon;
+  }
+  TSYNC();
+  FOR_T(e, 2 * X.npair) {
+    int p = e >> 1, k = e & 1;
+    int off = pcnt[p] >> 8, take = pcnt[p] & 255;
+    if (k < take) {
+      int g1 = X.pair[2 * p], g2 = X.pair[2 * p + 1];
+      int ga = g1, gb = g2;
+      if (m.geom_type[g1] > m.geom_type[g2]) { ga = g2; gb = g1; }
+      double margin = maxd(m.geom_margin[g1], m.geom_margin[g2]);
+      double gap = maxd(m.geom_gap[ga], m.geom_gap[gb]);
+      double s1 = m.geom_solmix[ga], s2 = m.geom_solmix[gb], mix;
+      if (s1 < MINVAL && s2 < MINVAL) mix = 0.5;
+      else if (s1 < MINVAL) mix = 0;
+      else if (s2 < MINVAL) mix = 1;
+      else mix = s1 / (s1 + s2);
+      const double* pc = pcon + 14 * p + 7 * k;
+      double* c = con + CON_ND * (off + k);
+      double fr[9];
+      fr[0] = pc[4]; fr[1] = pc[5]; fr[2] = pc[6];
+      make_frame(fr);
+      c[CON_DIST] = pc[0];
+      c[CON_POS] = pc[1]; c[CON_POS + 1] = pc[2]; c[CON_POS + 2] = pc[3];
+      for (int r = 0; r < 9; r++) c[CON_FRAME + r] = fr[r];
+      c[CON_INCLM] = margin - gap;
+      double f0 = maxd(m.geom_friction[3 * ga], m.geom_friction[3 * gb]);
+      double f1 = maxd(m.geom_friction[3 * ga + 1], m.geom_friction[3 * gb + 1]);
+      double f2 = maxd(m.geom_friction[3 * ga + 2], m.geom_friction[3 * gb + 2]);
+      c[CON_FRIC] = f0; c[CON_FRIC + 1] = f0; c[CON_FRIC + 2] = f1; c[CON_FRIC + 3] = f2; c[CON_FRIC + 4] = f2;
+      for (int r = 0; r < 2; r++)
+        c[CON_SOLREF + r] = mix * m.geom_solref[2 * ga + r] + (1 - mix) * m.geom_solref[2 * gb + r];
+      for (int r = 0; r < 5; r++)
+        c[CON_SOLIMP + r] = mix * m.geom_solimp[5 * ga + r] + (1 - mix) * m.geom_solimp[5 * gb + r];
+      int cd1 = m.geom_condim[ga], cd2 = m.geom_condim[gb];
+      int* ci = coni + CON_NI * (off + k);
+      ci[CONI_DIM] = cd1 > cd2 ? cd1 : cd2;
+      ci[CONI_G1] = ga;
+      ci[CONI_G2] = gb;
+      ci[CONI_EFCADR] = -1;
+    }
+  }
+  TSYNC();
+}
+
+__device__ inline void make_constraint(const DevModel& m, const WsLayout& L, const CoopLayout& C, const CoopAux& X,
+                                       const Team& T) {
+  const int nv = m.nv;
+  double* qpos = T.w + L.qpos;
+  double* con = T.w + L.con;
+  double* efcJ = T.w + L.efc_J;
+  double* efc_pos = T.w + L.efc_pos;
+  double* efc_margin = T.w + L.efc_margin;
+  double* efc_D = T.w + L.efc_D;
+  double* KBIP = T.w + L.efc_KBIP;
+  int* coni = T.iw + L.coni;
+  int* efc_type = T.iw + L.efc_type;
+  int* efc_id = T.iw + L.efc_id;
+  int* rsub = T.ci + C.rsub;
+  int* jcnt = T.ci + C.jcnt;
+  double* jc = T.c + C.jc;
+  double* scom = T.w + L.scom;
+  double* cdof = T.w + L.cdof;
+  const int ncon = T.iw[L.ncon];
+  const int njmax = m.njmax < m.maxefc ? m.njmax : m.maxefc;
+  // which limit sides are violated: bit 0 lower, bit 1 upper
+  FOR_T(j, m.njnt) {
+    int type = m.jnt_type[j], mask = 0;
+    if (m.jnt_limited[j] && (type == JNT_SLIDE || type == JNT_HINGE)) {
+      double value = qpos[m.jnt_qposadr[j]];
+      for (int side = -1; side <= 1; side += 2) {
+        double dist = side * (m.jnt_range[2 * j + (side + 1) / 2] - value);
+        if (dist < m.jnt_margin[j]) mask |= (side < 0 ? 1 : 2);
+      }
+    }
+    jcnt[j] = mask;
+  }
+  // contact jacobians in the contact frame: one lane per (contact, dof)
+  FOR_T(e, ncon * nv) {
+    int c = e / nv, k = e % nv;
+    const double* cc = con + CON_ND * c;
+    int b1 = m.geom_bodyid[coni[CON_NI * c + CONI_G1]], b2 = m.geom_bodyid[coni[CON_NI * c + CONI_G2]];
+    double pos[3] = {cc[CON_POS], cc[CON_POS + 1], cc[CON_POS + 2]}, a[3], b[3];
+    jac_col(m, X, scom, cdof, pos, b1, k, a);
+    jac_col(m, X, scom, cdof, pos, b2, k, b);
+    b[0] -= a[0]; b[1] -= a[1]; b[2] -= a[2];
+    for (int r = 0; r < 3; r++)
+      jc[(c * 3 + r) * nv + k] = cc[CON_FRAME + 3 * r] * b[0] + cc[CON_FRAME + 3 * r + 1] * b[1] +
+                                 cc[CON_FRAME + 3 * r + 2] * b[2];
+  }
+  TSYNC();
+  // row allocation in the oracle's order (limits, then contacts), lane 0
+  if (T.tid == 0) {
+    int nefc = 0;
+    for (int j = 0; j < m.njnt; j++) {
+      int mask = jcnt[j];
+      for (int side = -1; side <= 1; side += 2) {
+        if (!(mask & (side < 0 ? 1 : 2))) continue;
+        if (nefc + 1 > njmax) break;
+        efc_type[nefc] = C_LIMIT;
+        efc_id[nefc] = j;
+        rsub[nefc] = side;
+        nefc++;
+      }
+    }
+    for (int c = 0; c < ncon; c++) {
+      int dim = coni[CON_NI * c + CONI_DIM];
+      int nrow = dim == 1 ? 1 : 2 * (dim - 1);
+      if (nefc + nrow > njmax) continue;
+      coni[CON_NI * c + CONI_EFCADR] = nefc;
+      for (int r = 0; r < nrow; r++) {
+        efc_type[nefc] = dim == 1 ? C_FRICTIONLESS : C_PYRAMIDAL;
+        efc_id[nefc] = c;
+        rsub[nefc] = r;
+        nefc++;
+      }
+    }
+    T.iw[L.nefc] = nefc;
+  }
+  TSYNC();
+  const int nefc = T.iw[L.nefc];
+  FOR_T(e, nefc * nv) {
+    int i = e / nv, k = e % nv;
+    int type = efc_type[i], id = efc_id[i], sub = rsub[i];
+    double v;
+    if (type == C_LIMIT) {
+      v = (k == m.jnt_dofadr[id]) ? (double)(-sub) : 0.0;
+    } else if (type == C_FRICTIONLESS) {
+      v = jc[(id * 3 + 0) * nv + k];
+    } else {
+      int kk = sub / 2 + 1;
+      double f = con[CON_ND * id + CON_FRIC + kk - 1];
+      double j0 = jc[(id * 3 + 0) * nv + k], jk = jc[(id * 3 + kk) * nv + k];
+      v = (sub & 1) ? j0 + (-f) * jk : j0 + f * jk;
+    }
+    efcJ[i * nv + k] = v;
+  }
+  FOR_T(i, nefc) {
+    int type = efc_type[i], id = efc_id[i];
+    double solref[2], solimp[5], dA, imp, tc, dr, dmax, K, B, pos, mar;
+    if (type == C_LIMIT) {
+      double value = qpos[m.jnt_qposadr[id]];
+      int side = rsub[i];
+      pos = side * (m.jnt_range[2 * id + (side + 1) / 2] - value);
+      mar = m.jnt_margin[id];
+      ldm<2>(solref, m.jnt_solref + 2 * id);
+      ldm<5>(solimp, m.jnt_solimp + 5 * id);
+      dA = m.dof_invweight0[m.jnt_dofadr[id]];
+    } else {
+      const double* cc = con + CON_ND * id;
+      int b1 = m.geom_bodyid[coni[CON_NI * id + CONI_G1]], b2 = m.geom_bodyid[coni[CON_NI * id + CONI_G2]];
+      double tran = m.body_invweight0[2 * b1] + m.body_invweight0[2 * b2];
+      pos = cc[CON_DIST];
+      mar = cc[CON_INCLM];
+      ldm<2>(solref, cc + CON_SOLREF);
+      ldm<5>(solimp, cc + CON_SOLIMP);
+      if (type == C_FRICTIONLESS) {
+        dA = tran;
+      } else {
+        int k = (i - coni[CON_NI * id + CONI_EFCADR]) / 2;
+        double f = cc[CON_FRIC + k];
+        dA = tran + f * f * tran;
+      }
+    }
+    efc_pos[i] = pos;
+    efc_margin[i] = mar;
+    imp = get_impedance(solimp, pos, mar);
+    dmax = clipd(solimp[1], MINIMP, MAXIMP);
+    tc = solref[0];
+    dr = solref[1];
+    if (tc > 0) {
+      if (tc < 2 * m.opt_timestep) tc = 2 * m.opt_timestep;
+      K = 1 / (dmax * dmax * tc * tc * dr * dr);
+      B = 2 / (dmax * tc);
+    } else {
+      K = -tc / (dmax * dmax);
+      B = -dr / dmax;
+    }
+    KBIP[4 * i] = K;
+    KBIP[4 * i + 1] = B;
+    KBIP[4 * i + 2] = imp;
+    KBIP[4 * i + 3] = 0;
+    double R = maxd(MINVAL, (1 - imp) * dA / imp);
+    efc_D[i] = 1 / R;
+  }
+  TSYNC();
+}
+
+__device__ inline void fwd_position(const DevModel& m, const WsLayout& L, const CoopLayout& C, const CoopAux& X,
+                                    const Team& T) {
+  kinematics(m, L, C, T);
+  com_pos(m, L, T);
+  // transmission: actuator_moment
+  double* amom = T.w + L.amom;
+  FOR_T(e, m.nu * m.nv) {
+    int i = e / m.nv, k = e % m.nv;
+    int j = m.actuator_trnid[i];
+    amom[e] = (k == m.jnt_dofadr[j]) ? m.actuator_gear[i] : 0.0;
+  }
+  crb(m, L, C, X, T);
+  factor_ld(m, X, T, T.w + L.qM, T.w + L.qLD, T.w + L.qLDinv, T.c + C.ftmp);
+  collision(m, L, C, X, T);
+  make_constraint(m, L, C, X, T);
+}
+
+// ------------------------------------------------------ velocity stage ---
+__device__ inline void fwd_velocity(const DevModel& m, const WsLayout& L, const CoopLayout& C, const Team& T) {
+  const int nv = m.nv, nb = m.nbody;
+  double* cvelw = T.w + L.cvel;
+  double* cdof = T.w + L.cdof;
+  double* cdd = T.w + L.cdof_dot;
+  double* qvel = T.w + L.qvel;
+  double* qpos = T.w + L.qpos;
+  // com velocities (serial tree recursion): lane 0
+  if (T.tid == 0) {
+    for (int k = 0; k < 6; k++) cvelw[k] = 0;
+    for (int i = 1; i < nb; i++) {
+      int bda = m.body_dofadr[i];
+      double cvel[6], tmp[6], cd[6], r[6];
+      ldm<6>(cvel, cvelw + 6 * m.body_parentid[i]);
+      for (int j = 0; j < m.body_dofnum[i]; j++) {
+        int type = m.jnt_type[m.dof_jntid[bda + j]];
+        if (type == JNT_FREE) {
+          for (int k = 0; k < 18; k++) cdd[6 * (bda + j) + k] = 0;
+          for (int k = 0; k < 6; k++) {
+            double s = 0;
+            for (int q = 0; q < 3; q++) s += cdof[6 * (bda + q) + k] * qvel[bda + q];
+            tmp[k] = s;
+          }
+          for (int k = 0; k < 6; k++) cvel[k] += tmp[k];
+          j += 3;
+        }
+        if (type == JNT_FREE || type == JNT_BALL) {
+          for (int k = 0; k < 3; k++) {
+            ldm<6>(cd, cdof + 6 * (bda + j + k));
+            cross_motion(r, cvel, cd);
+            for (int q = 0; q < 6; q++) cdd[6 * (bda + j + k) + q] = r[q];
+          }
+          for (int k = 0; k < 6; k++) {
+            double s = 0;
+            for (int q = 0; q < 3; q++) s += cdof[6 * (bda + j + q) + k] * qvel[bda + j + q];
+            tmp[k] = s;
+          }
+          for (int k = 0; k < 6; k++) cvel[k] += tmp[k];
+          j += 2;
+        } else {
+          ldm<6>(cd, cdof + 6 * (bda + j));
+          cross_motion(r, cvel, cd);
+          for (int q = 0; q < 6; q++) cdd[6 * (bda + j) + q] = r[q];
+          double qv = qvel[bda + j];
+          for (int k = 0; k < 6; k++) {
+            double s = 0;
+            s += cd[k] * qv;
+            tmp[k] = s;
+          }
+          for (int k = 0; k < 6; k++) cvel[k] += tmp[k];
+        }
+      }
+      for (int k = 0; k < 6; k++) cvelw[6 * i + k] = cvel[k];
+    }
+  }
+  // passive forces: one lane per dof (hinge/slide springs; ball/free rejected on the host)
+  double* qp = T.w + L.qfrc_passive;
+  FOR_T(i, nv) {
+    int j = m.dof_jntid[i];
+    double v = 0;
+    double k = m.jnt_stiffness[j];
+    if (k != 0) {
+      int pa = m.jnt_qposadr[j];
+      v = -k * (qpos[pa] - m.qpos_spring[pa]);
+    }
+    v -= m.dof_damping[i] * qvel[i];
+    qp[i] = v;
+  }
+  // constraint velocities and reference accelerations: one lane per row
+  const int nefc = T.iw[L.nefc];
+  double* KBIP = T.w + L.efc_KBIP;
+  double* efc_vel = T.w + L.efc_vel;
+  double* aref = T.w + L.efc_aref;
+  double* J = T.w + L.efc_J;
+  double* pos = T.w + L.efc_pos;
+  double* mar = T.w + L.efc_margin;
+  FOR_T(i, nefc) {
+    double k0 = KBIP[4 * i], k1 = KBIP[4 * i + 1], k2 = KBIP[4 * i + 2];
+    double v = tdot(J + i * nv, qvel, nv);
+    efc_vel[i] = v;
+    aref[i] = -k1 * v - k0 * k2 * (pos[i] - mar[i]);
+  }
+  TSYNC();
+  // RNE: per (body, component) dof-velocity terms, then the chain per component
+  double* rt = T.c + C.rtmp;
+  double* cacc = T.w + L.s_rne;
+  double* cfrc = cacc + 6 * nb;
+  FOR_T(e, 6 * nb) {
+    int i = e / 6, k = e % 6;
+    if (i > 0) {
+      int bda = m.body_dofadr[i], nd = m.body_dofnum[i];
+      double sum = 0;
+      for (int j = 0; j < nd; j++) sum += cdd[6 * (bda + j) + k] * qvel[bda + j];
+      rt[e] = nd ? sum : 0;
+    }
+  }
+  TSYNC();
+  FOR_T(k, 6) {
+    cacc[k] = k < 3 ? 0.0 : (k == 3 ? -m.opt_gravity0 : (k == 4 ? -m.opt_gravity1 : -m.opt_gravity2));
+    for (int i = 1; i < nb; i++) cacc[6 * i + k] = cacc[6 * m.body_parentid[i] + k] + rt[6 * i + k];
+  }
+  TSYNC();
+  double* cinert = T.w + L.cinert;
+  FOR_T(i, nb) {
+    if (i == 0) {
+      for (int k = 0; k < 6; k++) cfrc[k] = 0;
+    } else {
+      double ci[10], a[6], f[6], cv[6], tmp[6], tmp1[6];
+      ldm<10>(ci, cinert + 10 * i);
+      ldm<6>(a, cacc + 6 * i);
+      ldm<6>(cv, cvelw + 6 * i);
+      mul_inert_vec(f, ci, a);
+      mul_inert_vec(tmp, ci, cv);
+      cross_force(tmp1, cv, tmp);
+      for (int k = 0; k < 6; k++) cfrc[6 * i + k] = f[k] + tmp1[k];
+    }
+  }
+  TSYNC();
+  FOR_T(k, 6) {
+    for (int i = nb - 1; i > 0; i--) {
+      int p = m.body_parentid[i];
+      if (p) cfrc[6 * p + k] += cfrc[6 * i + k];
+    }
+  }
+  TSYNC();
+  double* bias = T.w + L.qfrc_bias;
+  FOR_T(i, nv) bias[i] = tdot(cdof + 6 * i, cfrc + 6 * m.dof_bodyid[i], 6);
+  TSYNC();
+}
+
+// -------------------------------------------------- acceleration stage ---
+__device__ inline void fwd_acceleration(const DevModel& m, const WsLayout& L, const CoopAux& X, const Team& T) {
+  const int nv = m.nv, nu = m.nu;
+  double* ctrl = T.w + L.ctrl;
+  double* af = T.w + L.afrc;
+  double* amom = T.w + L.amom;
+  double* qa = T.w + L.qfrc_act;
+  FOR_T(i, nu) {
+    double c = ctrl[i], f;
+    if (m.actuator_ctrllimited[i]) c = clipd(c, m.actuator_ctrlrange[2 * i], m.actuator_ctrlrange[2 * i + 1]);
+    f = m.actuator_gainprm[i] * c;
+    if (m.actuator_forcelimited[i]) f = clipd(f, m.actuator_forcerange[2 * i], m.actuator_forcerange[2 * i + 1]);
+    af[i] = f;
+  }
+  TSYNC();
+  double* sm = T.w + L.qfrc_smooth;
+  double* qp = T.w + L.qfrc_passive;
+  double* qb = T.w + L.qfrc_bias;
+  double* qap = T.w + L.qfrc_applied;
+  double* xf = T.w + L.xfrc_applied;
+  double* xipos = T.w + L.xipos;
+  double* scom = T.w + L.scom;
+  double* cdof = T.w + L.cdof;
+  double* qs = T.w + L.qacc_smooth;
+  FOR_T(j, nv) {
+    double s = 0;
+    for (int i = 0; i < nu; i++) s += amom[i * nv + j] * af[i];
+    qa[j] = s;
+    double v = qp[j] - qb[j];
+    v += qap[j];
+    v += s;
+    // xfrc_applied: jac columns of dof j at each loaded body's COM
+    for (int b = 1; b < m.nbody; b++) {
+      double f[6];
+      ldm<6>(f, xf + 6 * b);
+      if (f[0] == 0 && f[1] == 0 && f[2] == 0 && f[3] == 0 && f[4] == 0 && f[5] == 0) continue;
+      double p[3] = {xipos[3 * b], xipos[3 * b + 1], xipos[3 * b + 2]}, jp[3], jr[3] = {0, 0, 0};
+      jac_col(m, X, scom, cdof, p, b, j, jp);
+      int bb = b;
+      while (bb && !m.body_dofnum[bb]) bb = m.body_parentid[bb];
+      if (bb && X.isanc[(m.body_dofadr[bb] + m.body_dofnum[bb] - 1) * nv + j]) {
+        jr[0] = cdof[6 * j]; jr[1] = cdof[6 * j + 1]; jr[2] = cdof[6 * j + 2];
+      }
+      double t1 = jp[0] * f[0] + jp[1] * f[1] + jp[2] * f[2];
+      double t2 = jr[0] * f[3] + jr[1] * f[4] + jr[2] * f[5];
+      v += t1 + t2;
+    }
+    sm[j] = v;
+    qs[j] = v;
+  }
+  TSYNC();
+  solve_ld(m, T, T.w + L.qLD, T.w + L.qLDinv, qs);
+}
+
+// constraint cost of residuals `jar`; force/state per row, qfrc_constraint per dof
+__device__ inline double constraint_update(const DevModel& m, const WsLayout& L, const CoopLayout& C, const Team& T,
+                                           const double* jar) {
+  const int nv = m.nv, ne = T.iw[L.nefc];
+  double* D = T.w + L.efc_D;
+  double* force = T.w + L.efc_force;
+  double* J = T.w + L.efc_J;
+  double* qc = T.w + L.qfrc_con;
+  int* state = T.iw + L.efc_state;
+  double* term = T.c + C.cterm;
+  FOR_T(i, ne) {
+    double jr = jar[i];
+    if (jr < 0) {
+      double Di = D[i];
+      force[i] = -Di * jr;
+      state[i] = 1;
+      term[i] = 0.5 * Di * jr * jr;
+    } else {
+      force[i] = 0;
+      state[i] = 0;
+    }
+  }
+  TSYNC();
+  FOR_T(j, nv) {
+    double s = 0;
+    for (int i = 0; i < ne; i++) s += J[i * nv + j] * force[i];
+    qc[j] = s;
+  }
+  if (T.tid == 0) {
+    double cost = 0;
+    for (int i = 0; i < ne; i++)
+      if (state[i]) cost += term[i];
+    T.c[C.bc] = cost;
+  }
+  TSYNC();
+  return T.c[C.bc];
+}
+
+__device__ inline void hessian_factor(const DevModel& m, const WsLayout& L, const CoopLayout& C, const Team& T,
+                                      double* H) {
+  const int nv = m.nv, ne = T.iw[L.nefc];
+  double* J = T.w + L.efc_J;
+  double* D = T.w + L.efc_D;
+  double* qM = T.w + L.qM;
+  int* state = T.iw + L.efc_state;
+  FOR_T(e, nv * nv) {
+    int r = e / nv, c = e % nv;
+    if (c <= r) {
+      double h = 0;
+      for (int i = 0; i < ne; i++)
+        if (state[i]) h += J[i * nv + r] * D[i] * J[i * nv + c];
+      H[e] = qM[e] + h;
+    }
+  }
+  TSYNC();
+  for (int j = 0; j < nv; j++) {
+    if (T.tid == 0) {
+      double t = H[j * nv + j];
+      if (j) t -= tdot(H + j * nv, H + j * nv, j);
+      if (t < MINVAL) t = MINVAL;
+      H[j * nv + j] = sqrt(t);
+      T.c[C.bc + 1] = 1 / H[j * nv + j];
+    }
+    TSYNC();
+    const double tinv = T.c[C.bc + 1];
+    FOR_T(i, nv) {
+      if (i > j) H[i * nv + j] = (H[i * nv + j] - tdot(H + i * nv, H + j * nv, j)) * tinv;
+    }
+    TSYNC();
+  }
+}
+
+__device__ inline void solver_newton(const DevModel& m, const WsLayout& L, const CoopLayout& C, const Team& T,
+                                     int maxiter, double tol) {
+  const int nv = m.nv, ne = T.iw[L.nefc];
+  const double scale = 1 / (m.stat_meaninertia * (nv > 1 ? nv : 1));
+  double* s = T.w + L.s_newton;
+  double *Ma = s, *grad = s + nv, *search = s + 2 * nv, *Mv = s + 3 * nv, *H = s + 4 * nv;
+  double* jar = s + 4 * nv + nv * nv;
+  double* Jv = jar + ne;
+  double* qM = T.w + L.qM;
+  double* qacc = T.w + L.qacc;
+  double* J = T.w + L.efc_J;
+  double* aref = T.w + L.efc_aref;
+  double* qfs = T.w + L.qfrc_smooth;
+  double* qas = T.w + L.qacc_smooth;
+  double* qc = T.w + L.qfrc_con;
+  double* Dv = T.w + L.efc_D;
+  double* bc = T.c + C.bc;
+  FOR_T(i, nv) Ma[i] = tdot(qM + i * nv, qacc, nv);
+  FOR_T(i, ne) jar[i] = tdot(J + i * nv, qacc, nv) - aref[i];
+  TSYNC();
+  double ccost = constraint_update(m, L, C, T, jar);
+  if (T.tid == 0) {
+    double g = 0;
+    for (int j = 0; j < nv; j++) g += (Ma[j] - qfs[j]) * (qacc[j] - qas[j]);
+    bc[2] = 0.5 * g + ccost;
+  }
+  FOR_T(j, nv) grad[j] = (Ma[j] - qfs[j]) - qc[j];
+  TSYNC();
+  double cost = bc[2];
+  hessian_factor(m, L, C, T, H);
+  int iter = 0;
+  while (iter < maxiter) {
+    // search = -H^-1 grad ; line search ; all on lane 0 except the parallel products
+    if (T.tid == 0) {
+      for (int i = 0; i < nv; i++) search[i] = grad[i];
+      for (int i = 0; i < nv; i++) {
+        if (i) search[i] -= tdot(H + i * nv, search, i);
+        search[i] /= H[i * nv + i];
+      }
+      for (int i = nv - 1; i >= 0; i--) {
+        for (int j = i + 1; j < nv; j++) search[i] -= H[j * nv + i] * search[j];
+        search[i] /= H[i * nv + i];
+      }
+      for (int j = 0; j < nv; j++) search[j] = -search[j];
+    }
+    TSYNC();
+    FOR_T(i, nv) Mv[i] = tdot(qM + i * nv, search, nv);
+    FOR_T(i, ne) Jv[i] = tdot(J + i * nv, search, nv);
+    TSYNC();
+    if (T.tid == 0) {
+      double alpha = 0;
+      double snorm = sqrt(tdot(search, search, nv));
+      if (!(snorm < MINVAL)) {
+        double g1 = 0, g2 = 0, d1, d2, lo = 0, hi = -1;
+        for (int j = 0; j < nv; j++) g1 += search[j] * (Ma[j] - qfs[j]);
+        for (int j = 0; j < nv; j++) g2 += search[j] * Mv[j];
+        auto eval = [&](double a) {
+          d1 = g1 + g2 * a;
+          d2 = g2;
+          for (int i = 0; i < ne; i++) {
+            double jv = Jv[i];
+            double x = jar[i] + a * jv;
+            if (x < 0) {
+              double Di = Dv[i];
+              d1 += Di * x * jv;
+              d2 += Di * jv * jv;
+            }
+          }
+        };
+        eval(0.0);
+        if (d1 < 0) {
+          double gtol = LS_TOL * fabs(d1);
+          for (int it = 0; it < LS_ITER; it++) {
+            double anew = alpha - d1 / d2;
+            if (hi >= 0 && !(anew > lo && anew < hi)) anew = 0.5 * (lo + hi);
+            alpha = anew;
+            eval(alpha);
+            if (fabs(d1) < gtol) break;
+            if (d1 < 0) lo = alpha; else hi = alpha;
+          }
+        }
+      }
+      bc[3] = alpha;
+    }
+    TSYNC();
+    const double alpha = bc[3];
+    if (alpha == 0) break;
+    FOR_T(j, nv) {
+      qacc[j] += alpha * search[j];
+      Ma[j] += alpha * Mv[j];
+    }
+    FOR_T(i, ne) jar[i] += alpha * Jv[i];
+    TSYNC();
+    iter++;
+    double oldcost = cost;
+    ccost = constraint_update(m, L, C, T, jar);
+    FOR_T(j, nv) grad[j] = (Ma[j] - qfs[j]) - qc[j];
+    TSYNC();
+    if (T.tid == 0) {
+      double g = 0;
+      for (int j = 0; j < nv; j++) g += (Ma[j] - qfs[j]) * (qacc[j] - qas[j]);
+      double c2 = 0.5 * g + ccost;
+      double improvement = scale * (oldcost - c2);
+      double gradient = scale * sqrt(tdot(grad, grad, nv));
+      bc[2] = c2;
+      bc[4] = (improvement < tol || gradient < tol) ? 1.0 : 0.0;
+    }
+    TSYNC();
+    cost = bc[2];
+    if (bc[4] != 0) break;
+    hessian_factor(m, L, C, T, H);
+  }
+}
+
+__device__ inline void fwd_constraint(const DevModel& m, const WsLayout& L, const CoopLayout& C, const Team& T,
+                                      int maxiter, double tol) {
+  const int nv = m.nv, ne = T.iw[L.nefc];
+  double* qacc = T.w + L.qacc;
+  double* warm = T.w + L.warm;
+  double* qas = T.w + L.qacc_smooth;
+  double* qc = T.w + L.qfrc_con;
+  if (!ne) {
+    FOR_T(i, nv) { double v = qas[i]; qacc[i] = v; warm[i] = v; qc[i] = 0; }
+    TSYNC();
+    return;
+  }
+  {
+    double* s = T.w + L.s_newton;
+    double* Ma = s;
+    double* jar = s + 4 * nv + nv * nv;
+    double* J = T.w + L.efc_J;
+    double* aref = T.w + L.efc_aref;
+    double* b = T.w + L.efc_b;
+    double* qM = T.w + L.qM;
+    double* qfs = T.w + L.qfrc_smooth;
+    FOR_T(i, ne) {
+      b[i] = tdot(J + i * nv, qas, nv) - aref[i];
+      jar[i] = tdot(J + i * nv, warm, nv) - aref[i];
+    }
+    FOR_T(i, nv) Ma[i] = tdot(qM + i * nv, warm, nv);
+    TSYNC();
+    double cost_smooth = constraint_update(m, L, C, T, b);
+    double cw = constraint_update(m, L, C, T, jar);
+    if (T.tid == 0) {
+      double g = 0;
+      for (int j = 0; j < nv; j++) g += (Ma[j] - qfs[j]) * (warm[j] - qas[j]);
+      double cost_warm = 0.5 * g + cw;
+      T.ci[C.ibc] = cost_warm > cost_smooth ? 1 : 0;
+    }
+    TSYNC();
+    const int use_smooth = T.ci[C.ibc];
+    FOR_T(i, nv) qacc[i] = use_smooth ? qas[i] : warm[i];
+    TSYNC();
+  }
+  solver_newton(m, L, C, T, maxiter, tol);
+  FOR_T(i, nv) warm[i] = qacc[i];
+  TSYNC();
+}
+
+__device__ inline void forward_skip(const DevModel& m, const WsLayout& L, const CoopLayout& C, const CoopAux& X,
+                                    const Team& T, int skipstage, int maxiter, double tol) {
+  if (skipstage < STAGE_POS) fwd_position(m, L, C, X, T);
+  if (skipstage < STAGE_VEL) fwd_velocity(m, L, C, T);
+  fwd_acceleration(m, L, X, T);
+  fwd_constraint(m, L, C, T, maxiter, tol);
+}
+
+__device__ inline void integrate_pos(const DevModel& m, const Team& T, double* qpos, const double* qvel, double dt) {
+  FOR_T(j, m.njnt) {
+    int pa = m.jnt_qposadr[j], va = m.jnt_dofadr[j];
+    int type = m.jnt_type[j];
+    if (type == JNT_FREE || type == JNT_BALL) {
+      if (type == JNT_FREE) {
+        for (int i = 0; i < 3; i++) qpos[pa + i] += dt * qvel[va + i];
+        pa += 3;
+        va += 3;
+      }
+      double q[4], v[3];
+      ldm<4>(q, qpos + pa);
+      ldm<3>(v, qvel + va);
+      quat_integrate(q, v, dt);
+      for (int k = 0; k < 4; k++) qpos[pa + k] = q[k];
+    } else {
+      qpos[pa] += dt * qvel[va];
+    }
+  }
+  TSYNC();
+}
+
+__device__ inline void reset_data(const DevModel& m, const WsLayout& L, const Team& T) {
+  double* qpos = T.w + L.qpos;
+  FOR_T(i, m.nq) qpos[i] = m.qpos0[i];
+  FOR_T(i, m.nv) {
+    T.w[L.qvel + i] = 0;
+    T.w[L.warm + i] = 0;
+    T.w[L.qfrc_applied + i] = 0;
+  }
+  FOR_T(i, m.nu) T.w[L.ctrl + i] = 0;
+  FOR_T(i, 6 * m.nbody) T.w[L.xfrc_applied + i] = 0;
+  if (T.tid == 0) T.w[L.time] = 0;
+  TSYNC();
+}
+
+__device__ inline int any_bad(const Team& T, const CoopLayout& C, const double* x, int n) {
+  if (T.tid == 0) {
+    int bad = 0;
+    for (int i = 0; i < n; i++)
+      if (is_bad(x[i])) { bad = 1; break; }
+    T.ci[C.ibc + 1] = bad;
+  }
+  TSYNC();
+  int r = T.ci[C.ibc + 1];
+  TSYNC();
+  return r;
+}
+
+__device__ inline void euler(const DevModel& m, const WsLayout& L, const CoopLayout& C, const CoopAux& X,
+                             const Team& T) {
+  const int nv = m.nv;
+  double* s = T.w + L.s_euler;
+  double *qacc = s, *qH = s + nv, *qHLD = s + nv + nv * nv, *qHinv = s + nv + 2 * nv * nv;
+  double* qM = T.w + L.qM;
+  double* dq = T.w + L.qacc;
+  double* qvel = T.w + L.qvel;
+  bool dmp = false;
+  for (int i = 0; i < nv; i++)
+    if (m.dof_damping[i] > 0) { dmp = true; break; }
+  if (!dmp) {
+    FOR_T(i, nv) qacc[i] = dq[i];
+    TSYNC();
+  } else {
+    FOR_T(i, nv) qacc[i] = tdot(qM + i * nv, dq, nv);
+    FOR_T(e, nv * nv) {
+      int i = e / nv, j = e % nv;
+      double v = qM[e];
+      if (i == j) v += m.opt_timestep * m.dof_damping[i];
+      qH[e] = v;
+    }
+    TSYNC();
+    factor_ld(m, X, T, qH, qHLD, qHinv, T.c + C.ftmp);
+    solve_ld(m, T, qHLD, qHinv, qacc);
+  }
+  const double h = m.opt_timestep;
+  FOR_T(i, nv) qvel[i] += qacc[i] * h;
+  TSYNC();
+  integrate_pos(m, T, T.w + L.qpos, qvel, h);
+  if (T.tid == 0) T.w[L.time] += h;
+  TSYNC();
+}
+
+__device__ inline void rk4(const DevModel& m, const WsLayout& L, const CoopLayout& C, const CoopAux& X, const Team& T,
+                           int maxiter, double tol) {
+  const double A[9] = {0.5, 0, 0, 0, 0.5, 0, 0, 0, 1};
+  const double Bw[4] = {1.0 / 6, 1.0 / 3, 1.0 / 3, 1.0 / 6};
+  const int nv = m.nv, nq = m.nq, N = 4;
+  const double h = m.opt_timestep;
+  double* qpos = T.w + L.qpos;
+  double* qvel = T.w + L.qvel;
+  double* qaccw = T.w + L.qacc;
+  const double time = T.w[L.time];
+  double Cc[3], Tt[3];
+  double* s = T.w + L.s_rk4;
+  double *dX = s, *X0 = s + 2 * nv, *F = s + 2 * nv + 4 * (nq + nv);
+  for (int i = 1; i < N; i++) {
+    Cc[i - 1] = 0;
+    for (int j = 0; j < i; j++) Cc[i - 1] += A[(i - 1) * (N - 1) + j];
+    Tt[i - 1] = time + Cc[i - 1] * h;
+  }
+  FOR_T(k, nq) X0[k] = qpos[k];
+  FOR_T(k, nv) { X0[nq + k] = qvel[k]; F[k] = qaccw[k]; }
+  TSYNC();
+  for (int i = 1; i < N; i++) {
+    double* Xi = X0 + i * (nq + nv);
+    FOR_T(k, nv) {
+      double a0 = 0, a1 = 0;
+      for (int j = 0; j < i; j++) {
+        double a = A[(i - 1) * (N - 1) + j];
+        a0 += X0[j * (nq + nv) + nq + k] * a;
+        a1 += F[j * nv + k] * a;
+      }
+      dX[k] = a0;
+      dX[nv + k] = a1;
+    }
+    FOR_T(k, nq + nv) Xi[k] = X0[k];
+    TSYNC();
+    integrate_pos(m, T, Xi, dX, h);
+    FOR_T(k, nv) Xi[nq + k] += dX[nv + k] * h;
+    TSYNC();
+    FOR_T(k, nq) qpos[k] = Xi[k];
+    FOR_T(k, nv) qvel[k] = Xi[nq + k];
+    if (T.tid == 0) T.w[L.time] = Tt[i - 1];
+    TSYNC();
+    forward_skip(m, L, C, X, T, STAGE_NONE, maxiter, tol);
+    FOR_T(k, nv) F[i * nv + k] = qaccw[k];
+    TSYNC();
+  }
+  FOR_T(k, nv) {
+    double a0 = 0, a1 = 0;
+    for (int j = 0; j < N; j++) {
+      a0 += X0[j * (nq + nv) + nq + k] * Bw[j];
+      a1 += F[j * nv + k] * Bw[j];
+    }
+    dX[k] = a0;
+    dX[nv + k] = a1;
+  }
+  TSYNC();
+  FOR_T(k, nq) qpos[k] = X0[k];
+  FOR_T(k, nv) qvel[k] = X0[nq + k] + dX[nv + k] * h;
+  if (T.tid == 0) T.w[L.time] = time;
+  TSYNC();
+  integrate_pos(m, T, qpos, dX, h);
+  if (T.tid == 0) T.w[L.time] += h;
+  TSYNC();
+}
+
+// mj_step with the model's own solver settings
+__device__ inline void step(const DevModel& m, const WsLayout& L, const CoopLayout& C, const CoopAux& X,
+                            const Team& T) {
+  if (any_bad(T, C, T.w + L.qpos, m.nq)) reset_data(m, L, T);
+  if (any_bad(T, C, T.w + L.qvel, m.nv)) reset_data(m, L, T);
+  forward_skip(m, L, C, X, T, STAGE_NONE, m.opt_iterations, m.opt_tolerance);
+  if (any_bad(T, C, T.w + L.qacc, m.nv)) {
+    reset_data(m, L, T);
+    forward_skip(m, L, C, X, T, STAGE_NONE, m.opt_iterations, m.opt_tolerance);
+  }
+  if (m.opt_integrator == 1)
+    rk4(m, L, C, X, T, m.opt_iterations, m.opt_tolerance);
+  else
+    euler(m, L, C, X, T);
+}
+
+}  // namespace coop
+}  // namespace ilqg

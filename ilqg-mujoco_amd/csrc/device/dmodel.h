@@ -90,4 +90,42 @@ inline WsLayout make_layout(const DevModel& m) {
   return L;
 }
 
+namespace coop {
+// extra per-team scratch (doubles / ints), appended after the WsLayout block
+struct CoopLayout {
+  int qloc, buf6, ftmp, pcon, jc, cterm, rtmp, bc;  // doubles
+  int nd;
+  int pcnt, rsub, jcnt, ibc;  // ints
+  int ni;
+};
+
+inline CoopLayout make_coop_layout(const DevModel& m, int npair) {
+  CoopLayout C{};
+  int o = 0, oi = 0;
+  const int nc = m.maxcon > 0 ? m.maxcon : 1, ne = m.maxefc > 0 ? m.maxefc : 1;
+  C.qloc = o; o += 4 * m.njnt;
+  C.buf6 = o; o += 6 * m.nv;
+  C.ftmp = o; o += m.nv;
+  C.pcon = o; o += 14 * (npair > 0 ? npair : 1);
+  C.jc = o; o += 3 * m.nv * nc;
+  C.cterm = o; o += ne;
+  C.rtmp = o; o += 6 * m.nbody;
+  C.bc = o; o += 8;
+  C.nd = o;
+  C.pcnt = oi; oi += (npair > 0 ? npair : 1);
+  C.rsub = oi; oi += ne;
+  C.jcnt = oi; oi += 2 * m.njnt;
+  C.ibc = oi; oi += 8;
+  C.ni = oi;
+  return C;
+}
+
+// static data the host derives once per model
+struct CoopAux {
+  const int* isanc;  // nv*nv: isanc[i*nv+j] = 1 if dof j is dof i or an ancestor of it
+  const int* pair;   // 2*npair: geom pairs passing the static collision filters, oracle order
+  int npair;
+};
+
+}  // namespace coop
 }  // namespace ilqg

@@ -57,3 +57,21 @@ hipError_t launch_forward(const DevModel& m, const WsLayout& L, WsDev ws, TrajDe
 size_t backward_lds_bytes(int nv, int nu);
 
 }  // namespace ilqg
+
+// ---- cooperative (one wavefront per evaluation, LDS workspace) variants ----
+namespace ilqg {
+size_t coop_lds_bytes(const WsLayout& L, const coop::CoopLayout& C);
+hipError_t launch_fd_centre_coop(const DevModel& m, const WsLayout& L, const coop::CoopLayout& C,
+                                 const coop::CoopAux& X, TrajDev tr, int npts, int P, const double* qfrc_applied,
+                                 const double* xfrc_applied, CostDev cost, double* warm_c, double* cost_c,
+                                 hipStream_t st);
+hipError_t launch_fd_cols_coop(const DevModel& m, const WsLayout& L, const coop::CoopLayout& C,
+                               const coop::CoopAux& X, TrajDev tr, int npts, int P, const double* qfrc_applied,
+                               const double* xfrc_applied, CostDev cost, const double* warm_c, const double* cost_c,
+                               double* deriv, hipStream_t st);
+hipError_t launch_rollout_coop(const DevModel& m, const WsLayout& L, const coop::CoopLayout& C,
+                               const coop::CoopAux& X, int S, int A, int P, TrajDev nominal, TrajDev out,
+                               int out_is_cand, const double* K, const double* k, const double* alphas, TrajDev dinit,
+                               const double* qfrc_applied, const double* xfrc_applied, int passive, CostDev cost,
+                               double* cost_cand, hipStream_t st);
+}  // namespace ilqg

@@ -1,0 +1,271 @@
+// Cooperative hot-path kernels: one 64-lane workgroup (one wavefront) per
+// physics evaluation, workspace in LDS (dcoop.h).
+//   k_fd_centre_coop  src/mjderivative.cpp:61-75   one workgroup per trajectory point
+//   k_fd_cols_coop    src/mjderivative.cpp:78-206  one workgroup per (point, column)
+//   k_rollout_coop    inc/ilqr.h:116-130           one workgroup per (seed, alpha)
+#include "dcoop.h"
+#include "kernels.h"
+
+namespace ilqg {
+namespace {
+
+using namespace coop;
+
+constexpr double FD_EPS = 1e-6;  // mjderivative.cpp:39
+constexpr int FD_NITER = 30;     // mjderivative.cpp:37
+constexpr int FD_NWARMUP = 3;    // mjderivative.cpp:38
+constexpr int TEAM = 64;
+
+__device__ inline Team make_team(const WsLayout& L, const CoopLayout& C) {
+  extern __shared__ double lds[];
+  Team T;
+  T.w = lds;
+  T.c = lds + L.nd;
+  T.iw = reinterpret_cast<int*>(lds + L.nd + C.nd);
+  T.ci = T.iw + L.ni;
+  T.tid = threadIdx.x;
+  T.nt = blockDim.x;
+  return T;
+}
+
+__device__ inline double cost_terms(double c, const double* x, const double* w, const double* t, const double* l,
+                                    int n) {
+  for (int i = 0; i < n; i++) {
+    double xi = x[i];
+    if (w[i] != 0) {
+      double dx = xi - t[i];
+      c += w[i] * dx * dx;
+    }
+    if (l[i] != 0) c += l[i] * xi;
+  }
+  return c;
+}
+__device__ inline double step_cost(const DevModel& m, const CostDev& c, const double* qpos, const double* qvel,
+                                   const double* ctrl) {
+  double s = 0;
+  s = cost_terms(s, qpos, c.wq, c.tq, c.lq, m.nq);
+  s = cost_terms(s, qvel, c.wv, c.tv, c.lv, m.nv);
+  s = cost_terms(s, ctrl, c.wu, c.tu, c.lu, m.nu);
+  return s;
+}
+
+// cpMjData(d, src) from a trajectory record (src/util.cpp:4-14)
+__device__ inline void load_state(const DevModel& m, const WsLayout& L, const Team& T, const TrajDev& tr, int pt,
+                                  int seed, const double* qfrc_applied, const double* xfrc_applied) {
+  FOR_T(i, m.nq) T.w[L.qpos + i] = tr.qpos[(size_t)pt * m.nq + i];
+  FOR_T(i, m.nv) {
+    T.w[L.qvel + i] = tr.qvel[(size_t)pt * m.nv + i];
+    T.w[L.warm + i] = tr.warm[(size_t)pt * m.nv + i];
+    T.w[L.qfrc_applied + i] = qfrc_applied ? qfrc_applied[(size_t)seed * m.nv + i] : 0.0;
+  }
+  FOR_T(i, m.nu) T.w[L.ctrl + i] = tr.ctrl[(size_t)pt * m.nu + i];
+  FOR_T(i, 6 * m.nbody) T.w[L.xfrc_applied + i] = xfrc_applied ? xfrc_applied[(size_t)seed * 6 * m.nbody + i] : 0.0;
+  if (T.tid == 0) T.w[L.time] = tr.time[pt];
+  TSYNC();
+}
+
+__global__ __launch_bounds__(TEAM) void k_fd_centre_coop(DevModel m, WsLayout L, CoopLayout C, CoopAux X, TrajDev tr,
+                                                         int P, const double* qfrc_applied,
+                                                         const double* xfrc_applied, CostDev cost, double* warm_c,
+                                                         double* cost_c) {
+  const int pt = blockIdx.x;
+  Team T = make_team(L, C);
+  load_state(m, L, T, tr, pt, pt / P, qfrc_applied, xfrc_applied);
+  forward_skip(m, L, C, X, T, STAGE_NONE, FD_NITER, 0.0);
+  for (int rep = 1; rep < FD_NWARMUP; rep++) forward_skip(m, L, C, X, T, STAGE_VEL, FD_NITER, 0.0);
+  FOR_T(i, m.nv) warm_c[(size_t)pt * m.nv + i] = T.w[L.warm + i];
+  if (T.tid == 0)
+    cost_c[pt] = step_cost(m, cost, tr.qpos + (size_t)pt * m.nq, tr.qvel + (size_t)pt * m.nv,
+                           tr.ctrl + (size_t)pt * m.nu);
+}
+
+__global__ __launch_bounds__(TEAM) void k_fd_cols_coop(DevModel m, WsLayout L, CoopLayout C, CoopAux X, TrajDev tr,
+                                                       int P, const double* qfrc_applied, const double* xfrc_applied,
+                                                       CostDev cost, const double* warm_c, const double* cost_c,
+                                                       double* deriv) {
+  const int nv = m.nv, nu = m.nu;
+  const int nctrl = nu < nv ? nu : nv;  // mjderivative.cpp:78-82 (assumes nv >= nu)
+  const int ncol = nctrl + 2 * nv;
+  const int pt = blockIdx.x / ncol, col = blockIdx.x % ncol;
+  Team T = make_team(L, C);
+  const int D = nv * (2 * nv + nu) + 2 * nv + nu;
+  double* dr = deriv + (size_t)pt * D;
+  const double* wc = warm_c + (size_t)pt * nv;
+  const double costCenter = cost_c[pt];
+  double* qpos = T.w + L.qpos;
+  double* qvel = T.w + L.qvel;
+  double* ctrl = T.w + L.ctrl;
+  double* warm = T.w + L.warm;
+  double* qacc = T.w + L.qacc;
+  double* temp = T.w + L.s_fd;
+  const double* dq = tr.qpos + (size_t)pt * m.nq;
+  const double* dv = tr.qvel + (size_t)pt * nv;
+  const double* du = tr.ctrl + (size_t)pt * nu;
+  load_state(m, L, T, tr, pt, pt / P, qfrc_applied, xfrc_applied);
+  int kind, i, skip_minus;
+  if (col < nctrl) { kind = 0; i = col; skip_minus = STAGE_VEL; }
+  else if (col < nctrl + nv) { kind = 1; i = col - nctrl; skip_minus = STAGE_POS; }
+  else { kind = 2; i = col - nctrl - nv; skip_minus = STAGE_NONE; }
+  int quatadr = -1, dofpos = 0, jid = m.dof_jntid[i];
+  if (kind == 2) {
+    if (m.jnt_type[jid] == JNT_BALL) {
+      quatadr = m.jnt_qposadr[jid];
+      dofpos = i - m.jnt_dofadr[jid];
+    } else if (m.jnt_type[jid] == JNT_FREE && i >= m.jnt_dofadr[jid] + 3) {
+      quatadr = m.jnt_qposadr[jid] + 3;
+      dofpos = i - m.jnt_dofadr[jid] - 3;
+    }
+  }
+  // + side: perturb, forward-difference cost, dynamics from the centre warmstart
+  if (T.tid == 0) {
+    if (kind == 0) ctrl[i] = du[i] + FD_EPS;
+    else if (kind == 1) qvel[i] = dv[i] + FD_EPS;
+    else if (quatadr >= 0) {
+      double angvel[3] = {0, 0, 0}, q[4];
+      angvel[dofpos] = FD_EPS;
+      ldm<4>(q, qpos + quatadr);
+      quat_integrate(q, angvel, 1);
+      for (int k = 0; k < 4; k++) qpos[quatadr + k] = q[k];
+    } else {
+      qpos[m.jnt_qposadr[jid] + i - m.jnt_dofadr[jid]] += FD_EPS;
+    }
+    double cp = (step_cost(m, cost, qpos, qvel, ctrl) - costCenter) / FD_EPS;
+    int at = kind == 0 ? 2 * nv * nv + nv * nu + 2 * nv + i
+                       : (kind == 1 ? 2 * nv * nv + nv * nu + nv + i : 2 * nv * nv + nv * nu + i);
+    dr[at] = cp;
+  }
+  FOR_T(j, nv) warm[j] = wc[j];
+  TSYNC();
+  forward_skip(m, L, C, X, T, STAGE_NONE, FD_NITER, 0.0);
+  FOR_T(j, nv) temp[j] = qacc[j];
+  if (kind == 2) FOR_T(k, m.nq) qpos[k] = dq[k];
+  TSYNC();
+  // - side
+  if (T.tid == 0) {
+    if (kind == 0) ctrl[i] = du[i] - FD_EPS;
+    else if (kind == 1) qvel[i] = dv[i] - FD_EPS;
+    else if (quatadr >= 0) {
+      double angvel[3] = {0, 0, 0}, q[4];
+      angvel[dofpos] = -FD_EPS;
+      ldm<4>(q, qpos + quatadr);
+      quat_integrate(q, angvel, 1);
+      for (int k = 0; k < 4; k++) qpos[quatadr + k] = q[k];
+    } else {
+      qpos[m.jnt_qposadr[jid] + i - m.jnt_dofadr[jid]] -= FD_EPS;
+    }
+  }
+  FOR_T(j, nv) warm[j] = wc[j];
+  TSYNC();
+  forward_skip(m, L, C, X, T, skip_minus, FD_NITER, 0.0);
+  FOR_T(j, nv) {
+    double v = (temp[j] - qacc[j]) / (2 * FD_EPS);
+    if (kind == 0) dr[2 * nv * nv + i + j * nu] = v;
+    else if (kind == 1) dr[nv * nv + i + j * nv] = v;
+    else dr[i + j * nv] = v;
+  }
+}
+
+__global__ __launch_bounds__(TEAM) void k_rollout_coop(DevModel m, WsLayout L, CoopLayout C, CoopAux X, int S, int A,
+                                                       int P, TrajDev nom, TrajDev out, int out_is_cand,
+                                                       const double* K, const double* k, const double* alphas,
+                                                       TrajDev dinit, const double* qfrc_applied,
+                                                       const double* xfrc_applied, int passive, CostDev cost,
+                                                       double* cost_cand) {
+  const int lane = blockIdx.x;
+  const int s = lane / A, a = lane % A;
+  const int nq = m.nq, nv = m.nv, nu = m.nu, nx = 2 * nv;
+  Team T = make_team(L, C);
+  load_state(m, L, T, dinit, s, s, qfrc_applied, xfrc_applied);
+  double* qpos = T.w + L.qpos;
+  double* qvel = T.w + L.qvel;
+  double* ctrl = T.w + L.ctrl;
+  double* warm = T.w + L.warm;
+  double* dx = T.w + L.s_fd;
+  const double alpha = alphas ? alphas[a] : 1.0;
+  const int ob = out_is_cand ? lane : s;
+  double c = 0;
+  for (int n = P - 1; n >= 0; n--) {
+    const size_t pn = (size_t)s * P + n;
+    if (!passive) {
+      const double* xs_q = nom.qpos + pn * nq;
+      const double* xs_v = nom.qvel + pn * nv;
+      FOR_T(j, nx) dx[j] = j < nv ? qpos[j] - xs_q[j] : qvel[j - nv] - xs_v[j - nv];
+      TSYNC();
+      const double* Kn = K + pn * nu * nx;
+      const double* kn = k + pn * nu;
+      const double* us = nom.ctrl + pn * nu;
+      FOR_T(i, nu) {
+        double t = 0;
+        for (int j = 0; j < nx; j++) t += Kn[i + j * nu] * dx[j];
+        ctrl[i] = (t + alpha * kn[i]) + us[i];
+      }
+      TSYNC();
+    }
+    const size_t po = (size_t)ob * P + n;
+    FOR_T(i, nq) out.qpos[po * nq + i] = qpos[i];
+    FOR_T(i, nv) {
+      out.qvel[po * nv + i] = qvel[i];
+      out.warm[po * nv + i] = warm[i];
+    }
+    FOR_T(i, nu) out.ctrl[po * nu + i] = ctrl[i];
+    if (T.tid == 0) {
+      out.time[po] = T.w[L.time];
+      c += step_cost(m, cost, qpos, qvel, ctrl);
+    }
+    TSYNC();
+    step(m, L, C, X, T);
+  }
+  if (T.tid == 0 && cost_cand) cost_cand[lane] = c;
+}
+
+template <typename K>
+hipError_t allow_lds(K kern, size_t lds) {
+  if (lds <= 65536) return hipSuccess;
+  return hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
+                             (int)lds);
+}
+
+}  // namespace
+
+size_t coop_lds_bytes(const WsLayout& L, const CoopLayout& C) {
+  return (size_t)(L.nd + C.nd) * sizeof(double) + (size_t)(L.ni + C.ni) * sizeof(int);
+}
+
+hipError_t launch_fd_centre_coop(const DevModel& m, const WsLayout& L, const CoopLayout& C, const CoopAux& X,
+                                 TrajDev tr, int npts, int P, const double* qfrc_applied, const double* xfrc_applied,
+                                 CostDev cost, double* warm_c, double* cost_c, hipStream_t st) {
+  if (npts <= 0) return hipSuccess;
+  hipError_t e = allow_lds(k_fd_centre_coop, coop_lds_bytes(L, C));
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(k_fd_centre_coop, dim3(npts), dim3(TEAM), coop_lds_bytes(L, C), st, m, L, C, X, tr, P,
+                     qfrc_applied, xfrc_applied, cost, warm_c, cost_c);
+  return hipGetLastError();
+}
+
+hipError_t launch_fd_cols_coop(const DevModel& m, const WsLayout& L, const CoopLayout& C, const CoopAux& X,
+                               TrajDev tr, int npts, int P, const double* qfrc_applied, const double* xfrc_applied,
+                               CostDev cost, const double* warm_c, const double* cost_c, double* deriv,
+                               hipStream_t st) {
+  const int nctrl = m.nu < m.nv ? m.nu : m.nv;
+  const long blocks = (long)npts * (nctrl + 2 * m.nv);
+  if (blocks <= 0) return hipSuccess;
+  hipError_t e = allow_lds(k_fd_cols_coop, coop_lds_bytes(L, C));
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(k_fd_cols_coop, dim3((unsigned)blocks), dim3(TEAM), coop_lds_bytes(L, C), st, m, L, C, X, tr, P,
+                     qfrc_applied, xfrc_applied, cost, warm_c, cost_c, deriv);
+  return hipGetLastError();
+}
+
+hipError_t launch_rollout_coop(const DevModel& m, const WsLayout& L, const CoopLayout& C, const CoopAux& X, int S,
+                               int A, int P, TrajDev nominal, TrajDev out, int out_is_cand, const double* K,
+                               const double* k, const double* alphas, TrajDev dinit, const double* qfrc_applied,
+                               const double* xfrc_applied, int passive, CostDev cost, double* cost_cand,
+                               hipStream_t st) {
+  hipError_t e = allow_lds(k_rollout_coop, coop_lds_bytes(L, C));
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(k_rollout_coop, dim3(S * A), dim3(TEAM), coop_lds_bytes(L, C), st, m, L, C, X, S, A, P, nominal,
+                     out, out_is_cand, K, k, alphas, dinit, qfrc_applied, xfrc_applied, passive, cost, cost_cand);
+  return hipGetLastError();
+}
+
+}  // namespace ilqg
