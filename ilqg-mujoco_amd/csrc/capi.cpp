@@ -100,7 +100,6 @@ struct ilqg_model {
   DevBuf buf;
   DevModel dm{};
   WsLayout L{};
-  DevBuf auxbuf;
   coop::CoopAux X{};
   coop::CoopLayout C{};
   int npair = 0;
@@ -109,29 +108,47 @@ struct ilqg_model {
   int upload(int device) {
     if (dev == device && buf.p) return ILQG_OK;
     HIPCHK(hipSetDevice(device));
-    size_t total = 0;
-#define ILQG_SZ_F(nm, cnt) total += ((host.nm.size() * 8 + 255) & ~(size_t)255);
-#define ILQG_SZ_I(nm, cnt) total += ((host.nm.size() * 4 + 255) & ~(size_t)255);
-    ILQG_MODEL_F64_ARRAYS(ILQG_SZ_F)
-    ILQG_MODEL_I32_ARRAYS(ILQG_SZ_I)
-    std::vector<unsigned char> img(total + 256, 0);
-    size_t off = 0;
+    const HostModel& h = host;
+    // cooperative-kernel aux data: dof ancestor matrix and the statically
+    // admissible geom pairs in the oracle's (g1 < g2) enumeration order
+    std::vector<int> isanc(h.nv * h.nv, 0), pairs;
+    for (int i = 0; i < h.nv; i++)
+      for (int j = i; j >= 0; j = h.dof_parentid[j]) isanc[i * h.nv + j] = 1;
+    for (int g1 = 0; g1 < h.ngeom; g1++)
+      for (int g2 = g1 + 1; g2 < h.ngeom; g2++) {
+        int b1 = h.geom_bodyid[g1], b2 = h.geom_bodyid[g2];
+        int w1 = h.body_weldid[b1], w2 = h.body_weldid[b2];
+        int wp1 = h.body_weldid[h.body_parentid[w1]], wp2 = h.body_weldid[h.body_parentid[w2]];
+        if (w1 == w2) continue;
+        if (w1 != 0 && w2 != 0 && (w1 == wp2 || w2 == wp1)) continue;
+        if (!((h.geom_contype[g1] & h.geom_conaffinity[g2]) || (h.geom_contype[g2] & h.geom_conaffinity[g1])))
+          continue;
+        pairs.push_back(g1);
+        pairs.push_back(g2);
+      }
+    npair = (int)pairs.size() / 2;
+    // one compact image, every array 8-byte aligned, so a workgroup can stage
+    // the whole read-only model into LDS with one coalesced copy
+    std::vector<unsigned char> img;
     std::vector<std::pair<size_t, const void**>> fix;
-#define ILQG_CP_F(nm, cnt)                                                     \
-  {                                                                            \
-    if (!host.nm.empty()) memcpy(img.data() + off, host.nm.data(), host.nm.size() * 8); \
-    fix.emplace_back(off, (const void**)&dm.nm);                               \
-    off += ((host.nm.size() * 8 + 255) & ~(size_t)255);                        \
-  }
-#define ILQG_CP_I(nm, cnt)                                                     \
-  {                                                                            \
-    std::vector<int> v_(host.nm.begin(), host.nm.end());                       \
-    if (!v_.empty()) memcpy(img.data() + off, v_.data(), v_.size() * 4);       \
-    fix.emplace_back(off, (const void**)&dm.nm);                               \
-    off += ((host.nm.size() * 4 + 255) & ~(size_t)255);                        \
+    auto put = [&](const void* src, size_t bytes, const void** dst) {
+      size_t at = img.size();
+      img.resize(at + ((bytes + 7) & ~(size_t)7), 0);
+      if (bytes) memcpy(img.data() + at, src, bytes);
+      if (dst) fix.emplace_back(at, dst);
+      return at;
+    };
+#define ILQG_CP_F(nm, cnt) put(host.nm.data(), host.nm.size() * 8, (const void**)&dm.nm);
+#define ILQG_CP_I(nm, cnt)                                          \
+  {                                                                 \
+    std::vector<int> v_(host.nm.begin(), host.nm.end());            \
+    put(v_.data(), v_.size() * 4, (const void**)&dm.nm);            \
   }
     ILQG_MODEL_F64_ARRAYS(ILQG_CP_F)
     ILQG_MODEL_I32_ARRAYS(ILQG_CP_I)
+    size_t isanc_at = put(isanc.data(), isanc.size() * 4, nullptr);
+    size_t pair_at = put(pairs.data(), pairs.size() * 4, nullptr);
+    img.resize(img.size() + 8, 0);
     HIPCHK(buf.alloc(img.size()));
     HIPCHK(hipMemcpy(buf.p, img.data(), img.size(), hipMemcpyHostToDevice));
     for (auto& f : fix) *f.second = static_cast<unsigned char*>(buf.p) + f.first;
@@ -141,38 +158,13 @@ struct ilqg_model {
     ILQG_MODEL_F64_SCALARS(ILQG_SC_F)
     dm.maxcon = host.maxcon;
     dm.maxefc = host.maxefc;
+    dm.img = static_cast<const unsigned char*>(buf.p);
+    dm.img_bytes = (int)img.size();
     L = make_layout(dm);
-    // cooperative-kernel aux data: dof ancestor matrix and the statically
-    // admissible geom pairs in the oracle's (g1 < g2) enumeration order
-    {
-      const HostModel& h = host;
-      std::vector<int> aux(h.nv * h.nv, 0), pairs;
-      for (int i = 0; i < h.nv; i++)
-        for (int j = i; j >= 0; j = h.dof_parentid[j]) aux[i * h.nv + j] = 1;
-      for (int g1 = 0; g1 < h.ngeom; g1++)
-        for (int g2 = g1 + 1; g2 < h.ngeom; g2++) {
-          int b1 = h.geom_bodyid[g1], b2 = h.geom_bodyid[g2];
-          int w1 = h.body_weldid[b1], w2 = h.body_weldid[b2];
-          int wp1 = h.body_weldid[h.body_parentid[w1]], wp2 = h.body_weldid[h.body_parentid[w2]];
-          if (w1 == w2) continue;
-          if (w1 != 0 && w2 != 0 && (w1 == wp2 || w2 == wp1)) continue;
-          if (!((h.geom_contype[g1] & h.geom_conaffinity[g2]) || (h.geom_contype[g2] & h.geom_conaffinity[g1])))
-            continue;
-          pairs.push_back(g1);
-          pairs.push_back(g2);
-        }
-      npair = (int)pairs.size() / 2;
-      size_t na = aux.size(), np = pairs.size();
-      std::vector<int> all(na + np + 2, 0);
-      std::copy(aux.begin(), aux.end(), all.begin());
-      std::copy(pairs.begin(), pairs.end(), all.begin() + na);
-      HIPCHK(auxbuf.alloc(all.size() * 4));
-      HIPCHK(hipMemcpy(auxbuf.p, all.data(), all.size() * 4, hipMemcpyHostToDevice));
-      X.isanc = auxbuf.as<int>();
-      X.pair = auxbuf.as<int>() + na;
-      X.npair = npair;
-      C = coop::make_coop_layout(dm, npair);
-    }
+    X.isanc = reinterpret_cast<const int*>(static_cast<unsigned char*>(buf.p) + isanc_at);
+    X.pair = reinterpret_cast<const int*>(static_cast<unsigned char*>(buf.p) + pair_at);
+    X.npair = npair;
+    C = coop::make_coop_layout(dm, npair);
     if (!stream) HIPCHK(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
     dev = device;
     return ILQG_OK;

@@ -26,7 +26,33 @@ struct Team {
 };
 
 #define TSYNC() __syncthreads()
+
+// diagnostic build only (-DILQG_STAMPS): per-stage s_memtime deltas of
+// workgroup 0, lane 0, taken right after the stage's closing barrier
+#ifdef ILQG_STAMPS
+__device__ unsigned long long g_stamp_acc[32];
+__device__ unsigned long long g_stamp_cnt[32];
+__device__ unsigned long long g_stamp_prev;
+#define STAMP(id)                                                            \
+  do {                                                                       \
+    if (T.tid == 0 && blockIdx.x == 0) {                                     \
+      unsigned long long t_ = __builtin_amdgcn_s_memtime();                  \
+      if ((id) >= 0) {                                                       \
+        g_stamp_acc[(id) < 0 ? 0 : (id)] += t_ - g_stamp_prev;               \
+        g_stamp_cnt[(id) < 0 ? 0 : (id)]++;                                  \
+      }                                                                      \
+      g_stamp_prev = t_;                                                     \
+    }                                                                        \
+  } while (0)
+#else
+#define STAMP(id) \
+  do {            \
+  } while (0)
+#endif
 #define FOR_T(v, n) for (int v = T.tid; v < (n); v += T.nt)
+
+// below this many dofs the small factorizations run on lane 0 (fewer LDS round trips)
+constexpr int SERIAL_NV = 12;
 
 __device__ __forceinline__ double tdot(const double* a, const double* b, int n) {
   double r = 0;
@@ -60,6 +86,7 @@ __device__ inline void kinematics(const DevModel& m, const WsLayout& L, const Co
     }
   }
   TSYNC();
+  STAMP(11);
   // the kinematic chain: lane 0
   if (T.tid == 0) {
     xpos[0] = xpos[1] = xpos[2] = 0;
@@ -112,6 +139,7 @@ __device__ inline void kinematics(const DevModel& m, const WsLayout& L, const Co
     }
   }
   TSYNC();
+  STAMP(12);
   // body frames and inertial frames: one lane per body
   FOR_T(i, m.nbody) {
     double xq[4], mat[9], tmp[3], ip[3], iq[4], q2[4];
@@ -134,6 +162,7 @@ __device__ inline void kinematics(const DevModel& m, const WsLayout& L, const Co
     }
   }
   TSYNC();
+  STAMP(13);
   double* gxpos = T.w + L.gxpos;
   double* gxmat = T.w + L.gxmat;
   FOR_T(g, m.ngeom) {
@@ -283,6 +312,22 @@ __device__ inline void factor_ld(const DevModel& m, const CoopAux& X, const Team
     LD[e] = (j <= i) ? mat[e] : 0;
   }
   TSYNC();
+  if (nv <= SERIAL_NV) {
+    // small trees: the oracle's loop on lane 0 beats 4 LDS round trips per k
+    if (T.tid == 0) {
+      for (int k = nv - 1; k >= 0; k--) {
+        if (LD[k * nv + k] < MINVAL) LD[k * nv + k] = MINVAL;
+        for (int i = m.dof_parentid[k]; i >= 0; i = m.dof_parentid[i]) {
+          double tmp = LD[k * nv + i] / LD[k * nv + k];
+          for (int j = i; j >= 0; j = m.dof_parentid[j]) LD[i * nv + j] -= tmp * LD[k * nv + j];
+          LD[k * nv + i] = tmp;
+        }
+      }
+      for (int i = 0; i < nv; i++) diaginv[i] = 1 / LD[i * nv + i];
+    }
+    TSYNC();
+    return;
+  }
   for (int k = nv - 1; k >= 0; k--) {
     if (T.tid == 0 && LD[k * nv + k] < MINVAL) LD[k * nv + k] = MINVAL;
     TSYNC();
@@ -582,7 +627,9 @@ __device__ inline void make_constraint(const DevModel& m, const WsLayout& L, con
 __device__ inline void fwd_position(const DevModel& m, const WsLayout& L, const CoopLayout& C, const CoopAux& X,
                                     const Team& T) {
   kinematics(m, L, C, T);
+  STAMP(14 - 14 + 0);
   com_pos(m, L, T);
+  STAMP(1);
   // transmission: actuator_moment
   double* amom = T.w + L.amom;
   FOR_T(e, m.nu * m.nv) {
@@ -591,9 +638,13 @@ __device__ inline void fwd_position(const DevModel& m, const WsLayout& L, const 
     amom[e] = (k == m.jnt_dofadr[j]) ? m.actuator_gear[i] : 0.0;
   }
   crb(m, L, C, X, T);
+  STAMP(2);
   factor_ld(m, X, T, T.w + L.qM, T.w + L.qLD, T.w + L.qLDinv, T.c + C.ftmp);
+  STAMP(3);
   collision(m, L, C, X, T);
+  STAMP(4);
   make_constraint(m, L, C, X, T);
+  STAMP(5);
 }
 
 // ------------------------------------------------------ velocity stage ---
@@ -836,6 +887,20 @@ __device__ inline void hessian_factor(const DevModel& m, const WsLayout& L, cons
     }
   }
   TSYNC();
+  if (nv <= SERIAL_NV) {
+    if (T.tid == 0) {
+      for (int j = 0; j < nv; j++) {
+        double t = H[j * nv + j];
+        if (j) t -= tdot(H + j * nv, H + j * nv, j);
+        if (t < MINVAL) t = MINVAL;
+        H[j * nv + j] = sqrt(t);
+        t = 1 / H[j * nv + j];
+        for (int i = j + 1; i < nv; i++) H[i * nv + j] = (H[i * nv + j] - tdot(H + i * nv, H + j * nv, j)) * t;
+      }
+    }
+    TSYNC();
+    return;
+  }
   for (int j = 0; j < nv; j++) {
     if (T.tid == 0) {
       double t = H[j * nv + j];
@@ -899,9 +964,11 @@ __device__ inline void solver_newton(const DevModel& m, const WsLayout& L, const
       for (int j = 0; j < nv; j++) search[j] = -search[j];
     }
     TSYNC();
+    STAMP(14);
     FOR_T(i, nv) Mv[i] = tdot(qM + i * nv, search, nv);
     FOR_T(i, ne) Jv[i] = tdot(J + i * nv, search, nv);
     TSYNC();
+    STAMP(15);
     if (T.tid == 0) {
       double alpha = 0;
       double snorm = sqrt(tdot(search, search, nv));
@@ -938,6 +1005,7 @@ __device__ inline void solver_newton(const DevModel& m, const WsLayout& L, const
       bc[3] = alpha;
     }
     TSYNC();
+    STAMP(16);
     const double alpha = bc[3];
     if (alpha == 0) break;
     FOR_T(j, nv) {
@@ -947,6 +1015,7 @@ __device__ inline void solver_newton(const DevModel& m, const WsLayout& L, const
     FOR_T(i, ne) jar[i] += alpha * Jv[i];
     TSYNC();
     iter++;
+    STAMP(17);
     double oldcost = cost;
     ccost = constraint_update(m, L, C, T, jar);
     FOR_T(j, nv) grad[j] = (Ma[j] - qfs[j]) - qc[j];
@@ -961,9 +1030,11 @@ __device__ inline void solver_newton(const DevModel& m, const WsLayout& L, const
       bc[4] = (improvement < tol || gradient < tol) ? 1.0 : 0.0;
     }
     TSYNC();
+    STAMP(18);
     cost = bc[2];
     if (bc[4] != 0) break;
     hessian_factor(m, L, C, T, H);
+    STAMP(19);
   }
 }
 
@@ -1014,10 +1085,18 @@ __device__ inline void fwd_constraint(const DevModel& m, const WsLayout& L, cons
 
 __device__ inline void forward_skip(const DevModel& m, const WsLayout& L, const CoopLayout& C, const CoopAux& X,
                                     const Team& T, int skipstage, int maxiter, double tol) {
+  STAMP(-1);
+  TSYNC();
+  STAMP(20);
+  TSYNC();
+  STAMP(21);
   if (skipstage < STAGE_POS) fwd_position(m, L, C, X, T);
   if (skipstage < STAGE_VEL) fwd_velocity(m, L, C, T);
+  STAMP(6);
   fwd_acceleration(m, L, X, T);
+  STAMP(7);
   fwd_constraint(m, L, C, T, maxiter, tol);
+  STAMP(8);
 }
 
 __device__ inline void integrate_pos(const DevModel& m, const Team& T, double* qpos, const double* qvel, double dt) {
@@ -1178,10 +1257,12 @@ __device__ inline void step(const DevModel& m, const WsLayout& L, const CoopLayo
     reset_data(m, L, T);
     forward_skip(m, L, C, X, T, STAGE_NONE, m.opt_iterations, m.opt_tolerance);
   }
+  STAMP(-1);
   if (m.opt_integrator == 1)
     rk4(m, L, C, X, T, m.opt_iterations, m.opt_tolerance);
   else
     euler(m, L, C, X, T);
+  STAMP(9);
 }
 
 }  // namespace coop

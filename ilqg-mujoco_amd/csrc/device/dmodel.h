@@ -30,6 +30,8 @@ struct DevModel {
 #undef ILQG_DM_FA
 #undef ILQG_DM_IA
   int maxcon, maxefc;
+  const unsigned char* img;  // base of the compact model image (device memory)
+  int img_bytes;             // image size, a multiple of 8
 };
 
 // contact record inside the workspace (doubles, then ints)
@@ -97,6 +99,7 @@ struct CoopLayout {
   int nd;
   int pcnt, rsub, jcnt, ibc;  // ints
   int ni;
+  int imgd;  // doubles of LDS holding the staged model image
 };
 
 inline CoopLayout make_coop_layout(const DevModel& m, int npair) {
@@ -117,6 +120,7 @@ inline CoopLayout make_coop_layout(const DevModel& m, int npair) {
   C.jcnt = oi; oi += 2 * m.njnt;
   C.ibc = oi; oi += 8;
   C.ni = oi;
+  C.imgd = (m.img_bytes + 7) / 8;
   return C;
 }
 

@@ -156,10 +156,8 @@ __device__ inline void rot_vec_quat(double* r, const double* v, const double* q)
   }
 }
 __device__ inline void quat2mat(double* r, const double* q) {
-  if (q[0] == 1 && q[1] == 0 && q[2] == 0 && q[3] == 0) {
-    r[0] = 1; r[1] = 0; r[2] = 0; r[3] = 0; r[4] = 1; r[5] = 0; r[6] = 0; r[7] = 0; r[8] = 1;
-    return;
-  }
+  // MuJoCo's identity shortcut is omitted: for q == (1,0,0,0) the general
+  // formula yields exactly the same doubles, and the branch forced r to scratch.
   double q00 = q[0] * q[0], q01 = q[0] * q[1], q02 = q[0] * q[2], q03 = q[0] * q[3];
   double q11 = q[1] * q[1], q12 = q[1] * q[2], q13 = q[1] * q[3];
   double q22 = q[2] * q[2], q23 = q[2] * q[3], q33 = q[3] * q[3];

@@ -257,8 +257,8 @@ __global__ void k_select(int nq, int nv, int nu, int S, int A, int P, int mode, 
 }
 
 // ---- Riccati backward pass: same loops, same order as oracle/ilqr_ora.c ----
-__device__ void ldlt_factor(int n, double* mat, int* transp) {
-  double temp[32];
+// temp: n doubles of LDS scratch (a private array would live in scratch memory)
+__device__ void ldlt_factor(int n, double* mat, int* transp, double* temp) {
   for (int k = 0; k < n; k++) {
     int big = k;
     double bigv = fabs(mat[k + k * n]);
@@ -311,7 +311,16 @@ __device__ void ldlt_solve(int n, const double* Lm, const int* transp, double* x
   for (int k = n - 1; k >= 0; k--) { double t = x[k]; x[k] = x[transp[k]]; x[transp[k]] = t; }
 }
 
-constexpr int BW_THREADS = 256;
+constexpr int BW_THREADS = 64;  // one wavefront: its barriers compile to nothing
+constexpr int BW_PF = 8;        // prefetch registers per lane: D <= 512
+
+// Three independent fixed-order dot products per lane (ILP 3): each output
+// keeps the oracle's summation order, the three chains overlap in the pipe.
+#define ILP3_BEGIN(n)                                                       \
+  for (int e0 = tid; e0 < (n); e0 += 3 * nt) {                              \
+    const int e1 = e0 + nt, e2 = e0 + 2 * nt;                               \
+    const bool h1 = e1 < (n), h2 = e2 < (n);                                \
+    const int f1 = h1 ? e1 : e0, f2 = h2 ? e2 : e0;
 
 __global__ __launch_bounds__(BW_THREADS) void k_backward(int nq, int nv, int nu, int P, double dt, double mu,
                                                          const double* deriv, TrajDev tr, double* Kg, double* kg,
@@ -342,19 +351,32 @@ __global__ __launch_bounds__(BW_THREADS) void k_backward(int nq, int nv, int nu,
   double* kR = kl + nu;
   double* col = kR + nu;
   double* r = col + nu;
-  int* trn = (int*)(r + nu);
+  double* dl = r + nu;  // FD record of the current step (prefetched)
+  int* trn = (int*)(dl + D);
 
   // initV at the terminal point dArray[0], inc/ilqr.h:100-107
   {
     const double* q0 = deriv + ((size_t)s * P + 0) * D + 2 * nv * nv + nv * nu;
     for (int i = tid; i < nx; i += nt) v[i] = q0[i];
+    const double* d1 = deriv + ((size_t)s * P + (P > 1 ? 1 : 0)) * D;
+    for (int i = tid; i < D; i += nt) dl[i] = d1[i];
     __syncthreads();
     for (int e = tid; e < nx * nx; e += nt) { int i = e % nx, j = e / nx; V[e] = v[i] * v[j]; }
     __syncthreads();
   }
   for (int n = 1; n < P; n++) {
-    const double* dn = deriv + ((size_t)s * P + n) * D;
     const size_t pc = (size_t)s * P + n, pp = pc - 1;
+    // prefetch the next step's FD record; consumed at the end of this step
+    double pf[BW_PF];
+    if (n + 1 < P) {
+      const double* dn1 = deriv + (pc + 1) * D;
+#pragma unroll
+      for (int t = 0; t < BW_PF; t++) {
+        int i = tid + t * nt;
+        pf[t] = i < D ? dn1[i] : 0.0;
+      }
+    }
+    const double* dn = dl;
     // stage 1: symmetrise V, assemble A/B (differentiator.h:66-71,89-92), q, r, c
     for (int e = tid; e < nx * nx; e += nt) {
       int i = e % nx, j = e / nx;
@@ -381,34 +403,45 @@ __global__ __launch_bounds__(BW_THREADS) void k_backward(int nq, int nv, int nu,
     for (int i = tid; i < nx; i += nt) Vs[i + i * nx] += mu;
     __syncthreads();
     // stage 2: T1 = B'V
-    for (int e = tid; e < nu * nx; e += nt) {
-      int a = e % nu, j = e / nu;
-      double sm = 0;
-      for (int kk = 0; kk < nx; kk++) sm += B[kk + a * nx] * Vs[kk + j * nx];
-      T1[e] = sm;
+    ILP3_BEGIN(nu * nx)
+      double s0 = 0, s1 = 0, s2 = 0;
+      const int a0 = e0 % nu, j0 = e0 / nu, a1 = f1 % nu, j1 = f1 / nu, a2 = f2 % nu, j2 = f2 / nu;
+      for (int kk = 0; kk < nx; kk++) {
+        s0 += B[kk + a0 * nx] * Vs[kk + j0 * nx];
+        s1 += B[kk + a1 * nx] * Vs[kk + j1 * nx];
+        s2 += B[kk + a2 * nx] * Vs[kk + j2 * nx];
+      }
+      T1[e0] = s0;
+      if (h1) T1[e1] = s1;
+      if (h2) T1[e2] = s2;
     }
     __syncthreads();
-    // stage 3: Mm = -2 T1 B - 2R ; T3 = T1 A
+    // stage 3: Mm = -2 T1 B - 2R ; T3 = T1 A ; w = v + 2 V c
     for (int e = tid; e < nu * nu; e += nt) {
       int a = e % nu, b = e / nu;
       double sm = 0;
       for (int kk = 0; kk < nx; kk++) sm += T1[a + kk * nu] * B[kk + b * nx];
       Mm[e] = -2 * sm - 2 * (r[a] * r[b]);
     }
-    for (int e = tid; e < nu * nx; e += nt) {
-      int a = e % nu, j = e / nu;
-      double sm = 0;
-      for (int kk = 0; kk < nx; kk++) sm += T1[a + kk * nu] * A[kk + j * nx];
-      T3[e] = sm;
+    ILP3_BEGIN(nu * nx)
+      double s0 = 0, s1 = 0, s2 = 0;
+      const int a0 = e0 % nu, j0 = e0 / nu, a1 = f1 % nu, j1 = f1 / nu, a2 = f2 % nu, j2 = f2 / nu;
+      for (int kk = 0; kk < nx; kk++) {
+        s0 += T1[a0 + kk * nu] * A[kk + j0 * nx];
+        s1 += T1[a1 + kk * nu] * A[kk + j1 * nx];
+        s2 += T1[a2 + kk * nu] * A[kk + j2 * nx];
+      }
+      T3[e0] = s0;
+      if (h1) T3[e1] = s1;
+      if (h2) T3[e2] = s2;
     }
-    // w = v + 2 V c
     for (int i = tid; i < nx; i += nt) {
       double sm = 0;
       for (int j = 0; j < nx; j++) sm += Vs[i + j * nx] * c[j];
       w[i] = v[i] + 2 * sm;
     }
     __syncthreads();
-    if (tid == 0) ldlt_factor(nu, Mm, trn);
+    if (tid == 0) ldlt_factor(nu, Mm, trn, y);  // y is free until stage 5
     for (int a = tid; a < nu; a += nt) {
       double sm = 0;
       for (int kk = 0; kk < nx; kk++) sm += B[kk + a * nx] * w[kk];
@@ -417,19 +450,16 @@ __global__ __launch_bounds__(BW_THREADS) void k_backward(int nq, int nv, int nu,
     __syncthreads();
     // stage 4: K = ldlt.solve(2 T3) column-parallel; k = ldlt.solve(B'w + r)
     for (int j = tid; j < nx + 1; j += nt) {
-      double x[32];
-      if (j < nx) {
+      // solved in place in LDS (a private array would live in scratch)
+      double* x = j < nx ? Kl + j * nu : kl;
+      if (j < nx)
         for (int a = 0; a < nu; a++) x[a] = 2 * T3[a + j * nu];
-        ldlt_solve(nu, Mm, trn, x);
-        for (int a = 0; a < nu; a++) Kl[a + j * nu] = x[a];
-      } else {
+      else
         for (int a = 0; a < nu; a++) x[a] = col[a];
-        ldlt_solve(nu, Mm, trn, x);
-        for (int a = 0; a < nu; a++) kl[a] = x[a];
-      }
+      ldlt_solve(nu, Mm, trn, x);
     }
     __syncthreads();
-    // stage 5: ABK = A + B K
+    // stage 5: ABK = A + B K ; T6 = K'R ; y = Bk + c ; kR = k'R
     for (int e = tid; e < nx * nx; e += nt) {
       int i = e % nx, j = e / nx;
       double sm = 0;
@@ -454,20 +484,36 @@ __global__ __launch_bounds__(BW_THREADS) void k_backward(int nq, int nv, int nu,
     }
     __syncthreads();
     // stage 6: T4 = ABK' V
-    for (int e = tid; e < nx * nx; e += nt) {
-      int i = e % nx, j = e / nx;
-      double sm = 0;
-      for (int kk = 0; kk < nx; kk++) sm += ABK[kk + i * nx] * Vs[kk + j * nx];
-      T4[e] = sm;
+    ILP3_BEGIN(nx * nx)
+      double s0 = 0, s1 = 0, s2 = 0;
+      const int i0 = e0 % nx, j0 = e0 / nx, i1 = f1 % nx, j1 = f1 / nx, i2 = f2 % nx, j2 = f2 / nx;
+      for (int kk = 0; kk < nx; kk++) {
+        s0 += ABK[kk + i0 * nx] * Vs[kk + j0 * nx];
+        s1 += ABK[kk + i1 * nx] * Vs[kk + j1 * nx];
+        s2 += ABK[kk + i2 * nx] * Vs[kk + j2 * nx];
+      }
+      T4[e0] = s0;
+      if (h1) T4[e1] = s1;
+      if (h2) T4[e2] = s2;
     }
     __syncthreads();
     // stage 7: V_new = (T4 ABK + Q) + T6 K
-    for (int e = tid; e < nx * nx; e += nt) {
-      int i = e % nx, j = e / nx;
-      double s5 = 0, s7 = 0;
-      for (int kk = 0; kk < nx; kk++) s5 += T4[i + kk * nx] * ABK[kk + j * nx];
-      for (int b = 0; b < nu; b++) s7 += T6[i + b * nx] * Kl[b + j * nu];
-      Vn[e] = (s5 + q[i] * q[j]) + s7;
+    ILP3_BEGIN(nx * nx)
+      double a0s = 0, a1s = 0, a2s = 0, b0s = 0, b1s = 0, b2s = 0;
+      const int i0 = e0 % nx, j0 = e0 / nx, i1 = f1 % nx, j1 = f1 / nx, i2 = f2 % nx, j2 = f2 / nx;
+      for (int kk = 0; kk < nx; kk++) {
+        a0s += T4[i0 + kk * nx] * ABK[kk + j0 * nx];
+        a1s += T4[i1 + kk * nx] * ABK[kk + j1 * nx];
+        a2s += T4[i2 + kk * nx] * ABK[kk + j2 * nx];
+      }
+      for (int b = 0; b < nu; b++) {
+        b0s += T6[i0 + b * nx] * Kl[b + j0 * nu];
+        b1s += T6[i1 + b * nx] * Kl[b + j1 * nu];
+        b2s += T6[i2 + b * nx] * Kl[b + j2 * nu];
+      }
+      Vn[e0] = (a0s + q[i0] * q[j0]) + b0s;
+      if (h1) Vn[e1] = (a1s + q[i1] * q[j1]) + b1s;
+      if (h2) Vn[e2] = (a2s + q[i2] * q[j2]) + b2s;
     }
     __syncthreads();
     // stage 8: z = (2y)' V_new ; v_new (reads the NEW V, Q14)
@@ -479,8 +525,10 @@ __global__ __launch_bounds__(BW_THREADS) void k_backward(int nq, int nv, int nu,
     __syncthreads();
     for (int j = tid; j < nx; j += nt) {
       double ta = 0, tb = 0, td = 0;
-      for (int i = 0; i < nx; i++) ta += z[i] * ABK[i + j * nx];
-      for (int i = 0; i < nx; i++) tb += v[i] * ABK[i + j * nx];
+      for (int i = 0; i < nx; i++) {
+        ta += z[i] * ABK[i + j * nx];
+        tb += v[i] * ABK[i + j * nx];
+      }
       for (int b = 0; b < nu; b++) td += (2 * kR[b]) * Kl[b + j * nu];
       vn[j] = ((ta + tb) + q[j]) + td;
     }
@@ -490,6 +538,13 @@ __global__ __launch_bounds__(BW_THREADS) void k_backward(int nq, int nv, int nu,
     __syncthreads();
     for (int e = tid; e < nx * nx; e += nt) V[e] = Vn[e];
     for (int i = tid; i < nx; i += nt) v[i] = vn[i];
+    if (n + 1 < P) {
+#pragma unroll
+      for (int t = 0; t < BW_PF; t++) {
+        int i = tid + t * nt;
+        if (i < D) dl[i] = pf[t];
+      }
+    }
     __syncthreads();
   }
   if (Vg)
@@ -532,7 +587,8 @@ inline int nblk(long n, int b) { return (int)((n + b - 1) / b); }
 
 size_t backward_lds_bytes(int nv, int nu) {
   const int nx = 2 * nv;
-  size_t nd = 6 * (size_t)nx * nx + 5 * (size_t)nx * nu + (size_t)nu * nu + 8 * (size_t)nx + 4 * (size_t)nu;
+  const size_t D = (size_t)nv * (2 * nv + nu) + 2 * nv + nu;
+  size_t nd = 6 * (size_t)nx * nx + 5 * (size_t)nx * nu + (size_t)nu * nu + 8 * (size_t)nx + 4 * (size_t)nu + D;
   return nd * sizeof(double) + (size_t)nu * sizeof(int) + 16;
 }
 

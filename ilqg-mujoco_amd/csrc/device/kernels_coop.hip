@@ -16,16 +16,39 @@ constexpr int FD_NITER = 30;     // mjderivative.cpp:37
 constexpr int FD_NWARMUP = 3;    // mjderivative.cpp:38
 constexpr int TEAM = 64;
 
+// LDS: [workspace doubles][coop doubles][model image][workspace ints][coop ints]
 __device__ inline Team make_team(const WsLayout& L, const CoopLayout& C) {
   extern __shared__ double lds[];
   Team T;
   T.w = lds;
   T.c = lds + L.nd;
-  T.iw = reinterpret_cast<int*>(lds + L.nd + C.nd);
+  T.iw = reinterpret_cast<int*>(lds + L.nd + C.nd + C.imgd);
   T.ci = T.iw + L.ni;
   T.tid = threadIdx.x;
   T.nt = blockDim.x;
   return T;
+}
+
+// Stage the read-only model image into LDS (one coalesced copy) and return a
+// DevModel / CoopAux whose array pointers address the LDS copy: every model
+// read on the serial paths then costs an LDS round trip instead of an L2 one.
+__device__ inline void stage_model(const DevModel& g, const CoopAux& Xg, const WsLayout& L, const CoopLayout& C,
+                                   const Team& T, DevModel& m, CoopAux& X) {
+  extern __shared__ double lds[];
+  double* dst = lds + L.nd + C.nd;
+  const double* src = reinterpret_cast<const double*>(g.img);
+  FOR_T(w, C.imgd) dst[w] = src[w];
+  const unsigned char* base = reinterpret_cast<const unsigned char*>(dst);
+  m = g;
+#define ILQG_RB(nm, cnt) \
+  m.nm = reinterpret_cast<decltype(m.nm)>(base + (reinterpret_cast<const unsigned char*>(g.nm) - g.img));
+  ILQG_MODEL_F64_ARRAYS(ILQG_RB)
+  ILQG_MODEL_I32_ARRAYS(ILQG_RB)
+#undef ILQG_RB
+  X.isanc = reinterpret_cast<const int*>(base + (reinterpret_cast<const unsigned char*>(Xg.isanc) - g.img));
+  X.pair = reinterpret_cast<const int*>(base + (reinterpret_cast<const unsigned char*>(Xg.pair) - g.img));
+  X.npair = Xg.npair;
+  TSYNC();
 }
 
 __device__ inline double cost_terms(double c, const double* x, const double* w, const double* t, const double* l,
@@ -64,12 +87,15 @@ __device__ inline void load_state(const DevModel& m, const WsLayout& L, const Te
   TSYNC();
 }
 
-__global__ __launch_bounds__(TEAM) void k_fd_centre_coop(DevModel m, WsLayout L, CoopLayout C, CoopAux X, TrajDev tr,
+__global__ __launch_bounds__(TEAM) void k_fd_centre_coop(DevModel mg, WsLayout L, CoopLayout C, CoopAux Xg, TrajDev tr,
                                                          int P, const double* qfrc_applied,
                                                          const double* xfrc_applied, CostDev cost, double* warm_c,
                                                          double* cost_c) {
-  const int pt = blockIdx.x;
   Team T = make_team(L, C);
+  DevModel m;
+  CoopAux X;
+  stage_model(mg, Xg, L, C, T, m, X);
+  const int pt = blockIdx.x;
   load_state(m, L, T, tr, pt, pt / P, qfrc_applied, xfrc_applied);
   forward_skip(m, L, C, X, T, STAGE_NONE, FD_NITER, 0.0);
   for (int rep = 1; rep < FD_NWARMUP; rep++) forward_skip(m, L, C, X, T, STAGE_VEL, FD_NITER, 0.0);
@@ -79,15 +105,18 @@ __global__ __launch_bounds__(TEAM) void k_fd_centre_coop(DevModel m, WsLayout L,
                            tr.ctrl + (size_t)pt * m.nu);
 }
 
-__global__ __launch_bounds__(TEAM) void k_fd_cols_coop(DevModel m, WsLayout L, CoopLayout C, CoopAux X, TrajDev tr,
+__global__ __launch_bounds__(TEAM) void k_fd_cols_coop(DevModel mg, WsLayout L, CoopLayout C, CoopAux Xg, TrajDev tr,
                                                        int P, const double* qfrc_applied, const double* xfrc_applied,
                                                        CostDev cost, const double* warm_c, const double* cost_c,
                                                        double* deriv) {
+  Team T = make_team(L, C);
+  DevModel m;
+  CoopAux X;
+  stage_model(mg, Xg, L, C, T, m, X);
   const int nv = m.nv, nu = m.nu;
   const int nctrl = nu < nv ? nu : nv;  // mjderivative.cpp:78-82 (assumes nv >= nu)
   const int ncol = nctrl + 2 * nv;
   const int pt = blockIdx.x / ncol, col = blockIdx.x % ncol;
-  Team T = make_team(L, C);
   const int D = nv * (2 * nv + nu) + 2 * nv + nu;
   double* dr = deriv + (size_t)pt * D;
   const double* wc = warm_c + (size_t)pt * nv;
@@ -165,16 +194,19 @@ __global__ __launch_bounds__(TEAM) void k_fd_cols_coop(DevModel m, WsLayout L, C
   }
 }
 
-__global__ __launch_bounds__(TEAM) void k_rollout_coop(DevModel m, WsLayout L, CoopLayout C, CoopAux X, int S, int A,
+__global__ __launch_bounds__(TEAM) void k_rollout_coop(DevModel mg, WsLayout L, CoopLayout C, CoopAux Xg, int S, int A,
                                                        int P, TrajDev nom, TrajDev out, int out_is_cand,
                                                        const double* K, const double* k, const double* alphas,
                                                        TrajDev dinit, const double* qfrc_applied,
                                                        const double* xfrc_applied, int passive, CostDev cost,
                                                        double* cost_cand) {
+  Team T = make_team(L, C);
+  DevModel m;
+  CoopAux X;
+  stage_model(mg, Xg, L, C, T, m, X);
   const int lane = blockIdx.x;
   const int s = lane / A, a = lane % A;
   const int nq = m.nq, nv = m.nv, nu = m.nu, nx = 2 * nv;
-  Team T = make_team(L, C);
   load_state(m, L, T, dinit, s, s, qfrc_applied, xfrc_applied);
   double* qpos = T.w + L.qpos;
   double* qvel = T.w + L.qvel;
@@ -228,7 +260,7 @@ hipError_t allow_lds(K kern, size_t lds) {
 }  // namespace
 
 size_t coop_lds_bytes(const WsLayout& L, const CoopLayout& C) {
-  return (size_t)(L.nd + C.nd) * sizeof(double) + (size_t)(L.ni + C.ni) * sizeof(int);
+  return (size_t)(L.nd + C.nd + C.imgd) * sizeof(double) + (size_t)(L.ni + C.ni) * sizeof(int);
 }
 
 hipError_t launch_fd_centre_coop(const DevModel& m, const WsLayout& L, const CoopLayout& C, const CoopAux& X,
@@ -269,3 +301,18 @@ hipError_t launch_rollout_coop(const DevModel& m, const WsLayout& L, const CoopL
 }
 
 }  // namespace ilqg
+
+#ifdef ILQG_STAMPS
+extern "C" int ilqg_debug_stamps(unsigned long long* acc, unsigned long long* cnt, int reset) {
+  if (hipMemcpyFromSymbol(acc, HIP_SYMBOL(ilqg::coop::g_stamp_acc), sizeof(unsigned long long) * 32) != hipSuccess)
+    return 3;
+  if (hipMemcpyFromSymbol(cnt, HIP_SYMBOL(ilqg::coop::g_stamp_cnt), sizeof(unsigned long long) * 32) != hipSuccess)
+    return 3;
+  if (reset) {
+    unsigned long long z[32] = {0};
+    (void)hipMemcpyToSymbol(HIP_SYMBOL(ilqg::coop::g_stamp_acc), z, sizeof(z));
+    (void)hipMemcpyToSymbol(HIP_SYMBOL(ilqg::coop::g_stamp_cnt), z, sizeof(z));
+  }
+  return 0;
+}
+#endif

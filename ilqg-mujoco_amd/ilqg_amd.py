@@ -24,7 +24,7 @@ from typing import Optional, Sequence
 import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "lib", "libilqg_amd.so")
+LIB_PATH = os.environ.get("ILQG_LIB") or os.path.join(_HERE, "lib", "libilqg_amd.so")
 
 _c_double_p = ctypes.POINTER(ctypes.c_double)
 _c_int_p = ctypes.POINTER(ctypes.c_int)

@@ -1,0 +1,27 @@
+"""Per-stage cycle breakdown of the cooperative physics (diagnostic build).
+ILQG_LIB=ilqg-mujoco_amd/lib/libilqg_amd_diag.so python tools/stamps.py"""
+import ctypes, os, sys
+import numpy as np
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "ilqg-mujoco_amd"))
+import ilqg_amd as ia, workloads
+NAMES = {0: "kinematics", 1: "com_pos", 2: "trn+crb", 3: "factor_ld(M)", 4: "collision", 5: "make_constraint",
+         6: "fwd_velocity", 7: "fwd_acceleration", 8: "fwd_constraint(newton)", 9: "integrator",
+         11: " kin: joint quats", 12: " kin: lane-0 chain", 13: " kin: body frames", 14: " nt: chol solve",
+         15: " nt: Mv,Jv", 16: " nt: linesearch", 17: " nt: update", 18: " nt: cost+grad", 19: " nt: hessian",
+         20: "empty sync", 21: "empty sync 2"}
+L = ia.lib()
+acc = (ctypes.c_ulonglong * 32)(); cnt = (ctypes.c_ulonglong * 32)()
+m = ia.Model.load(workloads.model_file(sys.argv[1] if len(sys.argv) > 1 else "hopper"))
+dmain = workloads.hopper_dmain(m, 1) if m.nv == 6 else workloads.pendulum_dmain(m, 1)
+g = ia.ILQR(m, dmain, 500 if m.nv == 6 else 200, ia.HOPPER_COST if m.nv == 6 else ia.PENDULUM_COST)
+g.iterate(); g.synchronize()
+for what, fn in (("rollout (1 seed)", g.forward_pass), ("fd sweep", g.fd_sweep)):
+    L.ilqg_debug_stamps(acc, cnt, 1)
+    fn(); g.synchronize()
+    L.ilqg_debug_stamps(acc, cnt, 1)
+    tot = sum(acc[i] for i in range(10))
+    print(f"== {what}: block 0, lane 0, total {tot} cycles")
+    for i in range(22):
+        if cnt[i]:
+            print(f"  {NAMES[i]:24s} calls {cnt[i]:6d}  cycles/call {acc[i]/cnt[i]:9.0f}  share {acc[i]/max(tot,1):6.1%}")
