@@ -114,6 +114,12 @@ struct ilqg_model {
     std::vector<int> isanc(h.nv * h.nv, 0), pairs;
     for (int i = 0; i < h.nv; i++)
       for (int j = i; j >= 0; j = h.dof_parentid[j]) isanc[i * h.nv + j] = 1;
+    // proper-ancestor bitmask per dof (nv <= 64): the serial tree recursions
+    // visit set bits from the highest down, i.e. MuJoCo's parent-chase order
+    std::vector<unsigned long long> pmask(h.nv, 0);
+    if (h.nv <= 64)
+      for (int i = 0; i < h.nv; i++)
+        for (int j = h.dof_parentid[i]; j >= 0; j = h.dof_parentid[j]) pmask[i] |= 1ull << j;
     for (int g1 = 0; g1 < h.ngeom; g1++)
       for (int g2 = g1 + 1; g2 < h.ngeom; g2++) {
         int b1 = h.geom_bodyid[g1], b2 = h.geom_bodyid[g2];
@@ -148,6 +154,7 @@ struct ilqg_model {
     ILQG_MODEL_I32_ARRAYS(ILQG_CP_I)
     size_t isanc_at = put(isanc.data(), isanc.size() * 4, nullptr);
     size_t pair_at = put(pairs.data(), pairs.size() * 4, nullptr);
+    size_t pmask_at = put(pmask.data(), pmask.size() * 8, nullptr);
     img.resize(img.size() + 8, 0);
     HIPCHK(buf.alloc(img.size()));
     HIPCHK(hipMemcpy(buf.p, img.data(), img.size(), hipMemcpyHostToDevice));
@@ -164,6 +171,8 @@ struct ilqg_model {
     X.isanc = reinterpret_cast<const int*>(static_cast<unsigned char*>(buf.p) + isanc_at);
     X.pair = reinterpret_cast<const int*>(static_cast<unsigned char*>(buf.p) + pair_at);
     X.npair = npair;
+    X.pmask = h.nv <= 64 ? reinterpret_cast<const unsigned long long*>(static_cast<unsigned char*>(buf.p) + pmask_at)
+                         : nullptr;
     C = coop::make_coop_layout(dm, npair);
     if (!stream) HIPCHK(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
     dev = device;

@@ -11,6 +11,7 @@
 #pragma once
 
 #include "dphys.h"
+#include "dsmall.h"
 
 namespace ilqg {
 namespace coop {
@@ -307,6 +308,10 @@ __device__ inline void crb(const DevModel& m, const WsLayout& L, const CoopLayou
 __device__ inline void factor_ld(const DevModel& m, const CoopAux& X, const Team& T, const double* mat, double* LD,
                                  double* diaginv, double* tmpv) {
   const int nv = m.nv;
+  if (nv <= RMAX && X.pmask) {
+    factor_ld_rows(nv, X.pmask, T.tid, mat, LD, diaginv);
+    return;
+  }
   FOR_T(e, nv * nv) {
     int i = e / nv, j = e % nv;
     LD[e] = (j <= i) ? mat[e] : 0;
@@ -315,12 +320,32 @@ __device__ inline void factor_ld(const DevModel& m, const CoopAux& X, const Team
   if (nv <= SERIAL_NV) {
     // small trees: the oracle's loop on lane 0 beats 4 LDS round trips per k
     if (T.tid == 0) {
-      for (int k = nv - 1; k >= 0; k--) {
-        if (LD[k * nv + k] < MINVAL) LD[k * nv + k] = MINVAL;
-        for (int i = m.dof_parentid[k]; i >= 0; i = m.dof_parentid[i]) {
-          double tmp = LD[k * nv + i] / LD[k * nv + k];
-          for (int j = i; j >= 0; j = m.dof_parentid[j]) LD[i * nv + j] -= tmp * LD[k * nv + j];
-          LD[k * nv + i] = tmp;
+      if (X.pmask) {
+        // ancestor bitmasks replace the dependent parent-pointer chase
+        for (int k = nv - 1; k >= 0; k--) {
+          if (LD[k * nv + k] < MINVAL) LD[k * nv + k] = MINVAL;
+          const double dk = LD[k * nv + k];
+          for (unsigned long long mi = X.pmask[k]; mi;) {
+            const int i = 63 - __builtin_clzll(mi);
+            mi &= ~(1ull << i);
+            double tmp = LD[k * nv + i] / dk;
+            // the ancestors of k below i are exactly i's ancestors (one root path)
+            for (unsigned long long mj = mi | (1ull << i); mj;) {
+              const int j = 63 - __builtin_clzll(mj);
+              mj &= ~(1ull << j);
+              LD[i * nv + j] -= tmp * LD[k * nv + j];
+            }
+            LD[k * nv + i] = tmp;
+          }
+        }
+      } else {
+        for (int k = nv - 1; k >= 0; k--) {
+          if (LD[k * nv + k] < MINVAL) LD[k * nv + k] = MINVAL;
+          for (int i = m.dof_parentid[k]; i >= 0; i = m.dof_parentid[i]) {
+            double tmp = LD[k * nv + i] / LD[k * nv + k];
+            for (int j = i; j >= 0; j = m.dof_parentid[j]) LD[i * nv + j] -= tmp * LD[k * nv + j];
+            LD[k * nv + i] = tmp;
+          }
         }
       }
       for (int i = 0; i < nv; i++) diaginv[i] = 1 / LD[i * nv + i];
@@ -350,17 +375,44 @@ __device__ inline void factor_ld(const DevModel& m, const CoopAux& X, const Team
 }
 
 // oracle solve_ld on lane 0 (ends with a barrier)
-__device__ inline void solve_ld(const DevModel& m, const Team& T, const double* LD, const double* diaginv, double* x) {
+__device__ inline void solve_ld(const DevModel& m, const CoopAux& X, const Team& T, const double* LD,
+                                const double* diaginv, double* x) {
   const int nv = m.nv;
+  if (nv <= RMAX && X.pmask) {
+    solve_ld_rows(nv, X.pmask, T.tid, LD, diaginv, x);
+    return;
+  }
   if (T.tid == 0) {
-    for (int i = nv - 1; i >= 0; i--) {
-      double tmp = x[i];
-      if (tmp != 0)
-        for (int j = m.dof_parentid[i]; j >= 0; j = m.dof_parentid[j]) x[j] -= LD[i * nv + j] * tmp;
+    if (X.pmask) {
+      for (int i = nv - 1; i >= 0; i--) {
+        double tmp = x[i];
+        if (tmp != 0)
+          for (unsigned long long mj = X.pmask[i]; mj;) {
+            const int j = 63 - __builtin_clzll(mj);
+            mj &= ~(1ull << j);
+            x[j] -= LD[i * nv + j] * tmp;
+          }
+      }
+      for (int i = 0; i < nv; i++) x[i] *= diaginv[i];
+      for (int i = 0; i < nv; i++) {
+        double xi = x[i];
+        for (unsigned long long mj = X.pmask[i]; mj;) {
+          const int j = 63 - __builtin_clzll(mj);
+          mj &= ~(1ull << j);
+          xi -= LD[i * nv + j] * x[j];
+        }
+        x[i] = xi;
+      }
+    } else {
+      for (int i = nv - 1; i >= 0; i--) {
+        double tmp = x[i];
+        if (tmp != 0)
+          for (int j = m.dof_parentid[i]; j >= 0; j = m.dof_parentid[j]) x[j] -= LD[i * nv + j] * tmp;
+      }
+      for (int i = 0; i < nv; i++) x[i] *= diaginv[i];
+      for (int i = 0; i < nv; i++)
+        for (int j = m.dof_parentid[i]; j >= 0; j = m.dof_parentid[j]) x[i] -= LD[i * nv + j] * x[j];
     }
-    for (int i = 0; i < nv; i++) x[i] *= diaginv[i];
-    for (int i = 0; i < nv; i++)
-      for (int j = m.dof_parentid[i]; j >= 0; j = m.dof_parentid[j]) x[i] -= LD[i * nv + j] * x[j];
   }
   TSYNC();
 }
@@ -829,7 +881,7 @@ __device__ inline void fwd_acceleration(const DevModel& m, const WsLayout& L, co
     qs[j] = v;
   }
   TSYNC();
-  solve_ld(m, T, T.w + L.qLD, T.w + L.qLDinv, qs);
+  solve_ld(m, X, T, T.w + L.qLD, T.w + L.qLDinv, qs);
 }
 
 // constraint cost of residuals `jar`; force/state per row, qfrc_constraint per dof
@@ -887,6 +939,10 @@ __device__ inline void hessian_factor(const DevModel& m, const WsLayout& L, cons
     }
   }
   TSYNC();
+  if (nv <= RMAX) {
+    cholesky_rows(nv, T.tid, H);
+    return;
+  }
   if (nv <= SERIAL_NV) {
     if (T.tid == 0) {
       for (int j = 0; j < nv; j++) {
@@ -951,19 +1007,23 @@ __device__ inline void solver_newton(const DevModel& m, const WsLayout& L, const
   int iter = 0;
   while (iter < maxiter) {
     // search = -H^-1 grad ; line search ; all on lane 0 except the parallel products
-    if (T.tid == 0) {
-      for (int i = 0; i < nv; i++) search[i] = grad[i];
-      for (int i = 0; i < nv; i++) {
-        if (i) search[i] -= tdot(H + i * nv, search, i);
-        search[i] /= H[i * nv + i];
+    if (nv <= RMAX) {
+      chol_solve_rows(nv, T.tid, H, grad, search);
+    } else {
+      if (T.tid == 0) {
+        for (int i = 0; i < nv; i++) search[i] = grad[i];
+        for (int i = 0; i < nv; i++) {
+          if (i) search[i] -= tdot(H + i * nv, search, i);
+          search[i] /= H[i * nv + i];
+        }
+        for (int i = nv - 1; i >= 0; i--) {
+          for (int j = i + 1; j < nv; j++) search[i] -= H[j * nv + i] * search[j];
+          search[i] /= H[i * nv + i];
+        }
+        for (int j = 0; j < nv; j++) search[j] = -search[j];
       }
-      for (int i = nv - 1; i >= 0; i--) {
-        for (int j = i + 1; j < nv; j++) search[i] -= H[j * nv + i] * search[j];
-        search[i] /= H[i * nv + i];
-      }
-      for (int j = 0; j < nv; j++) search[j] = -search[j];
+      TSYNC();
     }
-    TSYNC();
     STAMP(14);
     FOR_T(i, nv) Mv[i] = tdot(qM + i * nv, search, nv);
     FOR_T(i, ne) Jv[i] = tdot(J + i * nv, search, nv);
@@ -1172,7 +1232,7 @@ __device__ inline void euler(const DevModel& m, const WsLayout& L, const CoopLay
     }
     TSYNC();
     factor_ld(m, X, T, qH, qHLD, qHinv, T.c + C.ftmp);
-    solve_ld(m, T, qHLD, qHinv, qacc);
+    solve_ld(m, X, T, qHLD, qHinv, qacc);
   }
   const double h = m.opt_timestep;
   FOR_T(i, nv) qvel[i] += qacc[i] * h;

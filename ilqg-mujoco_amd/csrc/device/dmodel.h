@@ -129,6 +129,7 @@ struct CoopAux {
   const int* isanc;  // nv*nv: isanc[i*nv+j] = 1 if dof j is dof i or an ancestor of it
   const int* pair;   // 2*npair: geom pairs passing the static collision filters, oracle order
   int npair;
+  const unsigned long long* pmask;  // nv: proper-ancestor bitmask of each dof (null if nv > 64)
 };
 
 }  // namespace coop

@@ -1,0 +1,246 @@
+// Register-resident small-matrix kernels for one wavefront (nv <= RMAX).
+//
+// The serial recursions of the physics pipeline -- MuJoCo's tree L'DL of the
+// mass matrix, its solve, the dense Cholesky of the Newton Hessian and the
+// search-direction solve -- ran on lane 0 out of LDS, paying an LDS round trip
+// (~64-140 cycles on gfx950) per dependent access.  Here lane t holds row t
+// (and, for the solves, column t) of the matrix in VGPRs; the row needed by
+// step k is broadcast with v_readlane (k is wave-uniform), so the divisions
+// and row updates of one step run on all lanes at once.
+//
+// Bit-exactness: every matrix entry still receives exactly the same sequence
+// of IEEE operations as in the oracle's serial loops (oracle/mjsub.c
+// factor_ld / solve_ld / the Newton Cholesky): updates to entry (i,j) happen
+// in the same k order, dot products keep ascending index order, and every
+// division is the same operand pair.  Only independent work is overlapped.
+#pragma once
+
+#include <type_traits>
+
+#include "dphys.h"
+
+namespace ilqg {
+namespace coop {
+
+using dev::MINVAL;
+constexpr int RMAX = 8;  // register rows up to this many dofs
+
+// compile-time loop: f(std::integral_constant<int, I>) for I = B .. E-1, so
+// every register-array index is a constant (no scratch, no select chains)
+template <int B, int E, typename F>
+__device__ __forceinline__ void sfor(F&& f) {
+  if constexpr (B < E) {
+    f(std::integral_constant<int, B>{});
+    sfor<B + 1, E>(f);
+  }
+}
+#define SK(v) decltype(v)::value
+#define SLAM(v) [&](auto v) __attribute__((always_inline))
+
+// v_readlane of a double from a wave-uniform lane
+__device__ __forceinline__ double bcast(double x, int lane) {
+  long long b = __double_as_longlong(x);
+  int lo = __builtin_amdgcn_readlane((int)(b & 0xffffffffll), lane);
+  int hi = __builtin_amdgcn_readlane((int)(b >> 32), lane);
+  return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
+}
+
+// r[idx] for a per-lane index: select chain over constant indices (written
+// with sfor so SROA sees constant subscripts and keeps r in registers)
+__device__ __forceinline__ double rsel(const double (&r)[RMAX], int idx) {
+  double v = r[0];
+  sfor<1, RMAX>(SLAM(jj) { v = (idx == SK(jj)) ? r[SK(jj)] : v; });
+  return v;
+}
+
+// Tree L'DL factorization of the lower triangle of `mat` (nv x nv, row-major)
+// into LD (full nv x nv, zero upper) and diaginv.  pmask[i]: proper ancestors
+// of dof i.  Mirrors coop::factor_ld's serial loop entry by entry.
+__device__ inline void factor_ld_rows(int nv, const unsigned long long* pmask, int tid, const double* mat, double* LD,
+                                      double* diaginv) {
+  double r[RMAX];
+  unsigned long long pm[RMAX];  // wave-uniform ancestor masks, loaded up front
+  const bool own = tid < nv;
+  sfor<0, RMAX>(SLAM(jj) {
+    constexpr int j = SK(jj);
+    r[j] = (own && j < nv && j <= tid) ? mat[tid * nv + j] : 0.0;
+    pm[j] = j < nv ? pmask[j] : 0ull;
+  });
+  const unsigned long long self = own ? (pmask[tid] | (1ull << tid)) : 0ull;  // {t} u anc(t)
+  __syncthreads();  // all rows read before LD (may alias mat) is written
+  sfor<0, RMAX>(SLAM(kk) {
+    constexpr int k = RMAX - 1 - SK(kk);
+    if (k >= nv) return;
+    const unsigned long long ak = pm[k];
+    double dk = bcast(r[k], k);
+    if (dk < MINVAL) dk = MINVAL;
+    double rk[RMAX];
+    sfor<0, RMAX>(SLAM(jj) {
+      constexpr int j = SK(jj);
+      rk[j] = (j <= k) ? bcast(r[j], k) : 0.0;
+    });
+    // lanes i in anc(k): tmp_i = LD[k][i] / LD[k][k]; row i -= tmp_i * row k
+    double tmp = 0;
+    if (own && ((ak >> tid) & 1)) {
+      tmp = rsel(rk, tid) / dk;
+      sfor<0, k>(SLAM(jj) {
+        constexpr int j = SK(jj);
+        if ((self >> j) & 1) r[j] -= tmp * rk[j];
+      });
+    }
+    // lane k: LD[k][i] = tmp_i (the same quotient, gathered) and the clamp
+    sfor<0, k>(SLAM(ii) {
+      constexpr int i = SK(ii);
+      if ((ak >> i) & 1) {
+        const double ti = bcast(tmp, i);
+        if (tid == k) r[i] = ti;
+      }
+    });
+    if (tid == k) r[k] = dk;
+  });
+  if (own) {
+    sfor<0, RMAX>(SLAM(jj) {
+      if (SK(jj) < nv) LD[tid * nv + SK(jj)] = r[SK(jj)];
+    });
+    diaginv[tid] = 1 / rsel(r, tid);
+  }
+  __syncthreads();
+}
+
+// x <- (L'DL)^-1 x for the factor above; mirrors coop::solve_ld.
+__device__ inline void solve_ld_rows(int nv, const unsigned long long* pmask, int tid, const double* LD,
+                                     const double* diaginv, double* x) {
+  const bool own = tid < nv;
+  double row[RMAX], col[RMAX], xt = 0, dinv = 0;
+  unsigned long long anc = 0;
+  sfor<0, RMAX>(SLAM(jj) {
+    constexpr int j = SK(jj);
+    row[j] = (own && j < nv) ? LD[tid * nv + j] : 0.0;
+    col[j] = (own && j < nv) ? LD[j * nv + tid] : 0.0;
+  });
+  if (own) {
+    xt = x[tid];
+    dinv = diaginv[tid];
+    anc = pmask[tid];
+  }
+  // x[j] -= LD[i][j] * x[i] for j in anc(i), i descending (skipped when x[i] == 0)
+  sfor<0, RMAX>(SLAM(ii) {
+    constexpr int i = RMAX - 1 - SK(ii);
+    if (i >= nv) return;
+    const double xi = bcast(xt, i);
+    if (xi != 0 && own && ((pmask[i] >> tid) & 1)) xt -= col[i] * xi;
+  });
+  xt *= dinv;
+  // x[i] -= LD[i][j] * x[j] for j in anc(i) descending, i ascending
+  double xf[RMAX];
+  sfor<0, RMAX>(SLAM(ii) {
+    constexpr int i = SK(ii);
+    if (i >= nv) {
+      xf[i] = 0;
+      return;
+    }
+    if (tid == i) {
+      sfor<0, i>(SLAM(jj) {
+        constexpr int j = i - 1 - SK(jj);
+        if ((anc >> j) & 1) xt -= row[j] * xf[j];
+      });
+    }
+    xf[i] = bcast(xt, i);
+  });
+  __syncthreads();  // every lane has read x before it is overwritten
+  if (own) x[tid] = xt;
+  __syncthreads();
+}
+
+// In-place dense Cholesky of the lower triangle of H (row-major nv x nv);
+// mirrors coop::hessian_factor's serial loop.
+__device__ inline void cholesky_rows(int nv, int tid, double* H) {
+  const bool own = tid < nv;
+  double r[RMAX];
+  sfor<0, RMAX>(SLAM(jj) {
+    constexpr int j = SK(jj);
+    r[j] = (own && j < nv && j <= tid) ? H[tid * nv + j] : 0.0;
+  });
+  sfor<0, RMAX>(SLAM(jc) {
+    constexpr int j = SK(jc);
+    if (j >= nv) return;
+    double rj[RMAX];  // row j, entries 0..j-1 final
+    sfor<0, j>(SLAM(qq) { rj[SK(qq)] = bcast(r[SK(qq)], j); });
+    double t = bcast(r[j], j);
+    if (j) {
+      double s = 0;
+      sfor<0, j>(SLAM(qq) { s += rj[SK(qq)] * rj[SK(qq)]; });
+      t -= s;
+    }
+    if (t < MINVAL) t = MINVAL;
+    const double d = sqrt(t);
+    const double tinv = 1 / d;
+    if (tid == j) r[j] = d;
+    if (own && tid > j) {
+      double s = 0;
+      sfor<0, j>(SLAM(qq) { s += r[SK(qq)] * rj[SK(qq)]; });
+      r[j] = (r[j] - s) * tinv;
+    }
+  });
+  __syncthreads();
+  if (own) {
+    sfor<0, RMAX>(SLAM(jj) {
+      if (SK(jj) < nv && SK(jj) <= tid) H[tid * nv + SK(jj)] = r[SK(jj)];
+    });
+  }
+  __syncthreads();
+}
+
+// search = -(H H')^-1 grad with the Cholesky factor in H's lower triangle;
+// mirrors the lane-0 substitution in coop::solver_newton.
+__device__ inline void chol_solve_rows(int nv, int tid, const double* H, const double* grad, double* search) {
+  const bool own = tid < nv;
+  double row[RMAX], col[RMAX], g = 0;
+  sfor<0, RMAX>(SLAM(jj) {
+    constexpr int j = SK(jj);
+    row[j] = (own && j < nv) ? H[tid * nv + j] : 0.0;
+    col[j] = (own && j < nv) ? H[j * nv + tid] : 0.0;
+  });
+  if (own) g = grad[tid];
+  const double dg = own ? rsel(row, tid) : 1.0;
+  // forward: s[i] = (s[i] - sum_{j<i} H[i][j] s[j]) / H[i][i]
+  double sf[RMAX];
+  sfor<0, RMAX>(SLAM(ii) {
+    constexpr int i = SK(ii);
+    if (i >= nv) {
+      sf[i] = 0;
+      return;
+    }
+    if (tid == i) {
+      if (i) {
+        double s = 0;
+        sfor<0, i>(SLAM(jj) { s += row[SK(jj)] * sf[SK(jj)]; });
+        g -= s;
+      }
+      g /= dg;
+    }
+    sf[i] = bcast(g, i);
+  });
+  // backward: s[i] -= H[j][i] s[j] for j = i+1.. ascending, then / H[i][i]
+  double sb[RMAX];
+  sfor<0, RMAX>(SLAM(ii) {
+    constexpr int i = RMAX - 1 - SK(ii);
+    if (i >= nv) {
+      sb[i] = 0;
+      return;
+    }
+    if (tid == i) {
+      sfor<i + 1, RMAX>(SLAM(jj) {
+        constexpr int j = SK(jj);
+        if (j < nv) g -= col[j] * sb[j];
+      });
+      g /= dg;
+    }
+    sb[i] = bcast(g, i);
+  });
+  if (own) search[tid] = -g;
+  __syncthreads();
+}
+
+}  // namespace coop
+}  // namespace ilqg

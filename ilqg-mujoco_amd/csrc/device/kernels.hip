@@ -311,6 +311,25 @@ __device__ void ldlt_solve(int n, const double* Lm, const int* transp, double* x
   for (int k = n - 1; k >= 0; k--) { double t = x[k]; x[k] = x[transp[k]]; x[transp[k]] = t; }
 }
 
+#ifdef ILQG_STAMPS
+__device__ unsigned long long g_bstamp_acc[16];
+__device__ unsigned long long g_bstamp_cnt[16];
+#define BSTAMP(id)                                                \
+  do {                                                            \
+    if (tid == 0 && blockIdx.x == 0) {                            \
+      unsigned long long t_ = __builtin_amdgcn_s_memtime();       \
+      if ((id) >= 0) {                                            \
+        g_bstamp_acc[(id) < 0 ? 0 : (id)] += t_ - bst_prev;       \
+        g_bstamp_cnt[(id) < 0 ? 0 : (id)]++;                      \
+      }                                                           \
+      bst_prev = t_;                                              \
+    }                                                             \
+  } while (0)
+#else
+#define BSTAMP(id) \
+  do {             \
+  } while (0)
+#endif
 constexpr int BW_THREADS = 64;  // one wavefront: its barriers compile to nothing
 constexpr int BW_PF = 8;        // prefetch registers per lane: D <= 512
 
@@ -364,6 +383,10 @@ __global__ __launch_bounds__(BW_THREADS) void k_backward(int nq, int nv, int nu,
     for (int e = tid; e < nx * nx; e += nt) { int i = e % nx, j = e / nx; V[e] = v[i] * v[j]; }
     __syncthreads();
   }
+#ifdef ILQG_STAMPS
+  unsigned long long bst_prev = 0;
+#endif
+  BSTAMP(-1);
   for (int n = 1; n < P; n++) {
     const size_t pc = (size_t)s * P + n, pp = pc - 1;
     // prefetch the next step's FD record; consumed at the end of this step
@@ -402,6 +425,7 @@ __global__ __launch_bounds__(BW_THREADS) void k_backward(int nq, int nv, int nu,
     __syncthreads();
     for (int i = tid; i < nx; i += nt) Vs[i + i * nx] += mu;
     __syncthreads();
+    BSTAMP(0);
     // stage 2: T1 = B'V
     ILP3_BEGIN(nu * nx)
       double s0 = 0, s1 = 0, s2 = 0;
@@ -416,6 +440,7 @@ __global__ __launch_bounds__(BW_THREADS) void k_backward(int nq, int nv, int nu,
       if (h2) T1[e2] = s2;
     }
     __syncthreads();
+    BSTAMP(1);
     // stage 3: Mm = -2 T1 B - 2R ; T3 = T1 A ; w = v + 2 V c
     for (int e = tid; e < nu * nu; e += nt) {
       int a = e % nu, b = e / nu;
@@ -448,6 +473,7 @@ __global__ __launch_bounds__(BW_THREADS) void k_backward(int nq, int nv, int nu,
       col[a] = sm + r[a];
     }
     __syncthreads();
+    BSTAMP(2);
     // stage 4: K = ldlt.solve(2 T3) column-parallel; k = ldlt.solve(B'w + r)
     for (int j = tid; j < nx + 1; j += nt) {
       // solved in place in LDS (a private array would live in scratch)
@@ -459,6 +485,7 @@ __global__ __launch_bounds__(BW_THREADS) void k_backward(int nq, int nv, int nu,
       ldlt_solve(nu, Mm, trn, x);
     }
     __syncthreads();
+    BSTAMP(3);
     // stage 5: ABK = A + B K ; T6 = K'R ; y = Bk + c ; kR = k'R
     for (int e = tid; e < nx * nx; e += nt) {
       int i = e % nx, j = e / nx;
@@ -483,6 +510,7 @@ __global__ __launch_bounds__(BW_THREADS) void k_backward(int nq, int nv, int nu,
       kR[b] = sm;
     }
     __syncthreads();
+    BSTAMP(4);
     // stage 6: T4 = ABK' V
     ILP3_BEGIN(nx * nx)
       double s0 = 0, s1 = 0, s2 = 0;
@@ -497,6 +525,7 @@ __global__ __launch_bounds__(BW_THREADS) void k_backward(int nq, int nv, int nu,
       if (h2) T4[e2] = s2;
     }
     __syncthreads();
+    BSTAMP(5);
     // stage 7: V_new = (T4 ABK + Q) + T6 K
     ILP3_BEGIN(nx * nx)
       double a0s = 0, a1s = 0, a2s = 0, b0s = 0, b1s = 0, b2s = 0;
@@ -516,6 +545,7 @@ __global__ __launch_bounds__(BW_THREADS) void k_backward(int nq, int nv, int nu,
       if (h2) Vn[e2] = (a2s + q[i2] * q[j2]) + b2s;
     }
     __syncthreads();
+    BSTAMP(6);
     // stage 8: z = (2y)' V_new ; v_new (reads the NEW V, Q14)
     for (int j = tid; j < nx; j += nt) {
       double sm = 0;
@@ -532,6 +562,7 @@ __global__ __launch_bounds__(BW_THREADS) void k_backward(int nq, int nv, int nu,
       for (int b = 0; b < nu; b++) td += (2 * kR[b]) * Kl[b + j * nu];
       vn[j] = ((ta + tb) + q[j]) + td;
     }
+    BSTAMP(7);
     // gains out
     for (int e = tid; e < nu * nx; e += nt) Kg[pc * nu * nx + e] = Kl[e];
     for (int a = tid; a < nu; a += nt) kg[pc * nu + a] = kl[a];
@@ -546,6 +577,7 @@ __global__ __launch_bounds__(BW_THREADS) void k_backward(int nq, int nv, int nu,
       }
     }
     __syncthreads();
+    BSTAMP(8);
   }
   if (Vg)
     for (int e = tid; e < nx * nx; e += nt) Vg[(size_t)s * nx * nx + e] = V[e];
@@ -654,3 +686,19 @@ hipError_t launch_forward(const DevModel& m, const WsLayout& L, WsDev ws, TrajDe
 }
 
 }  // namespace ilqg
+
+#ifdef ILQG_STAMPS
+// diagnostic build only: per-stage cycles of the Riccati kernel (block 0)
+extern "C" int ilqg_debug_bstamps(unsigned long long* acc, unsigned long long* cnt, int reset) {
+  if (hipMemcpyFromSymbol(acc, HIP_SYMBOL(ilqg::g_bstamp_acc), sizeof(unsigned long long) * 16) != hipSuccess)
+    return 3;
+  if (hipMemcpyFromSymbol(cnt, HIP_SYMBOL(ilqg::g_bstamp_cnt), sizeof(unsigned long long) * 16) != hipSuccess)
+    return 3;
+  if (reset) {
+    unsigned long long z[16] = {0};
+    (void)hipMemcpyToSymbol(HIP_SYMBOL(ilqg::g_bstamp_acc), z, sizeof(z));
+    (void)hipMemcpyToSymbol(HIP_SYMBOL(ilqg::g_bstamp_cnt), z, sizeof(z));
+  }
+  return 0;
+}
+#endif

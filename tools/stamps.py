@@ -25,3 +25,15 @@ for what, fn in (("rollout (1 seed)", g.forward_pass), ("fd sweep", g.fd_sweep))
     for i in range(22):
         if cnt[i]:
             print(f"  {NAMES[i]:24s} calls {cnt[i]:6d}  cycles/call {acc[i]/cnt[i]:9.0f}  share {acc[i]/max(tot,1):6.1%}")
+
+BN = ["stage1 sym/A/B/q/c/r", "stage2 T1=B'V", "stage3 Mm,T3,w,ldlt,col", "stage4 K,k solves",
+      "stage5 ABK,T6,y,kR", "stage6 T4", "stage7 Vn", "stage8 z,vn,K/k out", "V copy + prefetch store"]
+acc = (ctypes.c_ulonglong * 16)(); cnt = (ctypes.c_ulonglong * 16)()
+L.ilqg_debug_bstamps(acc, cnt, 1)
+g.backward_pass(); g.synchronize()
+L.ilqg_debug_bstamps(acc, cnt, 1)
+tot = sum(acc[i] for i in range(9))
+print(f"== backward: block 0, lane 0, total {tot} cycles, {tot / max(cnt[0], 1):.0f} per step")
+for i in range(9):
+    if cnt[i]:
+        print(f"  {BN[i]:26s} calls {cnt[i]:6d}  cycles/call {acc[i]/cnt[i]:9.0f}  share {acc[i]/max(tot,1):6.1%}")
