@@ -29,6 +29,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "ilqg-mujoco_amd"))
 import ilqg_amd as ia  # noqa: E402
 import workloads  # noqa: E402
+from seed_shard import CostExchange, device_view, max_over_ranks, seed_offset  # noqa: E402
 
 METRIC = "iLQR iterations/sec (FD+backward+forward) for Hopper H=500 at 1/2/4/8 GPUs"
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md chip table (spec)
@@ -45,28 +46,6 @@ def algorithmic_bytes(m, S, A, P):
     bw = (P * (m.D + nx) + (P - 1) * Kk) * 8
     fw = P * (Kk + nx + m.nu + Sr) * 8
     return {"fd_sweep": S * fd, "backward": S * bw, "rollout": S * A * fw}
-
-
-class CostExchange:
-    """The one collective of the design: all-gather per-seed costs (fp64) and pick
-    the global best seed.  Runs on torch's current stream, which is also the
-    solver's launch stream, so no host round trip is needed."""
-
-    def __init__(self, solver, nseed, world):
-        self.world = world
-        self.nseed = nseed
-        ptr = solver.device_costs_ptr()
-
-        class _Arr:
-            __cuda_array_interface__ = {"shape": (nseed,), "typestr": "<f8", "data": (ptr, False), "version": 3}
-        self.local = torch.as_tensor(_Arr(), device="cuda")
-        self.glob = torch.empty(nseed * world, dtype=torch.float64, device="cuda")
-
-    def __call__(self):
-        if self.world > 1:
-            dist.all_gather_into_tensor(self.glob, self.local)
-            return torch.argmin(self.glob)
-        return torch.argmin(self.local)
 
 
 def cpu_baseline(budget_s, horizon, threads):
@@ -172,11 +151,11 @@ def main():
     P = H + 1
     alphas = tuple(2.0 ** -i for i in range(A))
     m = ia.Model.load(workloads.model_file("hopper"))
-    dmain = workloads.hopper_dmain(m, S, sigma=0.01, seed_offset=rank * S)
+    dmain = workloads.hopper_dmain(m, S, sigma=0.01, seed_offset=seed_offset(rank, S))
     solver = ia.ILQR(m, dmain, H, ia.HOPPER_COST, alphas=alphas, select="min_cost", device=local_rank)
     stream = torch.cuda.current_stream()
     solver.set_stream(stream.cuda_stream)
-    exchange = CostExchange(solver, S, world)
+    exchange = CostExchange(device_view(solver.device_costs_ptr(), S), world)
 
     def one_step():
         solver.iterate()
@@ -198,10 +177,7 @@ def main():
         dist.barrier()
     elapsed = time.perf_counter() - t0
     ktime = solver.timing()
-    el = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
-    if world > 1:
-        dist.all_reduce(el, op=dist.ReduceOp.MAX)
-    elapsed = float(el.item())
+    elapsed = max_over_ranks(elapsed, world, "cuda")
     best_seed = int(best.item())
 
     value = world * S * args.steps / elapsed
