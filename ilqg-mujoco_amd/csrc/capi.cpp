@@ -604,6 +604,13 @@ int ilqg_solver_get_deriv(ilqg_solver* s, double* deriv) {
   return ILQG_OK;
 }
 
+int ilqg_solver_set_deriv(ilqg_solver* s, const double* deriv) {
+  if (!s || !deriv) return fail(ILQG_ERR_ARG, "bad argument");
+  HIPCHK(hipStreamSynchronize(s->stream));
+  HIPCHK(hipMemcpy(s->deriv.p, deriv, s->deriv.n, hipMemcpyHostToDevice));
+  return ILQG_OK;
+}
+
 int ilqg_solver_get_value(ilqg_solver* s, double* V, double* v) {
   if (!s) return fail(ILQG_ERR_ARG, "null solver");
   HIPCHK(hipStreamSynchronize(s->stream));

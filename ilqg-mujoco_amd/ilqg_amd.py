@@ -57,7 +57,7 @@ EXPORTS = [
     "ilqg_step_batch", "ilqg_forward_batch", "ilqg_fd_batch",
     "ilqg_solver_create", "ilqg_solver_free", "ilqg_solver_init", "ilqg_solver_set_dinit",
     "ilqg_solver_set_traj", "ilqg_solver_get_traj", "ilqg_solver_set_gains", "ilqg_solver_get_gains",
-    "ilqg_solver_get_deriv", "ilqg_solver_get_value", "ilqg_solver_get_costs",
+    "ilqg_solver_get_deriv", "ilqg_solver_set_deriv", "ilqg_solver_get_value", "ilqg_solver_get_costs",
     "ilqg_forward", "ilqg_fd_sweep", "ilqg_backward", "ilqg_iterate", "ilqg_synchronize",
     "ilqg_solver_stream", "ilqg_solver_device_costs", "ilqg_solver_set_stream", "ilqg_solver_set_timing",
     "ilqg_solver_get_timing",
@@ -315,6 +315,12 @@ class ILQR:
         d = np.zeros((self.S, self.P, self.model.D))
         _check(lib().ilqg_solver_get_deriv(self._h, _ptr(d)), "get_deriv")
         return d
+
+    def set_deriv(self, d):
+        d = _f64(d)
+        if d.size != self.S * self.P * self.model.D:
+            raise IlqgError(f"deriv must hold {self.S}x{self.P}x{self.model.D} doubles")
+        _check(lib().ilqg_solver_set_deriv(self._h, _ptr(d)), "set_deriv")
 
     def value(self):
         V = np.zeros((self.S, self.nx * self.nx))

@@ -115,6 +115,9 @@ int ilqg_solver_get_traj(ilqg_solver* s, double* time, double* qpos, double* qve
 int ilqg_solver_set_gains(ilqg_solver* s, const double* K, const double* k);
 int ilqg_solver_get_gains(ilqg_solver* s, double* K, double* k);
 int ilqg_solver_get_deriv(ilqg_solver* s, double* deriv);     /* nseed x (N+1) x D */
+/* overwrite the FD records before ilqg_backward, e.g. with cost-gradient
+   entries from a host cost callback (stepCostFn_t, inc/mjderivative.h:5) */
+int ilqg_solver_set_deriv(ilqg_solver* s, const double* deriv);
 int ilqg_solver_get_value(ilqg_solver* s, double* V, double* v); /* nseed x nx x nx (col-major), nseed x nx */
 /* per-seed trajectory cost of every candidate (nseed x nalpha) and the selected index */
 int ilqg_solver_get_costs(ilqg_solver* s, double* cost, int* selected);

@@ -1,0 +1,62 @@
+// Support types for the legacy C++ boundary (ilqr.h / differentiator.h):
+// a small fixed-size column-major matrix (the reference's Eigen members'
+// storage order) and the non-template solver core in libilqg_mujoco.so that
+// drives the MI355X path (include/ilqg_amd.h).
+#pragma once
+
+#include <cstddef>
+
+#include "mjderivative.h"
+#include "mujoco/mujoco.h"
+
+struct ilqg_cost;
+
+namespace ilqg_legacy {
+
+// Column-major R x C storage, like Eigen::Matrix<mjtNum, R, C> (the types of
+// ILQR::K / k / V / v and Differentiator::A / B in the reference).
+template <int R, int C>
+struct Mat {
+  mjtNum a[R * C] = {};
+  mjtNum& operator()(int i, int j) { return a[i + j * R]; }
+  const mjtNum& operator()(int i, int j) const { return a[i + j * R]; }
+  mjtNum* data() { return a; }
+  const mjtNum* data() const { return a; }
+  static constexpr int rows() { return R; }
+  static constexpr int cols() { return C; }
+};
+
+// Register a device cost descriptor for a host cost callback: ILQR / calcMJDerivatives
+// then evaluate the cost on the GPU instead of calling `fn` on the host.  The
+// descriptor must reproduce fn bit for bit (e.g. inc/inverted_pendulum/cost.h is
+// wq = {1,10}, wv = {1,10}, wu = {1}); the arrays are copied.
+void register_cost(stepCostFn_t fn, const ilqg_cost* desc, int nq, int nv, int nu);
+
+// Cost-gradient entries of one FD record by host evaluation of fn, exactly as
+// src/mjderivative.cpp:72,78-206 forms them (one-sided, perturbed state, eps 1e-6).
+void host_cost_columns(const mjModel* m, const mjData* dmain, stepCostFn_t fn, mjtNum* deriv);
+
+// The non-template part of ILQR<nv,nu,N>: one device solver (1 seed, 1
+// candidate, reference semantics) plus host mirrors of its trajectory.
+class SolverCore {
+ public:
+  SolverCore(mjModel* m, int N, stepCostFn_t fn);
+  ~SolverCore();
+  SolverCore(const SolverCore&) = delete;
+  SolverCore& operator=(const SolverCore&) = delete;
+
+  // ILQR ctor: d = dmain, passive rollout into dArray (inc/ilqr.h:69-97)
+  void init(const mjData* dmain, mjData* const* dArray);
+  void set_dinit(const mjData* dinit);                    // inc/ilqr.h:110-113
+  void forward(mjData* const* dArray, const mjtNum* K, const mjtNum* k);  // inc/ilqr.h:116-130
+  void backward(mjData* const* dArray, mjtNum* K, mjtNum* k, mjtNum* V, mjtNum* v);  // :133-176
+  void iterate(mjData* const* dArray, mjtNum* K, mjtNum* k, mjtNum* V, mjtNum* v);   // :179-186
+
+ private:
+  void push_traj(mjData* const* dArray);
+  void pull_traj(mjData* const* dArray);
+  struct Impl;
+  Impl* p_;
+};
+
+}  // namespace ilqg_legacy

@@ -28,8 +28,12 @@ def _ensure_built():
     if os.path.exists("/root/reference/src/mjderivative.cpp") and not os.path.exists(
             os.path.join(ORACLE, "_ref", "libilqg_ref.so")):
         subprocess.run(["make", "-s", "-C", ORACLE, "ref"], check=True)
-    if not os.path.exists(os.path.join(PKG, "lib", "libilqg_amd.so")):
+    if not all(os.path.exists(os.path.join(PKG, *p)) for p in
+               (("lib", "libilqg_amd.so"), ("lib", "libilqg_mujoco.so"), ("bin", "ilqg_headless"))):
         subprocess.run(["make", "-s", "-j8", "-C", PKG], check=True)
+    if os.path.exists("/root/reference/src/inverted_pendulum/inverted_pendulum.cpp") and not os.path.exists(
+            os.path.join(ORACLE, "_ref", "ref_pendulum_legacy")):
+        subprocess.run(["make", "-s", "-C", ORACLE, "legacy"], check=True)
 
 
 _ensure_built()

@@ -1,0 +1,116 @@
+"""Legacy C++ boundary: include/legacy (mujoco.h subset,
+mjderivative.h, util.h, update.h, differentiator.h, ilqr.h) over
+libilqg_mujoco.so.
+
+CPU: the library exports the reference's C++ symbols with the reference's
+mangling and the MuJoCo C API subset; the reference's own controller
+(src/inverted_pendulum/inverted_pendulum.cpp) compiles unmodified against the
+headers and links (when /root/reference is present); without a GPU the path
+fails loudly.
+GPU: the headless cmd/basic.cpp loop (ilqg_headless, host-callback cost and
+registered device cost) and the reference's controller linked against the
+product reproduce the oracle's MPC loop bit for bit."""
+import os
+import subprocess
+
+import numpy as np
+import pytest
+
+from conftest import ROOT, model_path
+
+LIB = os.path.join(ROOT, "ilqg-mujoco_amd", "lib", "libilqg_mujoco.so")
+HEADLESS = os.path.join(ROOT, "ilqg-mujoco_amd", "bin", "ilqg_headless")
+REF_LOOP = os.path.join(ROOT, "oracle", "_ref", "ref_pendulum_legacy")
+
+REF_SYMBOLS = [
+    "_Z17calcMJDerivativesP8_mjModelP7_mjDataPdPFdPKS1_E",  # inc/mjderivative.h:7
+    "_Z8cpMjDataPK8_mjModelP7_mjDataPKS2_",  # inc/util.h:6
+    "_Z11forwardStepP8_mjModelP7_mjData",  # inc/update.h:6
+    "_Z12forwardFrameP8_mjModelP7_mjData",  # inc/update.h:8
+]
+MJ_API = ["mj_activate", "mj_deactivate", "mj_loadXML", "mj_deleteModel", "mj_makeData", "mj_deleteData",
+          "mj_resetData", "mj_stackAlloc", "mj_step", "mj_forward", "mj_forwardSkip", "mju_copy", "mju_zero",
+          "mju_malloc", "mju_free", "mju_error", "mju_error_s", "mju_quatIntegrate"]
+
+
+def _exports(path):
+    out = subprocess.run(["nm", "-D", "--defined-only", path], capture_output=True, text=True, check=True).stdout
+    return {line.split()[-1] for line in out.splitlines() if line.strip()}
+
+
+def test_legacy_exports_reference_symbols():
+    syms = _exports(LIB)
+    for s in REF_SYMBOLS + MJ_API:
+        assert s in syms, s
+
+
+@pytest.mark.skipif(not os.path.isdir("/root/reference/src"), reason="/root/reference not present (GPU box)")
+def test_reference_controller_compiles_against_legacy_headers():
+    r = subprocess.run(["make", "-s", "-C", os.path.join(ROOT, "oracle"), "legacy"], capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr
+    assert os.path.exists(REF_LOOP)
+
+
+@pytest.mark.skipif(os.path.exists("/dev/kfd"), reason="a GPU is visible")
+def test_headless_fails_loudly_without_gpu():
+    r = subprocess.run([HEADLESS, model_path("inverted_pendulum"), "1"], capture_output=True, text=True)
+    assert r.returncode != 0 and "ERROR" in r.stderr
+
+
+# ------------------------------------------------------------------ GPU
+FRAMES = 3
+
+
+def _parse(out):
+    rows = []
+    for line in out.splitlines():
+        if line.startswith("frame "):
+            rows.append([float.fromhex(x) for x in line.split()[2:]])
+    return np.array(rows)
+
+
+def _oracle_loop(ora, frames):
+    """InvertedPendulum (src/inverted_pendulum/inverted_pendulum.cpp:7-30) on the oracle:
+    10 passive steps, ILQR<2,1,20>; per frame setDInit, 10 iterate, first control, mj_step."""
+    import ilqg_amd as ia
+    m = ia.Model.load(model_path("inverted_pendulum"))
+    om = ora.OModel(m.blob())
+    d = om.make_data()
+    d.step(10)
+    il = ora.OILQR(om, d, 20, cost_fn="ora_cost_pendulum")
+
+    def row():
+        return [d.time] + list(d.arr("qpos")) + list(d.arr("qvel")) + list(d.arr("ctrl"))
+    rows = [row()]
+    for _ in range(frames):
+        il.set_dinit(d)
+        for _ in range(10):
+            il.iterate()
+        d.arr("ctrl")[:] = il.traj()["ctrl"][20]
+        d.step(1)
+        rows.append(row())
+    return np.array(rows)
+
+
+def _run(cmd):
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stderr
+    return _parse(r.stdout)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("device_cost", [False, True])
+def test_headless_loop_bitexact(ora, device_cost):
+    cmd = [HEADLESS, model_path("inverted_pendulum"), str(FRAMES)] + (["--device-cost"] if device_cost else [])
+    got = _run(cmd)
+    ref = _oracle_loop(ora, FRAMES)
+    assert got.shape == ref.shape
+    assert np.array_equal(got, ref), np.abs(got - ref).max()
+
+
+@pytest.mark.gpu
+@pytest.mark.skipif(not os.path.exists(REF_LOOP), reason="oracle/_ref/ref_pendulum_legacy not built")
+def test_reference_controller_on_gpu_bitexact(ora):
+    got = _run([REF_LOOP, model_path("inverted_pendulum"), str(FRAMES)])
+    ref = _oracle_loop(ora, FRAMES)
+    assert np.array_equal(got, ref), np.abs(got - ref).max()
