@@ -12,6 +12,7 @@
 
 #include "device/dmodel.h"
 #include "device/kernels.h"
+#include "device/static_models.h"
 #include "ilqg_amd.h"
 #include "model/model.h"
 
@@ -56,6 +57,16 @@ struct DevBuf {
   T* as() const { return static_cast<T*>(p); }
 };
 
+// model-specific kernels for the bundled models (ILQG_STATIC=0 disables, for A/B)
+bool use_static() {
+  static int v = -1;
+  if (v < 0) {
+    const char* e = getenv("ILQG_STATIC");
+    v = (e && e[0] == '0') ? 0 : 1;
+  }
+  return v == 1;
+}
+
 // kernel family: cooperative (one wavefront per evaluation, LDS workspace,
 // default) or lane-per-evaluation (ILQG_PATH=lane; kept for A/B comparison)
 bool use_coop() {
@@ -95,6 +106,14 @@ int check_device_support(const HostModel& m, bool solver, std::string& why) {
 struct ilqg_model {
   HostModel host;
   std::vector<unsigned char> blob;
+  // host-side device image: every model array 8-byte aligned in one block, so a
+  // workgroup stages the whole read-only model into LDS with one coalesced copy
+  std::vector<unsigned char> img;
+  std::vector<std::pair<size_t, const void**>> fix;  // (image offset, DevModel pointer field)
+  size_t isanc_at = 0, pair_at = 0, pmask_at = 0;
+  int npair = 0;
+  std::vector<int> key;  // specialization key (ilqg_model_static_key)
+  int static_id = 0;     // compiled model-specific kernels, 0 = generic
   // device copy (per device ordinal)
   int dev = -1;
   DevBuf buf;
@@ -102,15 +121,13 @@ struct ilqg_model {
   WsLayout L{};
   coop::CoopAux X{};
   coop::CoopLayout C{};
-  int npair = 0;
   hipStream_t stream = nullptr;
 
-  int upload(int device) {
-    if (dev == device && buf.p) return ILQG_OK;
-    HIPCHK(hipSetDevice(device));
+  // host preparation: static collision pairs, dof ancestry, image layout, key
+  void prepare() {
     const HostModel& h = host;
-    // cooperative-kernel aux data: dof ancestor matrix and the statically
-    // admissible geom pairs in the oracle's (g1 < g2) enumeration order
+    // dof ancestor matrix and the statically admissible geom pairs in the
+    // oracle's (g1 < g2) enumeration order
     std::vector<int> isanc(h.nv * h.nv, 0), pairs;
     for (int i = 0; i < h.nv; i++)
       for (int j = i; j >= 0; j = h.dof_parentid[j]) isanc[i * h.nv + j] = 1;
@@ -133,15 +150,15 @@ struct ilqg_model {
         pairs.push_back(g2);
       }
     npair = (int)pairs.size() / 2;
-    // one compact image, every array 8-byte aligned, so a workgroup can stage
-    // the whole read-only model into LDS with one coalesced copy
-    std::vector<unsigned char> img;
-    std::vector<std::pair<size_t, const void**>> fix;
+    img.clear();
+    fix.clear();
+    std::vector<int> offs;
     auto put = [&](const void* src, size_t bytes, const void** dst) {
       size_t at = img.size();
       img.resize(at + ((bytes + 7) & ~(size_t)7), 0);
       if (bytes) memcpy(img.data() + at, src, bytes);
       if (dst) fix.emplace_back(at, dst);
+      offs.push_back((int)at);
       return at;
     };
 #define ILQG_CP_F(nm, cnt) put(host.nm.data(), host.nm.size() * 8, (const void**)&dm.nm);
@@ -152,21 +169,48 @@ struct ilqg_model {
   }
     ILQG_MODEL_F64_ARRAYS(ILQG_CP_F)
     ILQG_MODEL_I32_ARRAYS(ILQG_CP_I)
-    size_t isanc_at = put(isanc.data(), isanc.size() * 4, nullptr);
-    size_t pair_at = put(pairs.data(), pairs.size() * 4, nullptr);
-    size_t pmask_at = put(pmask.data(), pmask.size() * 8, nullptr);
+#undef ILQG_CP_F
+#undef ILQG_CP_I
+    isanc_at = put(isanc.data(), isanc.size() * 4, nullptr);
+    pair_at = put(pairs.data(), pairs.size() * 4, nullptr);
+    pmask_at = put(pmask.data(), pmask.size() * 8, nullptr);
     img.resize(img.size() + 8, 0);
+    // key: everything the model-specific kernels take as compile-time constants
+    key.clear();
+#define ILQG_K_S(nm) key.push_back(h.nm);
+    ILQG_MODEL_I32_SCALARS(ILQG_K_S)
+#undef ILQG_K_S
+    key.push_back(h.maxcon);
+    key.push_back(h.maxefc);
+    key.push_back(npair);
+    key.push_back((int)img.size());
+    key.push_back((int)offs.size());
+    key.insert(key.end(), offs.begin(), offs.end());
+#define ILQG_K_A(nm, cnt) key.insert(key.end(), h.nm.begin(), h.nm.end());
+    ILQG_MODEL_I32_ARRAYS(ILQG_K_A)
+#undef ILQG_K_A
+    key.insert(key.end(), pairs.begin(), pairs.end());
+    static_id = match_static_model(key);
+  }
+
+  int upload(int device) {
+    if (dev == device && buf.p) return ILQG_OK;
+    HIPCHK(hipSetDevice(device));
+    const HostModel& h = host;
     HIPCHK(buf.alloc(img.size()));
     HIPCHK(hipMemcpy(buf.p, img.data(), img.size(), hipMemcpyHostToDevice));
     for (auto& f : fix) *f.second = static_cast<unsigned char*>(buf.p) + f.first;
-#define ILQG_SC_I(nm) dm.nm = host.nm;
-#define ILQG_SC_F(nm) dm.nm = host.nm;
+#define ILQG_SC_I(nm) dm.nm = h.nm;
+#define ILQG_SC_F(nm) dm.nm = h.nm;
     ILQG_MODEL_I32_SCALARS(ILQG_SC_I)
     ILQG_MODEL_F64_SCALARS(ILQG_SC_F)
-    dm.maxcon = host.maxcon;
-    dm.maxefc = host.maxefc;
+#undef ILQG_SC_I
+#undef ILQG_SC_F
+    dm.maxcon = h.maxcon;
+    dm.maxefc = h.maxefc;
     dm.img = static_cast<const unsigned char*>(buf.p);
     dm.img_bytes = (int)img.size();
+    dm.static_id = use_static() ? static_id : 0;
     L = make_layout(dm);
     X.isanc = reinterpret_cast<const int*>(static_cast<unsigned char*>(buf.p) + isanc_at);
     X.pair = reinterpret_cast<const int*>(static_cast<unsigned char*>(buf.p) + pair_at);
@@ -275,6 +319,7 @@ int ilqg_device_count(int* count) {
 // ---------------------------------------------------------------- model --
 static int finish_model(ilqg_model* m, ilqg_model** out) {
   m->blob = write_blob(m->host);
+  m->prepare();
   *out = m;
   return ILQG_OK;
 }
@@ -320,6 +365,22 @@ int ilqg_model_timestep(const ilqg_model* m, double* dt) {
 int ilqg_model_qpos0(const ilqg_model* m, double* q) {
   if (!m || !q) return fail(ILQG_ERR_ARG, "null argument");
   std::copy(m->host.qpos0.begin(), m->host.qpos0.end(), q);
+  return ILQG_OK;
+}
+
+int ilqg_model_static_key(const ilqg_model* m, int* key, int cap, int* n) {
+  if (!m || !n) return fail(ILQG_ERR_ARG, "null argument");
+  *n = (int)m->key.size();
+  if (key) {
+    if (cap < (int)m->key.size()) return fail(ILQG_ERR_ARG, "buffer too small");
+    std::copy(m->key.begin(), m->key.end(), key);
+  }
+  return ILQG_OK;
+}
+
+int ilqg_model_static_id(const ilqg_model* m, int* id) {
+  if (!m || !id) return fail(ILQG_ERR_ARG, "null argument");
+  *id = use_static() ? m->static_id : 0;
   return ILQG_OK;
 }
 

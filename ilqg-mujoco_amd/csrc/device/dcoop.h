@@ -62,7 +62,7 @@ __device__ __forceinline__ double tdot(const double* a, const double* b, int n) 
 }
 
 // ------------------------------------------------------ position stage ---
-__device__ inline void kinematics(const DevModel& m, const WsLayout& L, const CoopLayout& C, const Team& T) {
+__device__ inline void kinematics(const auto& m, const auto& L, const auto& C, const Team& T) {
   double* qpos = T.w + L.qpos;
   double* xpos = T.w + L.xpos;
   double* xquat = T.w + L.xquat;
@@ -184,7 +184,7 @@ __device__ inline void kinematics(const DevModel& m, const WsLayout& L, const Co
   TSYNC();
 }
 
-__device__ inline void com_pos(const DevModel& m, const WsLayout& L, const Team& T) {
+__device__ inline void com_pos(const auto& m, const auto& L, const Team& T) {
   const int nb = m.nbody;
   double* xipos = T.w + L.xipos;
   double* scom = T.w + L.scom;
@@ -267,7 +267,7 @@ __device__ inline void com_pos(const DevModel& m, const WsLayout& L, const Team&
   TSYNC();
 }
 
-__device__ inline void crb(const DevModel& m, const WsLayout& L, const CoopLayout& C, const CoopAux& X,
+__device__ inline void crb(const auto& m, const auto& L, const auto& C, const auto& X,
                            const Team& T) {
   const int nv = m.nv, nb = m.nbody;
   double* crbv = T.w + L.crb;
@@ -305,7 +305,7 @@ __device__ inline void crb(const DevModel& m, const WsLayout& L, const CoopLayou
 }
 
 // tree L'DL (oracle factor_ld), parallel over ancestor pairs for each k
-__device__ inline void factor_ld(const DevModel& m, const CoopAux& X, const Team& T, const double* mat, double* LD,
+__device__ inline void factor_ld(const auto& m, const auto& X, const Team& T, const double* mat, double* LD,
                                  double* diaginv, double* tmpv) {
   const int nv = m.nv;
   if (nv <= RMAX && X.pmask) {
@@ -375,7 +375,7 @@ __device__ inline void factor_ld(const DevModel& m, const CoopAux& X, const Team
 }
 
 // oracle solve_ld on lane 0 (ends with a barrier)
-__device__ inline void solve_ld(const DevModel& m, const CoopAux& X, const Team& T, const double* LD,
+__device__ inline void solve_ld(const auto& m, const auto& X, const Team& T, const double* LD,
                                 const double* diaginv, double* x) {
   const int nv = m.nv;
   if (nv <= RMAX && X.pmask) {
@@ -417,7 +417,7 @@ __device__ inline void solve_ld(const DevModel& m, const CoopAux& X, const Team&
   TSYNC();
 }
 
-__device__ inline void jac_col(const DevModel& m, const CoopAux& X, const double* scom, const double* cdof,
+__device__ inline void jac_col(const auto& m, const auto& X, const double* scom, const double* cdof,
                                const double* point, int body, int k, double* out3) {
   // one dof column of jac_point (oracle): zero unless dof k lies on the chain of `body`
   const int nv = m.nv;
@@ -436,7 +436,7 @@ __device__ inline void jac_col(const DevModel& m, const CoopAux& X, const double
   out3[2] = cd[5] + tmp[2];
 }
 
-__device__ inline void collision(const DevModel& m, const WsLayout& L, const CoopLayout& C, const CoopAux& X,
+__device__ inline void collision(const auto& m, const auto& L, const auto& C, const auto& X,
                                  const Team& T) {
   double* gxpos = T.w + L.gxpos;
   double* gxmat = T.w + L.gxmat;
@@ -533,7 +533,7 @@ __device__ inline void collision(const DevModel& m, const WsLayout& L, const Coo
   TSYNC();
 }
 
-__device__ inline void make_constraint(const DevModel& m, const WsLayout& L, const CoopLayout& C, const CoopAux& X,
+__device__ inline void make_constraint(const auto& m, const auto& L, const auto& C, const auto& X,
                                        const Team& T) {
   const int nv = m.nv;
   double* qpos = T.w + L.qpos;
@@ -676,7 +676,7 @@ __device__ inline void make_constraint(const DevModel& m, const WsLayout& L, con
   TSYNC();
 }
 
-__device__ inline void fwd_position(const DevModel& m, const WsLayout& L, const CoopLayout& C, const CoopAux& X,
+__device__ inline void fwd_position(const auto& m, const auto& L, const auto& C, const auto& X,
                                     const Team& T) {
   kinematics(m, L, C, T);
   STAMP(14 - 14 + 0);
@@ -700,7 +700,7 @@ __device__ inline void fwd_position(const DevModel& m, const WsLayout& L, const 
 }
 
 // ------------------------------------------------------ velocity stage ---
-__device__ inline void fwd_velocity(const DevModel& m, const WsLayout& L, const CoopLayout& C, const Team& T) {
+__device__ inline void fwd_velocity(const auto& m, const auto& L, const auto& C, const Team& T) {
   const int nv = m.nv, nb = m.nbody;
   double* cvelw = T.w + L.cvel;
   double* cdof = T.w + L.cdof;
@@ -831,7 +831,7 @@ __device__ inline void fwd_velocity(const DevModel& m, const WsLayout& L, const 
 }
 
 // -------------------------------------------------- acceleration stage ---
-__device__ inline void fwd_acceleration(const DevModel& m, const WsLayout& L, const CoopAux& X, const Team& T) {
+__device__ inline void fwd_acceleration(const auto& m, const auto& L, const auto& X, const Team& T) {
   const int nv = m.nv, nu = m.nu;
   double* ctrl = T.w + L.ctrl;
   double* af = T.w + L.afrc;
@@ -885,7 +885,7 @@ __device__ inline void fwd_acceleration(const DevModel& m, const WsLayout& L, co
 }
 
 // constraint cost of residuals `jar`; force/state per row, qfrc_constraint per dof
-__device__ inline double constraint_update(const DevModel& m, const WsLayout& L, const CoopLayout& C, const Team& T,
+__device__ inline double constraint_update(const auto& m, const auto& L, const auto& C, const Team& T,
                                            const double* jar) {
   const int nv = m.nv, ne = T.iw[L.nefc];
   double* D = T.w + L.efc_D;
@@ -922,7 +922,7 @@ __device__ inline double constraint_update(const DevModel& m, const WsLayout& L,
   return T.c[C.bc];
 }
 
-__device__ inline void hessian_factor(const DevModel& m, const WsLayout& L, const CoopLayout& C, const Team& T,
+__device__ inline void hessian_factor(const auto& m, const auto& L, const auto& C, const Team& T,
                                       double* H) {
   const int nv = m.nv, ne = T.iw[L.nefc];
   double* J = T.w + L.efc_J;
@@ -974,7 +974,7 @@ __device__ inline void hessian_factor(const DevModel& m, const WsLayout& L, cons
   }
 }
 
-__device__ inline void solver_newton(const DevModel& m, const WsLayout& L, const CoopLayout& C, const Team& T,
+__device__ inline void solver_newton(const auto& m, const auto& L, const auto& C, const Team& T,
                                      int maxiter, double tol) {
   const int nv = m.nv, ne = T.iw[L.nefc];
   const double scale = 1 / (m.stat_meaninertia * (nv > 1 ? nv : 1));
@@ -1098,7 +1098,7 @@ __device__ inline void solver_newton(const DevModel& m, const WsLayout& L, const
   }
 }
 
-__device__ inline void fwd_constraint(const DevModel& m, const WsLayout& L, const CoopLayout& C, const Team& T,
+__device__ inline void fwd_constraint(const auto& m, const auto& L, const auto& C, const Team& T,
                                       int maxiter, double tol) {
   const int nv = m.nv, ne = T.iw[L.nefc];
   double* qacc = T.w + L.qacc;
@@ -1143,7 +1143,7 @@ __device__ inline void fwd_constraint(const DevModel& m, const WsLayout& L, cons
   TSYNC();
 }
 
-__device__ inline void forward_skip(const DevModel& m, const WsLayout& L, const CoopLayout& C, const CoopAux& X,
+__device__ inline void forward_skip(const auto& m, const auto& L, const auto& C, const auto& X,
                                     const Team& T, int skipstage, int maxiter, double tol) {
   STAMP(-1);
   TSYNC();
@@ -1159,7 +1159,7 @@ __device__ inline void forward_skip(const DevModel& m, const WsLayout& L, const 
   STAMP(8);
 }
 
-__device__ inline void integrate_pos(const DevModel& m, const Team& T, double* qpos, const double* qvel, double dt) {
+__device__ inline void integrate_pos(const auto& m, const Team& T, double* qpos, const double* qvel, double dt) {
   FOR_T(j, m.njnt) {
     int pa = m.jnt_qposadr[j], va = m.jnt_dofadr[j];
     int type = m.jnt_type[j];
@@ -1181,7 +1181,7 @@ __device__ inline void integrate_pos(const DevModel& m, const Team& T, double* q
   TSYNC();
 }
 
-__device__ inline void reset_data(const DevModel& m, const WsLayout& L, const Team& T) {
+__device__ inline void reset_data(const auto& m, const auto& L, const Team& T) {
   double* qpos = T.w + L.qpos;
   FOR_T(i, m.nq) qpos[i] = m.qpos0[i];
   FOR_T(i, m.nv) {
@@ -1195,7 +1195,7 @@ __device__ inline void reset_data(const DevModel& m, const WsLayout& L, const Te
   TSYNC();
 }
 
-__device__ inline int any_bad(const Team& T, const CoopLayout& C, const double* x, int n) {
+__device__ inline int any_bad(const Team& T, const auto& C, const double* x, int n) {
   if (T.tid == 0) {
     int bad = 0;
     for (int i = 0; i < n; i++)
@@ -1208,7 +1208,7 @@ __device__ inline int any_bad(const Team& T, const CoopLayout& C, const double* 
   return r;
 }
 
-__device__ inline void euler(const DevModel& m, const WsLayout& L, const CoopLayout& C, const CoopAux& X,
+__device__ inline void euler(const auto& m, const auto& L, const auto& C, const auto& X,
                              const Team& T) {
   const int nv = m.nv;
   double* s = T.w + L.s_euler;
@@ -1242,7 +1242,7 @@ __device__ inline void euler(const DevModel& m, const WsLayout& L, const CoopLay
   TSYNC();
 }
 
-__device__ inline void rk4(const DevModel& m, const WsLayout& L, const CoopLayout& C, const CoopAux& X, const Team& T,
+__device__ inline void rk4(const auto& m, const auto& L, const auto& C, const auto& X, const Team& T,
                            int maxiter, double tol) {
   const double A[9] = {0.5, 0, 0, 0, 0.5, 0, 0, 0, 1};
   const double Bw[4] = {1.0 / 6, 1.0 / 3, 1.0 / 3, 1.0 / 6};
@@ -1308,7 +1308,7 @@ __device__ inline void rk4(const DevModel& m, const WsLayout& L, const CoopLayou
 }
 
 // mj_step with the model's own solver settings
-__device__ inline void step(const DevModel& m, const WsLayout& L, const CoopLayout& C, const CoopAux& X,
+__device__ inline void step(const auto& m, const auto& L, const auto& C, const auto& X,
                             const Team& T) {
   if (any_bad(T, C, T.w + L.qpos, m.nq)) reset_data(m, L, T);
   if (any_bad(T, C, T.w + L.qvel, m.nv)) reset_data(m, L, T);

@@ -32,6 +32,7 @@ struct DevModel {
   int maxcon, maxefc;
   const unsigned char* img;  // base of the compact model image (device memory)
   int img_bytes;             // image size, a multiple of 8
+  int static_id;             // compiled model-specific kernels (static_models.h), 0 = generic
 };
 
 // contact record inside the workspace (doubles, then ints)
@@ -54,7 +55,8 @@ struct WsLayout {
   int ni;
 };
 
-inline WsLayout make_layout(const DevModel& m) {
+template <class M>
+constexpr WsLayout make_layout(const M& m) {
   WsLayout L{};
   int o = 0;
   const int nq = m.nq, nv = m.nv, nu = m.nu, nb = m.nbody, nj = m.njnt, ng = m.ngeom;
@@ -102,7 +104,8 @@ struct CoopLayout {
   int imgd;  // doubles of LDS holding the staged model image
 };
 
-inline CoopLayout make_coop_layout(const DevModel& m, int npair) {
+template <class M>
+constexpr CoopLayout make_coop_layout(const M& m, int npair) {
   CoopLayout C{};
   int o = 0, oi = 0;
   const int nc = m.maxcon > 0 ? m.maxcon : 1, ne = m.maxefc > 0 ? m.maxefc : 1;

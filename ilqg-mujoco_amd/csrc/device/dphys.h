@@ -567,7 +567,8 @@ __device__ inline int plane_sphere(RCon* c, double margin, const double* pos1, c
   c->pos[2] = p2[2] + n[2] * s;
   return 1;
 }
-__device__ inline int narrow(const DevModel& m, int t1, int t2, const double* pos1, const double* mat1,
+template <class M>
+__device__ inline int narrow(const M& m, int t1, int t2, const double* pos1, const double* mat1,
                              const double* sz1, const double* pos2, const double* mat2, const double* sz2,
                              double margin, RCon* con) {
   if (t1 == GEOM_PLANE && t2 == GEOM_SPHERE) return plane_sphere(con, margin, pos1, mat1, pos2, sz2[0]);

@@ -56,7 +56,7 @@ __device__ __forceinline__ double rsel(const double (&r)[RMAX], int idx) {
 // Tree L'DL factorization of the lower triangle of `mat` (nv x nv, row-major)
 // into LD (full nv x nv, zero upper) and diaginv.  pmask[i]: proper ancestors
 // of dof i.  Mirrors coop::factor_ld's serial loop entry by entry.
-__device__ inline void factor_ld_rows(int nv, const unsigned long long* pmask, int tid, const double* mat, double* LD,
+__device__ inline void factor_ld_rows(int nv, const auto& pmask, int tid, const double* mat, double* LD,
                                       double* diaginv) {
   double r[RMAX];
   unsigned long long pm[RMAX];  // wave-uniform ancestor masks, loaded up front
@@ -108,7 +108,7 @@ __device__ inline void factor_ld_rows(int nv, const unsigned long long* pmask, i
 }
 
 // x <- (L'DL)^-1 x for the factor above; mirrors coop::solve_ld.
-__device__ inline void solve_ld_rows(int nv, const unsigned long long* pmask, int tid, const double* LD,
+__device__ inline void solve_ld_rows(int nv, const auto& pmask, int tid, const double* LD,
                                      const double* diaginv, double* x) {
   const bool own = tid < nv;
   double row[RMAX], col[RMAX], xt = 0, dinv = 0;

@@ -5,6 +5,7 @@
 //   k_rollout_coop    inc/ilqr.h:116-130           one workgroup per (seed, alpha)
 #include "dcoop.h"
 #include "kernels.h"
+#include "static_models.h"
 
 namespace ilqg {
 namespace {
@@ -17,7 +18,7 @@ constexpr int FD_NWARMUP = 3;    // mjderivative.cpp:38
 constexpr int TEAM = 64;
 
 // LDS: [workspace doubles][coop doubles][model image][workspace ints][coop ints]
-__device__ inline Team make_team(const WsLayout& L, const CoopLayout& C) {
+__device__ inline Team make_team(const auto& L, const auto& C) {
   extern __shared__ double lds[];
   Team T;
   T.w = lds;
@@ -25,7 +26,7 @@ __device__ inline Team make_team(const WsLayout& L, const CoopLayout& C) {
   T.iw = reinterpret_cast<int*>(lds + L.nd + C.nd + C.imgd);
   T.ci = T.iw + L.ni;
   T.tid = threadIdx.x;
-  T.nt = blockDim.x;
+  T.nt = TEAM;  // every cooperative kernel is launched with one 64-lane wavefront
   return T;
 }
 
@@ -54,6 +55,18 @@ __device__ inline void stage_model(const DevModel& g, const CoopAux& Xg, const W
   TSYNC();
 }
 
+// model-specific variant: same image copy; sizes/tables are compile-time
+// (static_models.h), float arrays bound at compile-time LDS offsets
+template <class SM>
+__device__ inline void stage_model_s(const DevModel& g, const auto& L, const auto& C, const Team& T, SM& m) {
+  extern __shared__ double lds[];
+  double* dst = lds + L.nd + C.nd;
+  const double* src = reinterpret_cast<const double*>(g.img);
+  FOR_T(w, C.imgd) dst[w] = src[w];
+  m.bind(reinterpret_cast<const unsigned char*>(dst), g);
+  TSYNC();
+}
+
 __device__ inline double cost_terms(double c, const double* x, const double* w, const double* t, const double* l,
                                     int n) {
   for (int i = 0; i < n; i++) {
@@ -66,7 +79,7 @@ __device__ inline double cost_terms(double c, const double* x, const double* w, 
   }
   return c;
 }
-__device__ inline double step_cost(const DevModel& m, const CostDev& c, const double* qpos, const double* qvel,
+__device__ inline double step_cost(const auto& m, const CostDev& c, const double* qpos, const double* qvel,
                                    const double* ctrl) {
   double s = 0;
   s = cost_terms(s, qpos, c.wq, c.tq, c.lq, m.nq);
@@ -76,7 +89,7 @@ __device__ inline double step_cost(const DevModel& m, const CostDev& c, const do
 }
 
 // cpMjData(d, src) from a trajectory record (src/util.cpp:4-14)
-__device__ inline void load_state(const DevModel& m, const WsLayout& L, const Team& T, const TrajDev& tr, int pt,
+__device__ inline void load_state(const auto& m, const auto& L, const Team& T, const TrajDev& tr, int pt,
                                   int seed, const double* qfrc_applied, const double* xfrc_applied) {
   FOR_T(i, m.nq) T.w[L.qpos + i] = tr.qpos[(size_t)pt * m.nq + i];
   FOR_T(i, m.nv) {
@@ -90,14 +103,8 @@ __device__ inline void load_state(const DevModel& m, const WsLayout& L, const Te
   TSYNC();
 }
 
-__global__ __launch_bounds__(TEAM) void k_fd_centre_coop(DevModel mg, WsLayout L, CoopLayout C, CoopAux Xg, TrajDev tr,
-                                                         int P, const double* qfrc_applied,
-                                                         const double* xfrc_applied, CostDev cost, double* warm_c,
-                                                         double* cost_c) {
-  Team T = make_team(L, C);
-  DevModel m;
-  CoopAux X;
-  stage_model(mg, Xg, L, C, T, m, X);
+__device__ inline void fd_centre_body(const auto& m, const auto& L, const auto& C, const auto& X, const Team& T,
+                                TrajDev tr, int P, const double* qfrc_applied, const double* xfrc_applied, CostDev cost, double* warm_c, double* cost_c) {
   const int pt = blockIdx.x;
   load_state(m, L, T, tr, pt, pt / P, qfrc_applied, xfrc_applied);
   forward_skip(m, L, C, X, T, STAGE_NONE, FD_NITER, 0.0);
@@ -108,14 +115,28 @@ __global__ __launch_bounds__(TEAM) void k_fd_centre_coop(DevModel mg, WsLayout L
                            tr.ctrl + (size_t)pt * m.nu);
 }
 
-__global__ __launch_bounds__(TEAM) void k_fd_cols_coop(DevModel mg, WsLayout L, CoopLayout C, CoopAux Xg, TrajDev tr,
-                                                       int P, const double* qfrc_applied, const double* xfrc_applied,
-                                                       CostDev cost, const double* warm_c, const double* cost_c,
-                                                       double* deriv) {
+__global__ __launch_bounds__(TEAM) void k_fd_centre_coop(DevModel mg, WsLayout L, CoopLayout C, CoopAux Xg, TrajDev tr, int P, const double* qfrc_applied, const double* xfrc_applied, CostDev cost, double* warm_c, double* cost_c) {
   Team T = make_team(L, C);
   DevModel m;
   CoopAux X;
   stage_model(mg, Xg, L, C, T, m, X);
+  fd_centre_body(m, L, C, X, T, tr, P, qfrc_applied, xfrc_applied, cost, warm_c, cost_c);
+}
+
+// model-specific instance (static_models.h): compile-time sizes, tables and LDS layout
+template <class SM, class SX>
+__global__ __launch_bounds__(TEAM) void k_fd_centre_s(DevModel mg, TrajDev tr, int P, const double* qfrc_applied, const double* xfrc_applied, CostDev cost, double* warm_c, double* cost_c) {
+  static constexpr WsLayout L = make_layout(SM{});
+  static constexpr CoopLayout C = make_coop_layout(SM{}, SX::npair);
+  static constexpr SX X{};
+  Team T = make_team(L, C);
+  SM m;
+  stage_model_s(mg, L, C, T, m);
+  fd_centre_body(m, L, C, X, T, tr, P, qfrc_applied, xfrc_applied, cost, warm_c, cost_c);
+}
+
+__device__ inline void fd_cols_body(const auto& m, const auto& L, const auto& C, const auto& X, const Team& T,
+                                TrajDev tr, int P, const double* qfrc_applied, const double* xfrc_applied, CostDev cost, const double* warm_c, const double* cost_c, double* deriv) {
   const int nv = m.nv, nu = m.nu;
   const int nctrl = nu < nv ? nu : nv;  // mjderivative.cpp:78-82 (assumes nv >= nu)
   const int ncol = nctrl + 2 * nv;
@@ -197,16 +218,28 @@ __global__ __launch_bounds__(TEAM) void k_fd_cols_coop(DevModel mg, WsLayout L, 
   }
 }
 
-__global__ __launch_bounds__(TEAM) void k_rollout_coop(DevModel mg, WsLayout L, CoopLayout C, CoopAux Xg, int S, int A,
-                                                       int P, TrajDev nom, TrajDev out, int out_is_cand,
-                                                       const double* K, const double* k, const double* alphas,
-                                                       TrajDev dinit, const double* qfrc_applied,
-                                                       const double* xfrc_applied, int passive, CostDev cost,
-                                                       double* cost_cand) {
+__global__ __launch_bounds__(TEAM) void k_fd_cols_coop(DevModel mg, WsLayout L, CoopLayout C, CoopAux Xg, TrajDev tr, int P, const double* qfrc_applied, const double* xfrc_applied, CostDev cost, const double* warm_c, const double* cost_c, double* deriv) {
   Team T = make_team(L, C);
   DevModel m;
   CoopAux X;
   stage_model(mg, Xg, L, C, T, m, X);
+  fd_cols_body(m, L, C, X, T, tr, P, qfrc_applied, xfrc_applied, cost, warm_c, cost_c, deriv);
+}
+
+// model-specific instance (static_models.h): compile-time sizes, tables and LDS layout
+template <class SM, class SX>
+__global__ __launch_bounds__(TEAM) void k_fd_cols_s(DevModel mg, TrajDev tr, int P, const double* qfrc_applied, const double* xfrc_applied, CostDev cost, const double* warm_c, const double* cost_c, double* deriv) {
+  static constexpr WsLayout L = make_layout(SM{});
+  static constexpr CoopLayout C = make_coop_layout(SM{}, SX::npair);
+  static constexpr SX X{};
+  Team T = make_team(L, C);
+  SM m;
+  stage_model_s(mg, L, C, T, m);
+  fd_cols_body(m, L, C, X, T, tr, P, qfrc_applied, xfrc_applied, cost, warm_c, cost_c, deriv);
+}
+
+__device__ inline void rollout_body(const auto& m, const auto& L, const auto& C, const auto& X, const Team& T,
+                                int S, int A, int P, TrajDev nom, TrajDev out, int out_is_cand, const double* K, const double* k, const double* alphas, TrajDev dinit, const double* qfrc_applied, const double* xfrc_applied, int passive, CostDev cost, double* cost_cand) {
   const int lane = blockIdx.x;
   const int s = lane / A, a = lane % A;
   const int nq = m.nq, nv = m.nv, nu = m.nu, nx = 2 * nv;
@@ -253,6 +286,26 @@ __global__ __launch_bounds__(TEAM) void k_rollout_coop(DevModel mg, WsLayout L, 
   if (T.tid == 0 && cost_cand) cost_cand[lane] = c;
 }
 
+__global__ __launch_bounds__(TEAM) void k_rollout_coop(DevModel mg, WsLayout L, CoopLayout C, CoopAux Xg, int S, int A, int P, TrajDev nom, TrajDev out, int out_is_cand, const double* K, const double* k, const double* alphas, TrajDev dinit, const double* qfrc_applied, const double* xfrc_applied, int passive, CostDev cost, double* cost_cand) {
+  Team T = make_team(L, C);
+  DevModel m;
+  CoopAux X;
+  stage_model(mg, Xg, L, C, T, m, X);
+  rollout_body(m, L, C, X, T, S, A, P, nom, out, out_is_cand, K, k, alphas, dinit, qfrc_applied, xfrc_applied, passive, cost, cost_cand);
+}
+
+// model-specific instance (static_models.h): compile-time sizes, tables and LDS layout
+template <class SM, class SX>
+__global__ __launch_bounds__(TEAM) void k_rollout_s(DevModel mg, int S, int A, int P, TrajDev nom, TrajDev out, int out_is_cand, const double* K, const double* k, const double* alphas, TrajDev dinit, const double* qfrc_applied, const double* xfrc_applied, int passive, CostDev cost, double* cost_cand) {
+  static constexpr WsLayout L = make_layout(SM{});
+  static constexpr CoopLayout C = make_coop_layout(SM{}, SX::npair);
+  static constexpr SX X{};
+  Team T = make_team(L, C);
+  SM m;
+  stage_model_s(mg, L, C, T, m);
+  rollout_body(m, L, C, X, T, S, A, P, nom, out, out_is_cand, K, k, alphas, dinit, qfrc_applied, xfrc_applied, passive, cost, cost_cand);
+}
+
 template <typename K>
 hipError_t allow_lds(K kern, size_t lds) {
   if (lds <= 65536) return hipSuccess;
@@ -270,7 +323,22 @@ hipError_t launch_fd_centre_coop(const DevModel& m, const WsLayout& L, const Coo
                                  TrajDev tr, int npts, int P, const double* qfrc_applied, const double* xfrc_applied,
                                  CostDev cost, double* warm_c, double* cost_c, hipStream_t st) {
   if (npts <= 0) return hipSuccess;
-  hipError_t e = allow_lds(k_fd_centre_coop, coop_lds_bytes(L, C));
+  const size_t lds = coop_lds_bytes(L, C);
+  hipError_t e;
+#define ILQG_CASE(id, SMT, SXT)                                                                                 \
+  case id:                                                                                                      \
+    e = allow_lds(k_fd_centre_s<stat::SMT, stat::SXT>, lds);                                                    \
+    if (e != hipSuccess) return e;                                                                              \
+    hipLaunchKernelGGL((k_fd_centre_s<stat::SMT, stat::SXT>), dim3(npts), dim3(TEAM), lds, st, m, tr, P,         \
+                       qfrc_applied, xfrc_applied, cost, warm_c, cost_c);                                       \
+    return hipGetLastError();
+  switch (m.static_id) {
+    ILQG_STATIC_MODELS(ILQG_CASE)
+    default:
+      break;
+  }
+#undef ILQG_CASE
+  e = allow_lds(k_fd_centre_coop, coop_lds_bytes(L, C));
   if (e != hipSuccess) return e;
   hipLaunchKernelGGL(k_fd_centre_coop, dim3(npts), dim3(TEAM), coop_lds_bytes(L, C), st, m, L, C, X, tr, P,
                      qfrc_applied, xfrc_applied, cost, warm_c, cost_c);
@@ -284,7 +352,22 @@ hipError_t launch_fd_cols_coop(const DevModel& m, const WsLayout& L, const CoopL
   const int nctrl = m.nu < m.nv ? m.nu : m.nv;
   const long blocks = (long)npts * (nctrl + 2 * m.nv);
   if (blocks <= 0) return hipSuccess;
-  hipError_t e = allow_lds(k_fd_cols_coop, coop_lds_bytes(L, C));
+  const size_t lds = coop_lds_bytes(L, C);
+  hipError_t e;
+#define ILQG_CASE(id, SMT, SXT)                                                                                 \
+  case id:                                                                                                      \
+    e = allow_lds(k_fd_cols_s<stat::SMT, stat::SXT>, lds);                                                      \
+    if (e != hipSuccess) return e;                                                                              \
+    hipLaunchKernelGGL((k_fd_cols_s<stat::SMT, stat::SXT>), dim3((unsigned)blocks), dim3(TEAM), lds, st, m, tr,  \
+                       P, qfrc_applied, xfrc_applied, cost, warm_c, cost_c, deriv);                             \
+    return hipGetLastError();
+  switch (m.static_id) {
+    ILQG_STATIC_MODELS(ILQG_CASE)
+    default:
+      break;
+  }
+#undef ILQG_CASE
+  e = allow_lds(k_fd_cols_coop, coop_lds_bytes(L, C));
   if (e != hipSuccess) return e;
   hipLaunchKernelGGL(k_fd_cols_coop, dim3((unsigned)blocks), dim3(TEAM), coop_lds_bytes(L, C), st, m, L, C, X, tr, P,
                      qfrc_applied, xfrc_applied, cost, warm_c, cost_c, deriv);
@@ -296,7 +379,23 @@ hipError_t launch_rollout_coop(const DevModel& m, const WsLayout& L, const CoopL
                                const double* k, const double* alphas, TrajDev dinit, const double* qfrc_applied,
                                const double* xfrc_applied, int passive, CostDev cost, double* cost_cand,
                                hipStream_t st) {
-  hipError_t e = allow_lds(k_rollout_coop, coop_lds_bytes(L, C));
+  const size_t lds = coop_lds_bytes(L, C);
+  hipError_t e;
+#define ILQG_CASE(id, SMT, SXT)                                                                                 \
+  case id:                                                                                                      \
+    e = allow_lds(k_rollout_s<stat::SMT, stat::SXT>, lds);                                                      \
+    if (e != hipSuccess) return e;                                                                              \
+    hipLaunchKernelGGL((k_rollout_s<stat::SMT, stat::SXT>), dim3(S * A), dim3(TEAM), lds, st, m, S, A, P,        \
+                       nominal, out, out_is_cand, K, k, alphas, dinit, qfrc_applied, xfrc_applied, passive, cost, \
+                       cost_cand);                                                                              \
+    return hipGetLastError();
+  switch (m.static_id) {
+    ILQG_STATIC_MODELS(ILQG_CASE)
+    default:
+      break;
+  }
+#undef ILQG_CASE
+  e = allow_lds(k_rollout_coop, coop_lds_bytes(L, C));
   if (e != hipSuccess) return e;
   hipLaunchKernelGGL(k_rollout_coop, dim3(S * A), dim3(TEAM), coop_lds_bytes(L, C), st, m, L, C, X, S, A, P, nominal,
                      out, out_is_cand, K, k, alphas, dinit, qfrc_applied, xfrc_applied, passive, cost, cost_cand);

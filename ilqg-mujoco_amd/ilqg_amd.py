@@ -57,6 +57,7 @@ EXPORTS = [
     "ilqg_step_batch", "ilqg_forward_batch", "ilqg_fd_batch",
     "ilqg_solver_create", "ilqg_solver_free", "ilqg_solver_init", "ilqg_solver_set_dinit",
     "ilqg_solver_set_traj", "ilqg_solver_get_traj", "ilqg_solver_set_gains", "ilqg_solver_get_gains",
+    "ilqg_model_static_key", "ilqg_model_static_id",
     "ilqg_solver_get_deriv", "ilqg_solver_set_deriv", "ilqg_solver_get_value", "ilqg_solver_get_costs",
     "ilqg_forward", "ilqg_fd_sweep", "ilqg_backward", "ilqg_iterate", "ilqg_synchronize",
     "ilqg_solver_stream", "ilqg_solver_device_costs", "ilqg_solver_set_stream", "ilqg_solver_set_timing",
@@ -186,6 +187,21 @@ class Model:
         buf = ctypes.create_string_buffer(n.value)
         _check(lib().ilqg_model_blob(self._h, buf, n.value, ctypes.byref(n)))
         return buf.raw
+
+    def static_key(self) -> np.ndarray:
+        """integer data compiled into model-specific kernels (ilqg_model_static_key)"""
+        n = ctypes.c_int()
+        _check(lib().ilqg_model_static_key(self._h, None, 0, ctypes.byref(n)))
+        key = np.zeros(n.value, dtype=np.int32)
+        _check(lib().ilqg_model_static_key(self._h, key.ctypes.data_as(ctypes.POINTER(ctypes.c_int)), n.value,
+                                           ctypes.byref(n)))
+        return key
+
+    def static_id(self) -> int:
+        """compiled model-specific kernel set this model runs on (0 = generic)"""
+        v = ctypes.c_int()
+        _check(lib().ilqg_model_static_id(self._h, ctypes.byref(v)))
+        return v.value
 
     def reset_state(self, n=1):
         """mj_resetData: qpos0, zero velocity/warmstart/ctrl/time."""

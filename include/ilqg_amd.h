@@ -78,6 +78,13 @@ int ilqg_model_timestep(const ilqg_model* m, double* dt);
 int ilqg_model_qpos0(const ilqg_model* m, double* qpos0);
 /* compiled-model record (include/ilqg_model_blob.h); needed = bytes required */
 int ilqg_model_blob(const ilqg_model* m, void* buf, size_t cap, size_t* needed);
+/* specialisation key: the integer data (sizes, topology, static collision
+   pairs, device-image layout) that model-specific kernels compile in
+   (tools/gen_static_models.py); n = entries written (or required if key is
+   NULL).  static_id: the compiled specialisation this model runs on, 0 = the
+   generic kernels.  Results are identical either way. */
+int ilqg_model_static_key(const ilqg_model* m, int* key, int cap, int* n);
+int ilqg_model_static_id(const ilqg_model* m, int* id);
 
 /* ---- batched single-point physics (device) ----
    n independent states; host buffers (n x nq etc.).  step: mj_step

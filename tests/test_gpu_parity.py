@@ -258,3 +258,26 @@ def test_edge_cases(ia, ora):
     hum = ia.Model.load(model_path("humanoid"))
     with pytest.raises(ia.IlqgError, match="nq == nv"):
         ia.ILQR(hum, hum.reset_state(1), 10, ia.Cost())
+
+
+def test_generic_kernels_unbundled_model(ia, ora):
+    """a model outside the compiled specialisations (hopper with a frictionless
+    floor: different condim -> different key) runs the generic cooperative
+    kernels and still matches the oracle bit for bit"""
+    import workloads
+    with open(model_path("hopper")) as f:
+        xml = f.read().replace('condim="3" name="floor"', 'condim="1" name="floor"')
+    m = ia.Model.from_string(xml)
+    assert m.static_id() == 0
+    om = ora.OModel(m.blob())
+    om.lib.L.ora_set_cost_desc(ora.CostDesc.from_cost(ia.HOPPER_COST, m.nq, m.nv, m.nu))
+    dmain = workloads.hopper_dmain(m)
+    il = _oracle_ilqr(ora, om, _state_dict(dmain, 0), 100, "ora_cost_desc_fn", 2)
+    g = ia.ILQR(m, dmain, 100, ia.HOPPER_COST)
+    g.iterate()
+    g.iterate()
+    g.synchronize()
+    ot, oa, gt = il.traj(), il.arrays(), g.traj()
+    exact(gt.qpos.reshape(ot["qpos"].shape), ot["qpos"], "traj.qpos")
+    exact(g.gains()[0][0], oa["K"], "K")
+    exact(g.deriv()[0], oa["deriv"], "deriv")

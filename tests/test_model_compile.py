@@ -125,3 +125,11 @@ def _global_geom_pos(b, g):
         p = p + rot(q, bpos[bb])
         q = qmul(q, bquat[bb])
     return p + rot(q, b["geom_pos"].reshape(-1, 3)[g])
+
+
+def test_static_specialisations_selected(ia):
+    """the bundled models map to their compiled model-specific kernels
+    (csrc/device/static_models.h, regenerated by tools/gen_static_models.py);
+    anything else, e.g. the humanoid, runs the generic kernels"""
+    ids = {n: ia.Model.load(model_path(n)).static_id() for n in ("inverted_pendulum", "hopper", "humanoid")}
+    assert ids == {"inverted_pendulum": 1, "hopper": 2, "humanoid": 0}
