@@ -368,6 +368,14 @@ int ilqg_model_qpos0(const ilqg_model* m, double* q) {
   return ILQG_OK;
 }
 
+// cooperative kernels: LDS workspace within one CU's 160 KB, rollout record
+// prefetch within 4 registers per lane (kernels_coop.hip)
+static bool coop_ok(const ilqg_model* m) {
+  const HostModel& h = m->host;
+  const int rec = h.nq + h.nv + 2 * h.nu + 2 * h.nv * h.nu;
+  return use_coop() && coop_lds_bytes(m->L, m->C) <= kMaxLds && rec <= 4 * 64;
+}
+
 int ilqg_model_static_key(const ilqg_model* m, int* key, int cap, int* n) {
   if (!m || !n) return fail(ILQG_ERR_ARG, "null argument");
   *n = (int)m->key.size();
@@ -496,7 +504,7 @@ int ilqg_fd_batch(const ilqg_model* mc, int n, const double* qpos, const double*
              c + 3 * nq + 3 * nv, c + 3 * nq + 3 * nv + nu, c + 3 * nq + 3 * nv + 2 * nu};
   TrajDev st{s.time.as<double>(), s.qpos.as<double>(), s.qvel.as<double>(), s.warm.as<double>(), s.ctrl.as<double>()};
   WsDev ws{s.wsd.as<double>(), s.wsi.as<int>(), lanes};
-  if (use_coop() && coop_lds_bytes(m->L, m->C) <= kMaxLds) {
+  if (coop_ok(m)) {
     HIPCHK(launch_fd_centre_coop(m->dm, m->L, m->C, m->X, st, n, 1, s.qa.as<double>(), s.xf.as<double>(), cd,
                                  s.warm_c.as<double>(), s.cost_c.as<double>(), m->stream));
     HIPCHK(launch_fd_cols_coop(m->dm, m->L, m->C, m->X, st, n, 1, s.qa.as<double>(), s.xf.as<double>(), cd,
@@ -695,7 +703,7 @@ int ilqg_forward(ilqg_solver* s) {
   const bool multi = s->A > 1;
   TrajDev outv = multi ? s->tview(s->cand) : nom;
   HIPCHK(s->timed(0, [&] {
-    if (use_coop() && coop_lds_bytes(m->L, m->C) <= kMaxLds)
+    if (coop_ok(m))
       return launch_rollout_coop(m->dm, m->L, m->C, m->X, s->S, s->A, s->P, nom, outv, multi ? 1 : 0,
                                  s->K.as<double>(), s->k.as<double>(), s->alphas.as<double>(), di,
                                  s->qfrc_applied.as<double>(), s->xfrc_applied.as<double>(), 0, s->cview(),
@@ -717,7 +725,7 @@ int ilqg_fd_sweep(ilqg_solver* s) {
   TrajDev nom = s->tview(s->traj);
   const int npts = s->S * s->P;
   HIPCHK(s->timed(2, [&] {
-    if (use_coop() && coop_lds_bytes(m->L, m->C) <= kMaxLds)
+    if (coop_ok(m))
       return launch_fd_centre_coop(m->dm, m->L, m->C, m->X, nom, npts, s->P, s->qfrc_applied.as<double>(),
                                    s->xfrc_applied.as<double>(), s->cview(), s->warm_c.as<double>(),
                                    s->cost_c.as<double>(), s->stream);
@@ -726,7 +734,7 @@ int ilqg_fd_sweep(ilqg_solver* s) {
                             s->cost_c.as<double>(), s->stream);
   }));
   HIPCHK(s->timed(3, [&] {
-    if (use_coop() && coop_lds_bytes(m->L, m->C) <= kMaxLds)
+    if (coop_ok(m))
       return launch_fd_cols_coop(m->dm, m->L, m->C, m->X, nom, npts, s->P, s->qfrc_applied.as<double>(),
                                  s->xfrc_applied.as<double>(), s->cview(), s->warm_c.as<double>(),
                                  s->cost_c.as<double>(), s->deriv.as<double>(), s->stream);

@@ -26,7 +26,8 @@ struct Team {
   int tid, nt;
 };
 
-#define TSYNC() __syncthreads()
+// Team synchronisation: team_sync() (dsmall.h).
+#define TSYNC() team_sync()
 
 // diagnostic build only (-DILQG_STAMPS): per-stage s_memtime deltas of
 // workgroup 0, lane 0, taken right after the stage's closing barrier
@@ -34,6 +35,8 @@ struct Team {
 __device__ unsigned long long g_stamp_acc[32];
 __device__ unsigned long long g_stamp_cnt[32];
 __device__ unsigned long long g_stamp_prev;
+__device__ unsigned long long g_newton_iters;  // all workgroups: Newton iterations
+__device__ unsigned long long g_newton_calls;  // all workgroups: solver calls
 #define STAMP(id)                                                            \
   do {                                                                       \
     if (T.tid == 0 && blockIdx.x == 0) {                                     \
@@ -1005,6 +1008,9 @@ __device__ inline void solver_newton(const auto& m, const auto& L, const auto& C
   double cost = bc[2];
   hessian_factor(m, L, C, T, H);
   int iter = 0;
+#ifdef ILQG_STAMPS
+  if (T.tid == 0) atomicAdd(&g_newton_calls, 1ull);
+#endif
   while (iter < maxiter) {
     // search = -H^-1 grad ; line search ; all on lane 0 except the parallel products
     if (nv <= RMAX) {
@@ -1050,7 +1056,7 @@ __device__ inline void solver_newton(const auto& m, const auto& L, const auto& C
           }
         };
         eval(0.0);
-        if (d1 < 0) {
+        if (!(d1 >= 0)) {  // oracle: return 0 iff d1 >= 0 (a NaN proceeds)
           double gtol = LS_TOL * fabs(d1);
           for (int it = 0; it < LS_ITER; it++) {
             double anew = alpha - d1 / d2;
@@ -1075,6 +1081,9 @@ __device__ inline void solver_newton(const auto& m, const auto& L, const auto& C
     FOR_T(i, ne) jar[i] += alpha * Jv[i];
     TSYNC();
     iter++;
+#ifdef ILQG_STAMPS
+    if (T.tid == 0) atomicAdd(&g_newton_iters, 1ull);
+#endif
     STAMP(17);
     double oldcost = cost;
     ccost = constraint_update(m, L, C, T, jar);
@@ -1098,7 +1107,203 @@ __device__ inline void solver_newton(const auto& m, const auto& L, const auto& C
   }
 }
 
-__device__ inline void fwd_constraint(const auto& m, const auto& L, const auto& C, const Team& T,
+
+// ---------------------------------------------------------------------------
+// Newton solver, wave-parallel form for nefc <= 64 (one constraint row per
+// lane).  Every ordered reduction over rows (constraint cost, line-search
+// derivatives) keeps the oracle's row order: each lane forms its row's term,
+// then the terms are added in lane order through v_readlane.  A row that the
+// oracle skips contributes -0.0, the exact identity of IEEE addition.  The
+// Hessian factor is reused while the active set is unchanged: it is a
+// function of (qM, J, D, active set) only, so the reused factor is the one
+// the oracle recomputes, bit for bit.
+
+// s0 + v[lane 0] + v[lane 1] + ... + v[lane n-1], in that order
+__device__ __forceinline__ double lane_sum(double s0, double v, int n) {
+  for (int i = 0; i < n; i++) s0 += bcast(v, i);
+  return s0;
+}
+
+// constraint_update for row registers: returns the cost (uniform) and the
+// active-row mask; with `full` also force/state and qfrc_constraint = J' force
+__device__ inline double cu_fast(const auto& m, const auto& L, const Team& T, double jr, double Di, bool full,
+                                 unsigned long long& mask) {
+  const int nv = m.nv, ne = T.iw[L.nefc];
+  const int r = T.tid;
+  const bool row = r < ne;
+  const bool act = row && jr < 0;
+  if (full) {
+    double* force = T.w + L.efc_force;
+    int* state = T.iw + L.efc_state;
+    if (row) {
+      force[r] = act ? -Di * jr : 0.0;
+      state[r] = act ? 1 : 0;
+    }
+    TSYNC();
+    double* J = T.w + L.efc_J;
+    double* qc = T.w + L.qfrc_con;
+    FOR_T(j, nv) {
+      double s = 0;
+      for (int i = 0; i < ne; i++) s += J[i * nv + j] * force[i];
+      qc[j] = s;
+    }
+    TSYNC();
+  }
+  mask = __ballot(act);
+  const double tv = act ? 0.5 * Di * jr * jr : -0.0;
+  return lane_sum(0.0, tv, ne);
+}
+
+// 0.5 * sum_j (Ma_j - qfs_j)(qacc_j - qas_j), every lane (uniform)
+__device__ inline double gauss_u(int nv, const double* Ma, const double* qfs, const double* qacc, const double* qas) {
+  double g = 0;
+  for (int j = 0; j < nv; j++) g += (Ma[j] - qfs[j]) * (qacc[j] - qas[j]);
+  return 0.5 * g;
+}
+
+__device__ inline void hessian_build_fast(const auto& m, const auto& L, const Team& T, double* H) {
+  const int nv = m.nv, ne = T.iw[L.nefc];
+  double* J = T.w + L.efc_J;
+  double* D = T.w + L.efc_D;
+  double* qM = T.w + L.qM;
+  int* state = T.iw + L.efc_state;
+  FOR_T(e, nv * nv) {
+    int r = e / nv, c = e % nv;
+    if (c <= r) {
+      double h = 0;
+      for (int i = 0; i < ne; i++)
+        if (state[i]) h += J[i * nv + r] * D[i] * J[i * nv + c];
+      H[e] = qM[e] + h;
+    }
+  }
+  TSYNC();
+}
+
+__device__ inline void fwd_constraint_fast(const auto& m, const auto& L, const auto& C, const auto& X,
+                                           const Team& T, int maxiter, double tol) {
+  const int nv = m.nv, ne = T.iw[L.nefc];
+  const double scale = 1 / (m.stat_meaninertia * (nv > 1 ? nv : 1));
+  double* s = T.w + L.s_newton;
+  double *Ma = s, *grad = s + nv, *search = s + 2 * nv, *Mv = s + 3 * nv, *H = s + 4 * nv;
+  double* jar = s + 4 * nv + nv * nv;
+  double* Jv = jar + ne;
+  double* qM = T.w + L.qM;
+  double* qacc = T.w + L.qacc;
+  double* warm = T.w + L.warm;
+  double* J = T.w + L.efc_J;
+  double* aref = T.w + L.efc_aref;
+  double* b = T.w + L.efc_b;
+  double* qfs = T.w + L.qfrc_smooth;
+  double* qas = T.w + L.qacc_smooth;
+  double* qc = T.w + L.qfrc_con;
+  const int r = T.tid;
+  const bool row = r < ne;
+  const double Di = row ? T.w[L.efc_D + r] : 0.0;
+  unsigned long long mask, hmask;
+  // warm-start selection (oracle fwd_constraint): smooth vs warmstart cost
+  double jb = 0, jw = 0;
+  if (row) {
+    jb = tdot(J + r * nv, qas, nv) - aref[r];
+    jw = tdot(J + r * nv, warm, nv) - aref[r];
+    b[r] = jb;
+  }
+  FOR_T(i, nv) Ma[i] = tdot(qM + i * nv, warm, nv);
+  TSYNC();
+  const double cost_smooth = cu_fast(m, L, T, jb, Di, false, mask);
+  const double cost_warm = gauss_u(nv, Ma, qfs, warm, qas) + cu_fast(m, L, T, jw, Di, false, mask);
+  const bool use_smooth = cost_warm > cost_smooth;
+  // solver start (oracle solver_newton): Ma, jar at qacc, full constraint update
+  double jr = use_smooth ? jb : jw;
+  FOR_T(i, nv) qacc[i] = use_smooth ? qas[i] : warm[i];
+  TSYNC();
+  if (use_smooth) {
+    FOR_T(i, nv) Ma[i] = tdot(qM + i * nv, qacc, nv);
+    TSYNC();
+  }
+  double cost = gauss_u(nv, Ma, qfs, qacc, qas) + cu_fast(m, L, T, jr, Di, true, mask);
+  FOR_T(j, nv) grad[j] = (Ma[j] - qfs[j]) - qc[j];
+  hessian_build_fast(m, L, T, H);
+  cholesky_rows(nv, T.tid, H);
+  hmask = mask;
+  int iter = 0;
+#ifdef ILQG_STAMPS
+  if (T.tid == 0) atomicAdd(&g_newton_calls, 1ull);
+#endif
+  while (iter < maxiter) {
+    chol_solve_rows(nv, T.tid, H, grad, search);
+    STAMP(14);
+    FOR_T(i, nv) Mv[i] = tdot(qM + i * nv, search, nv);
+    const double jv = row ? tdot(J + r * nv, search, nv) : 0.0;
+    TSYNC();
+    STAMP(15);
+    // exact line search (oracle linesearch), uniform on every lane
+    double alpha = 0;
+    {
+      double snorm = sqrt(tdot(search, search, nv));
+      if (!(snorm < MINVAL)) {
+        double g1 = 0, g2 = 0, d1, d2, lo = 0, hi = -1;
+        for (int j = 0; j < nv; j++) g1 += search[j] * (Ma[j] - qfs[j]);
+        for (int j = 0; j < nv; j++) g2 += search[j] * Mv[j];
+        auto eval = [&](double a) {
+          const double x = jr + a * jv;
+          const bool on = row && x < 0;
+          const double c1 = on ? Di * x * jv : -0.0;
+          const double c2 = on ? Di * jv * jv : -0.0;
+          d1 = g1 + g2 * a;
+          d2 = g2;
+          for (int i = 0; i < ne; i++) {
+            d1 += bcast(c1, i);
+            d2 += bcast(c2, i);
+          }
+        };
+        eval(0.0);
+        if (!(d1 >= 0)) {
+          double gtol = LS_TOL * fabs(d1);
+          for (int it = 0; it < LS_ITER; it++) {
+            double anew = alpha - d1 / d2;
+            if (hi >= 0 && !(anew > lo && anew < hi)) anew = 0.5 * (lo + hi);
+            alpha = anew;
+            eval(alpha);
+            if (fabs(d1) < gtol) break;
+            if (d1 < 0) lo = alpha; else hi = alpha;
+          }
+        }
+      }
+    }
+    STAMP(16);
+    if (alpha == 0) break;
+    FOR_T(j, nv) {
+      qacc[j] += alpha * search[j];
+      Ma[j] += alpha * Mv[j];
+    }
+    jr += alpha * jv;
+    TSYNC();
+    iter++;
+#ifdef ILQG_STAMPS
+    if (T.tid == 0) atomicAdd(&g_newton_iters, 1ull);
+#endif
+    STAMP(17);
+    const double oldcost = cost;
+    cost = gauss_u(nv, Ma, qfs, qacc, qas) + cu_fast(m, L, T, jr, Di, true, mask);
+    FOR_T(j, nv) grad[j] = (Ma[j] - qfs[j]) - qc[j];
+    TSYNC();
+    const double improvement = scale * (oldcost - cost);
+    const double gradient = scale * sqrt(tdot(grad, grad, nv));
+    STAMP(18);
+    if (improvement < tol || gradient < tol) break;
+    if (mask != hmask) {
+      hessian_build_fast(m, L, T, H);
+      cholesky_rows(nv, T.tid, H);
+      hmask = mask;
+    }
+    STAMP(19);
+  }
+  if (row) jar[r] = jr;
+  FOR_T(i, nv) warm[i] = qacc[i];
+  TSYNC();
+}
+
+__device__ inline void fwd_constraint(const auto& m, const auto& L, const auto& C, const auto& X, const Team& T,
                                       int maxiter, double tol) {
   const int nv = m.nv, ne = T.iw[L.nefc];
   double* qacc = T.w + L.qacc;
@@ -1108,6 +1313,10 @@ __device__ inline void fwd_constraint(const auto& m, const auto& L, const auto& 
   if (!ne) {
     FOR_T(i, nv) { double v = qas[i]; qacc[i] = v; warm[i] = v; qc[i] = 0; }
     TSYNC();
+    return;
+  }
+  if (ne <= TEAM_SIZE && nv <= RMAX) {
+    fwd_constraint_fast(m, L, C, X, T, maxiter, tol);
     return;
   }
   {
@@ -1155,7 +1364,7 @@ __device__ inline void forward_skip(const auto& m, const auto& L, const auto& C,
   STAMP(6);
   fwd_acceleration(m, L, X, T);
   STAMP(7);
-  fwd_constraint(m, L, C, T, maxiter, tol);
+  fwd_constraint(m, L, C, X, T, maxiter, tol);
   STAMP(8);
 }
 

@@ -98,6 +98,7 @@ namespace coop {
 // extra per-team scratch (doubles / ints), appended after the WsLayout block
 struct CoopLayout {
   int qloc, buf6, ftmp, pcon, jc, cterm, rtmp, bc;  // doubles
+  int cdesc, rec;  // cost descriptor copy; prefetched rollout record (x*, u*, K, k)
   int nd;
   int pcnt, rsub, jcnt, ibc;  // ints
   int ni;
@@ -117,6 +118,8 @@ constexpr CoopLayout make_coop_layout(const M& m, int npair) {
   C.cterm = o; o += ne;
   C.rtmp = o; o += 6 * m.nbody;
   C.bc = o; o += 8;
+  C.cdesc = o; o += 3 * (m.nq + m.nv + m.nu);
+  C.rec = o; o += m.nq + m.nv + 2 * m.nu + 2 * m.nv * m.nu;
   C.nd = o;
   C.pcnt = oi; oi += (npair > 0 ? npair : 1);
   C.rsub = oi; oi += ne;

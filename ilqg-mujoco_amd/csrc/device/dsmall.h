@@ -22,7 +22,21 @@
 namespace ilqg {
 namespace coop {
 
+// Team synchronisation.  A team is exactly one wavefront (every cooperative
+// kernel launches 64 lanes), whose LDS accesses the hardware executes in
+// instruction order, so the only thing needed between phases is a compiler
+// barrier that keeps LDS accesses from moving across it: wavefront-scope
+// fences emit no s_waitcnt.  __syncthreads() would also wait for every
+// outstanding global load/store (vmcnt(0)) at each phase boundary, exposing
+// HBM latency in the per-step output stores and prefetches.
+__device__ __forceinline__ void team_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
 using dev::MINVAL;
+constexpr int TEAM_SIZE = 64;  // lanes of a team: exactly one wavefront
 constexpr int RMAX = 8;  // register rows up to this many dofs
 
 // compile-time loop: f(std::integral_constant<int, I>) for I = B .. E-1, so
@@ -67,7 +81,7 @@ __device__ inline void factor_ld_rows(int nv, const auto& pmask, int tid, const 
     pm[j] = j < nv ? pmask[j] : 0ull;
   });
   const unsigned long long self = own ? (pmask[tid] | (1ull << tid)) : 0ull;  // {t} u anc(t)
-  __syncthreads();  // all rows read before LD (may alias mat) is written
+  team_sync();  // all rows read before LD (may alias mat) is written
   sfor<0, RMAX>(SLAM(kk) {
     constexpr int k = RMAX - 1 - SK(kk);
     if (k >= nv) return;
@@ -104,7 +118,7 @@ __device__ inline void factor_ld_rows(int nv, const auto& pmask, int tid, const 
     });
     diaginv[tid] = 1 / rsel(r, tid);
   }
-  __syncthreads();
+  team_sync();
 }
 
 // x <- (L'DL)^-1 x for the factor above; mirrors coop::solve_ld.
@@ -147,9 +161,9 @@ __device__ inline void solve_ld_rows(int nv, const auto& pmask, int tid, const d
     }
     xf[i] = bcast(xt, i);
   });
-  __syncthreads();  // every lane has read x before it is overwritten
+  team_sync();  // every lane has read x before it is overwritten
   if (own) x[tid] = xt;
-  __syncthreads();
+  team_sync();
 }
 
 // In-place dense Cholesky of the lower triangle of H (row-major nv x nv);
@@ -182,13 +196,13 @@ __device__ inline void cholesky_rows(int nv, int tid, double* H) {
       r[j] = (r[j] - s) * tinv;
     }
   });
-  __syncthreads();
+  team_sync();
   if (own) {
     sfor<0, RMAX>(SLAM(jj) {
       if (SK(jj) < nv && SK(jj) <= tid) H[tid * nv + SK(jj)] = r[SK(jj)];
     });
   }
-  __syncthreads();
+  team_sync();
 }
 
 // search = -(H H')^-1 grad with the Cholesky factor in H's lower triangle;
@@ -239,7 +253,7 @@ __device__ inline void chol_solve_rows(int nv, int tid, const double* H, const d
     sb[i] = bcast(g, i);
   });
   if (own) search[tid] = -g;
-  __syncthreads();
+  team_sync();
 }
 
 }  // namespace coop

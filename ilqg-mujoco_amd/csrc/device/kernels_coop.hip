@@ -15,7 +15,7 @@ using namespace coop;
 constexpr double FD_EPS = 1e-6;  // mjderivative.cpp:39
 constexpr int FD_NITER = 30;     // mjderivative.cpp:37
 constexpr int FD_NWARMUP = 3;    // mjderivative.cpp:38
-constexpr int TEAM = 64;
+constexpr int TEAM = TEAM_SIZE;
 
 // LDS: [workspace doubles][coop doubles][model image][workspace ints][coop ints]
 __device__ inline Team make_team(const auto& L, const auto& C) {
@@ -86,6 +86,24 @@ __device__ inline double step_cost(const auto& m, const CostDev& c, const double
   s = cost_terms(s, qvel, c.wv, c.tv, c.lv, m.nv);
   s = cost_terms(s, ctrl, c.wu, c.tu, c.lu, m.nu);
   return s;
+}
+
+// copy the cost descriptor into LDS (C.cdesc): the per-step cost loop on lane 0
+// then reads LDS instead of global memory
+__device__ inline CostDev stage_cost(const auto& m, const auto& C, const Team& T, const CostDev& g) {
+  double* d = T.c + C.cdesc;
+  const int nq = m.nq, nv = m.nv, nu = m.nu;
+  const double* src[9] = {g.wq, g.tq, g.lq, g.wv, g.tv, g.lv, g.wu, g.tu, g.lu};
+  const int off[9] = {0, nq, 2 * nq, 3 * nq, 3 * nq + nv, 3 * nq + 2 * nv, 3 * (nq + nv), 3 * (nq + nv) + nu,
+                      3 * (nq + nv) + 2 * nu};
+  const int len[9] = {nq, nq, nq, nv, nv, nv, nu, nu, nu};
+  for (int a = 0; a < 9; a++) FOR_T(i, len[a]) d[off[a] + i] = src[a][i];
+  TSYNC();
+  CostDev l;
+  l.wq = d + off[0]; l.tq = d + off[1]; l.lq = d + off[2];
+  l.wv = d + off[3]; l.tv = d + off[4]; l.lv = d + off[5];
+  l.wu = d + off[6]; l.tu = d + off[7]; l.lu = d + off[8];
+  return l;
 }
 
 // cpMjData(d, src) from a trajectory record (src/util.cpp:4-14)
@@ -240,32 +258,65 @@ __global__ __launch_bounds__(TEAM) void k_fd_cols_s(DevModel mg, TrajDev tr, int
 
 __device__ inline void rollout_body(const auto& m, const auto& L, const auto& C, const auto& X, const Team& T,
                                 int S, int A, int P, TrajDev nom, TrajDev out, int out_is_cand, const double* K, const double* k, const double* alphas, TrajDev dinit, const double* qfrc_applied, const double* xfrc_applied, int passive, CostDev cost, double* cost_cand) {
+#ifdef ILQG_STAMPS
+  unsigned long long rt0 = __builtin_amdgcn_s_memrealtime(), mt0 = __builtin_amdgcn_s_memtime();
+#endif
   const int lane = blockIdx.x;
   const int s = lane / A, a = lane % A;
   const int nq = m.nq, nv = m.nv, nu = m.nu, nx = 2 * nv;
   load_state(m, L, T, dinit, s, s, qfrc_applied, xfrc_applied);
+  const CostDev cl = stage_cost(m, C, T, cost);
   double* qpos = T.w + L.qpos;
   double* qvel = T.w + L.qvel;
   double* ctrl = T.w + L.ctrl;
   double* warm = T.w + L.warm;
   double* dx = T.w + L.s_fd;
+  // per-point record of the nominal trajectory and gains, [x*_q | x*_v | u* | K | k],
+  // prefetched one point ahead into registers and parked in LDS (C.rec)
+  double* rec = T.c + C.rec;
+  const int R = nq + nv + nu + nu * nx + nu;
+  const double* rq = rec;
+  const double* rv = rec + nq;
+  const double* ru = rec + nq + nv;
+  const double* rK = ru + nu;
+  const double* rk = rK + nu * nx;
+  auto fetch = [&](size_t pn, int t) -> double {
+    if (t < nq) return nom.qpos[pn * nq + t];
+    t -= nq;
+    if (t < nv) return nom.qvel[pn * nv + t];
+    t -= nv;
+    if (t < nu) return nom.ctrl[pn * nu + t];
+    t -= nu;
+    if (t < nu * nx) return K[pn * nu * nx + t];
+    return k[pn * nu + t - nu * nx];
+  };
+  constexpr int PFR = 4;  // registers per lane: R <= 4 * 64
+  double pf[PFR];
+  if (!passive) {
+    FOR_T(t, R) rec[t] = fetch((size_t)s * P + (P - 1), t);
+    TSYNC();
+  }
   const double alpha = alphas ? alphas[a] : 1.0;
   const int ob = out_is_cand ? lane : s;
   double c = 0;
   for (int n = P - 1; n >= 0; n--) {
-    const size_t pn = (size_t)s * P + n;
+    const bool pre = !passive && n > 0;
+    if (pre) {
+      // issue the next point's loads now; their latency hides behind this step
+      const size_t pn1 = (size_t)s * P + (n - 1);
+#pragma unroll
+      for (int q = 0; q < PFR; q++) {
+        const int t = T.tid + q * TEAM;
+        pf[q] = t < R ? fetch(pn1, t) : 0.0;
+      }
+    }
     if (!passive) {
-      const double* xs_q = nom.qpos + pn * nq;
-      const double* xs_v = nom.qvel + pn * nv;
-      FOR_T(j, nx) dx[j] = j < nv ? qpos[j] - xs_q[j] : qvel[j - nv] - xs_v[j - nv];
+      FOR_T(j, nx) dx[j] = j < nv ? qpos[j] - rq[j] : qvel[j - nv] - rv[j - nv];
       TSYNC();
-      const double* Kn = K + pn * nu * nx;
-      const double* kn = k + pn * nu;
-      const double* us = nom.ctrl + pn * nu;
       FOR_T(i, nu) {
         double t = 0;
-        for (int j = 0; j < nx; j++) t += Kn[i + j * nu] * dx[j];
-        ctrl[i] = (t + alpha * kn[i]) + us[i];
+        for (int j = 0; j < nx; j++) t += rK[i + j * nu] * dx[j];
+        ctrl[i] = (t + alpha * rk[i]) + ru[i];
       }
       TSYNC();
     }
@@ -278,12 +329,26 @@ __device__ inline void rollout_body(const auto& m, const auto& L, const auto& C,
     FOR_T(i, nu) out.ctrl[po * nu + i] = ctrl[i];
     if (T.tid == 0) {
       out.time[po] = T.w[L.time];
-      c += step_cost(m, cost, qpos, qvel, ctrl);
+      c += step_cost(m, cl, qpos, qvel, ctrl);
     }
     TSYNC();
     step(m, L, C, X, T);
+    if (pre) {
+#pragma unroll
+      for (int q = 0; q < PFR; q++) {
+        const int t = T.tid + q * TEAM;
+        if (t < R) rec[t] = pf[q];
+      }
+      TSYNC();
+    }
   }
   if (T.tid == 0 && cost_cand) cost_cand[lane] = c;
+#ifdef ILQG_STAMPS
+  if (T.tid == 0 && blockIdx.x == 0) {
+    g_stamp_acc[30] += __builtin_amdgcn_s_memrealtime() - rt0;
+    g_stamp_acc[31] += __builtin_amdgcn_s_memtime() - mt0;
+  }
+#endif
 }
 
 __global__ __launch_bounds__(TEAM) void k_rollout_coop(DevModel mg, WsLayout L, CoopLayout C, CoopAux Xg, int S, int A, int P, TrajDev nom, TrajDev out, int out_is_cand, const double* K, const double* k, const double* alphas, TrajDev dinit, const double* qfrc_applied, const double* xfrc_applied, int passive, CostDev cost, double* cost_cand) {
@@ -410,8 +475,15 @@ extern "C" int ilqg_debug_stamps(unsigned long long* acc, unsigned long long* cn
     return 3;
   if (hipMemcpyFromSymbol(cnt, HIP_SYMBOL(ilqg::coop::g_stamp_cnt), sizeof(unsigned long long) * 32) != hipSuccess)
     return 3;
+  unsigned long long nw[2];
+  (void)hipMemcpyFromSymbol(&nw[0], HIP_SYMBOL(ilqg::coop::g_newton_iters), 8);
+  (void)hipMemcpyFromSymbol(&nw[1], HIP_SYMBOL(ilqg::coop::g_newton_calls), 8);
+  acc[28] = nw[0];
+  acc[29] = nw[1];
   if (reset) {
     unsigned long long z[32] = {0};
+    (void)hipMemcpyToSymbol(HIP_SYMBOL(ilqg::coop::g_newton_iters), z, 8);
+    (void)hipMemcpyToSymbol(HIP_SYMBOL(ilqg::coop::g_newton_calls), z, 8);
     (void)hipMemcpyToSymbol(HIP_SYMBOL(ilqg::coop::g_stamp_acc), z, sizeof(z));
     (void)hipMemcpyToSymbol(HIP_SYMBOL(ilqg::coop::g_stamp_cnt), z, sizeof(z));
   }

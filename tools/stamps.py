@@ -16,12 +16,23 @@ m = ia.Model.load(workloads.model_file(sys.argv[1] if len(sys.argv) > 1 else "ho
 dmain = workloads.hopper_dmain(m, 1) if m.nv == 6 else workloads.pendulum_dmain(m, 1)
 g = ia.ILQR(m, dmain, 500 if m.nv == 6 else 200, ia.HOPPER_COST if m.nv == 6 else ia.PENDULUM_COST)
 g.iterate(); g.synchronize()
+g.set_timing(True)
 for what, fn in (("rollout (1 seed)", g.forward_pass), ("fd sweep", g.fd_sweep)):
     L.ilqg_debug_stamps(acc, cnt, 1)
+    g.timing()
     fn(); g.synchronize()
+    tm = g.timing()
     L.ilqg_debug_stamps(acc, cnt, 1)
     tot = sum(acc[i] for i in range(10))
-    print(f"== {what}: block 0, lane 0, total {tot} cycles")
+    ms = sum(v[0] for v in tm.values())
+    print(f"== {what}: block 0, lane 0, total {tot} ticks (stages 0-9); kernel time {ms:.3f} ms "
+          f"-> {tot / (ms * 1e3):.0f} ticks/us if the stages were all of it")
+    if acc[29]:
+        print(f"   Newton (all workgroups): {acc[29]} solves, {acc[28]} iterations, "
+              f"{acc[28] / acc[29]:.2f} iterations per solve")
+    if acc[30]:
+        print(f"   block 0 lifetime: {acc[30] / 100:.0f} us realtime, {acc[31]} memtime ticks "
+              f"-> shader clock {acc[31] / (acc[30] / 100) :.0f} MHz")
     for i in range(22):
         if cnt[i]:
             print(f"  {NAMES[i]:24s} calls {cnt[i]:6d}  cycles/call {acc[i]/cnt[i]:9.0f}  share {acc[i]/max(tot,1):6.1%}")
