@@ -710,52 +710,55 @@ __device__ inline void fwd_velocity(const auto& m, const auto& L, const auto& C,
   double* cdd = T.w + L.cdof_dot;
   double* qvel = T.w + L.qvel;
   double* qpos = T.w + L.qpos;
-  // com velocities (serial tree recursion): lane 0
-  if (T.tid == 0) {
-    for (int k = 0; k < 6; k++) cvelw[k] = 0;
+  // com velocities.  The recursion cvel_i = cvel_parent + sum_dof cdof*qvel is
+  // component-wise, so it runs as 6 parallel chains (lane k = component k);
+  // each dof's pre-update cvel is recorded (s_con) and the cdof_dot cross
+  // products, which mix components but feed nothing back, follow one lane per
+  // dof.  Per component the operations are the oracle's, in its order.
+  double* cvb = T.w + L.s_con;  // 6 x nv: cvel seen by each dof
+  FOR_T(k, 6) {
+    cvelw[k] = 0;
+    double cv = 0;
+    int prev = 0;
     for (int i = 1; i < nb; i++) {
-      int bda = m.body_dofadr[i];
-      double cvel[6], tmp[6], cd[6], r[6];
-      ldm<6>(cvel, cvelw + 6 * m.body_parentid[i]);
+      const int bda = m.body_dofadr[i], pid = m.body_parentid[i];
+      if (pid != prev) cv = cvelw[6 * pid + k];
       for (int j = 0; j < m.body_dofnum[i]; j++) {
-        int type = m.jnt_type[m.dof_jntid[bda + j]];
+        const int type = m.jnt_type[m.dof_jntid[bda + j]];
         if (type == JNT_FREE) {
-          for (int k = 0; k < 18; k++) cdd[6 * (bda + j) + k] = 0;
-          for (int k = 0; k < 6; k++) {
-            double s = 0;
-            for (int q = 0; q < 3; q++) s += cdof[6 * (bda + q) + k] * qvel[bda + q];
-            tmp[k] = s;
-          }
-          for (int k = 0; k < 6; k++) cvel[k] += tmp[k];
+          double t = 0;
+          for (int q = 0; q < 3; q++) t += cdof[6 * (bda + q) + k] * qvel[bda + q];
+          cv += t;
           j += 3;
         }
         if (type == JNT_FREE || type == JNT_BALL) {
-          for (int k = 0; k < 3; k++) {
-            ldm<6>(cd, cdof + 6 * (bda + j + k));
-            cross_motion(r, cvel, cd);
-            for (int q = 0; q < 6; q++) cdd[6 * (bda + j + k) + q] = r[q];
-          }
-          for (int k = 0; k < 6; k++) {
-            double s = 0;
-            for (int q = 0; q < 3; q++) s += cdof[6 * (bda + j + q) + k] * qvel[bda + j + q];
-            tmp[k] = s;
-          }
-          for (int k = 0; k < 6; k++) cvel[k] += tmp[k];
+          for (int q = 0; q < 3; q++) cvb[6 * (bda + j + q) + k] = cv;
+          double t = 0;
+          for (int q = 0; q < 3; q++) t += cdof[6 * (bda + j + q) + k] * qvel[bda + j + q];
+          cv += t;
           j += 2;
         } else {
-          ldm<6>(cd, cdof + 6 * (bda + j));
-          cross_motion(r, cvel, cd);
-          for (int q = 0; q < 6; q++) cdd[6 * (bda + j) + q] = r[q];
-          double qv = qvel[bda + j];
-          for (int k = 0; k < 6; k++) {
-            double s = 0;
-            s += cd[k] * qv;
-            tmp[k] = s;
-          }
-          for (int k = 0; k < 6; k++) cvel[k] += tmp[k];
+          cvb[6 * (bda + j) + k] = cv;
+          double t = 0;
+          t += cdof[6 * (bda + j) + k] * qvel[bda + j];
+          cv += t;
         }
       }
-      for (int k = 0; k < 6; k++) cvelw[6 * i + k] = cvel[k];
+      cvelw[6 * i + k] = cv;
+      prev = i;
+    }
+  }
+  TSYNC();
+  FOR_T(d, nv) {
+    const int jid = m.dof_jntid[d];
+    if (m.jnt_type[jid] == JNT_FREE && d < m.jnt_dofadr[jid] + 3) {
+      for (int q = 0; q < 6; q++) cdd[6 * d + q] = 0;
+    } else {
+      double cv[6], cd[6], r[6];
+      ldm<6>(cv, cvb + 6 * d);
+      ldm<6>(cd, cdof + 6 * d);
+      cross_motion(r, cv, cd);
+      for (int q = 0; q < 6; q++) cdd[6 * d + q] = r[q];
     }
   }
   // passive forces: one lane per dof (hinge/slide springs; ball/free rejected on the host)
