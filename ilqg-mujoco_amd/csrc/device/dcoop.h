@@ -30,28 +30,46 @@ struct Team {
 #define TSYNC() team_sync()
 
 // diagnostic build only (-DILQG_STAMPS): per-stage s_memtime deltas of
-// workgroup 0, lane 0, taken right after the stage's closing barrier
+// workgroup 0, lane 0, accumulated in LDS (a global read-modify-write per
+// stamp would itself wait on memory) and flushed once at kernel end
 #ifdef ILQG_STAMPS
 __device__ unsigned long long g_stamp_acc[32];
 __device__ unsigned long long g_stamp_cnt[32];
-__device__ unsigned long long g_stamp_prev;
 __device__ unsigned long long g_newton_iters;  // all workgroups: Newton iterations
 __device__ unsigned long long g_newton_calls;  // all workgroups: solver calls
+__shared__ unsigned long long s_stamp_acc[24], s_stamp_cnt[24], s_stamp_prev;
 #define STAMP(id)                                                            \
   do {                                                                       \
     if (T.tid == 0 && blockIdx.x == 0) {                                     \
       unsigned long long t_ = __builtin_amdgcn_s_memtime();                  \
       if ((id) >= 0) {                                                       \
-        g_stamp_acc[(id) < 0 ? 0 : (id)] += t_ - g_stamp_prev;               \
-        g_stamp_cnt[(id) < 0 ? 0 : (id)]++;                                  \
+        s_stamp_acc[(id) < 0 ? 0 : (id)] += t_ - s_stamp_prev;               \
+        s_stamp_cnt[(id) < 0 ? 0 : (id)]++;                                  \
       }                                                                      \
-      g_stamp_prev = t_;                                                     \
+      s_stamp_prev = t_;                                                     \
     }                                                                        \
+  } while (0)
+#define STAMP_INIT()                                                         \
+  do {                                                                       \
+    if (T.tid == 0 && blockIdx.x == 0) {                                     \
+      for (int i_ = 0; i_ < 24; i_++) s_stamp_acc[i_] = s_stamp_cnt[i_] = 0; \
+      s_stamp_prev = __builtin_amdgcn_s_memtime();                           \
+    }                                                                        \
+  } while (0)
+#define STAMP_FLUSH()                                                        \
+  do {                                                                       \
+    if (T.tid == 0 && blockIdx.x == 0)                                       \
+      for (int i_ = 0; i_ < 24; i_++) {                                      \
+        g_stamp_acc[i_] += s_stamp_acc[i_];                                  \
+        g_stamp_cnt[i_] += s_stamp_cnt[i_];                                  \
+      }                                                                      \
   } while (0)
 #else
 #define STAMP(id) \
   do {            \
   } while (0)
+#define STAMP_INIT() STAMP(-1)
+#define STAMP_FLUSH() STAMP(-1)
 #endif
 #define FOR_T(v, n) for (int v = T.tid; v < (n); v += T.nt)
 
@@ -860,6 +878,11 @@ __device__ inline void fwd_acceleration(const auto& m, const auto& L, const auto
   double* scom = T.w + L.scom;
   double* cdof = T.w + L.cdof;
   double* qs = T.w + L.qacc_smooth;
+  // any nonzero xfrc_applied on a non-world body? (else the per-body loop below
+  // skips every body, so leaving it out changes nothing)
+  unsigned long long fmask = 0;
+  for (int i0 = 6; i0 < 6 * m.nbody; i0 += TEAM_SIZE) fmask |= __ballot(i0 + T.tid < 6 * m.nbody && xf[i0 + T.tid] != 0);
+  const bool anyf = fmask != 0ull;
   FOR_T(j, nv) {
     double s = 0;
     for (int i = 0; i < nu; i++) s += amom[i * nv + j] * af[i];
@@ -868,7 +891,7 @@ __device__ inline void fwd_acceleration(const auto& m, const auto& L, const auto
     v += qap[j];
     v += s;
     // xfrc_applied: jac columns of dof j at each loaded body's COM
-    for (int b = 1; b < m.nbody; b++) {
+    for (int b = 1; anyf && b < m.nbody; b++) {
       double f[6];
       ldm<6>(f, xf + 6 * b);
       if (f[0] == 0 && f[1] == 0 && f[2] == 0 && f[3] == 0 && f[4] == 0 && f[5] == 0) continue;
@@ -1407,17 +1430,14 @@ __device__ inline void reset_data(const auto& m, const auto& L, const Team& T) {
   TSYNC();
 }
 
+// mj_checkPos/Vel/Acc test: any NaN/huge entry (a wave ballot, no serial scan)
 __device__ inline int any_bad(const Team& T, const auto& C, const double* x, int n) {
-  if (T.tid == 0) {
-    int bad = 0;
-    for (int i = 0; i < n; i++)
-      if (is_bad(x[i])) { bad = 1; break; }
-    T.ci[C.ibc + 1] = bad;
+  unsigned long long bad = 0;
+  for (int i0 = 0; i0 < n; i0 += TEAM_SIZE) {
+    const int i = i0 + T.tid;
+    bad |= __ballot(i < n && is_bad(x[i]));
   }
-  TSYNC();
-  int r = T.ci[C.ibc + 1];
-  TSYNC();
-  return r;
+  return bad != 0ull;
 }
 
 __device__ inline void euler(const auto& m, const auto& L, const auto& C, const auto& X,
@@ -1428,9 +1448,9 @@ __device__ inline void euler(const auto& m, const auto& L, const auto& C, const 
   double* qM = T.w + L.qM;
   double* dq = T.w + L.qacc;
   double* qvel = T.w + L.qvel;
-  bool dmp = false;
-  for (int i = 0; i < nv; i++)
-    if (m.dof_damping[i] > 0) { dmp = true; break; }
+  unsigned long long dmask = 0;
+  for (int i0 = 0; i0 < nv; i0 += TEAM_SIZE) dmask |= __ballot(i0 + T.tid < nv && m.dof_damping[i0 + T.tid] > 0);
+  const bool dmp = dmask != 0ull;
   if (!dmp) {
     FOR_T(i, nv) qacc[i] = dq[i];
     TSYNC();

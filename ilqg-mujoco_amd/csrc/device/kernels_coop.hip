@@ -123,6 +123,7 @@ __device__ inline void load_state(const auto& m, const auto& L, const Team& T, c
 
 __device__ inline void fd_centre_body(const auto& m, const auto& L, const auto& C, const auto& X, const Team& T,
                                 TrajDev tr, int P, const double* qfrc_applied, const double* xfrc_applied, CostDev cost, double* warm_c, double* cost_c) {
+  STAMP_INIT();
   const int pt = blockIdx.x;
   load_state(m, L, T, tr, pt, pt / P, qfrc_applied, xfrc_applied);
   forward_skip(m, L, C, X, T, STAGE_NONE, FD_NITER, 0.0);
@@ -131,6 +132,7 @@ __device__ inline void fd_centre_body(const auto& m, const auto& L, const auto& 
   if (T.tid == 0)
     cost_c[pt] = step_cost(m, cost, tr.qpos + (size_t)pt * m.nq, tr.qvel + (size_t)pt * m.nv,
                            tr.ctrl + (size_t)pt * m.nu);
+  STAMP_FLUSH();
 }
 
 __global__ __launch_bounds__(TEAM) void k_fd_centre_coop(DevModel mg, WsLayout L, CoopLayout C, CoopAux Xg, TrajDev tr, int P, const double* qfrc_applied, const double* xfrc_applied, CostDev cost, double* warm_c, double* cost_c) {
@@ -155,6 +157,7 @@ __global__ __launch_bounds__(TEAM) void k_fd_centre_s(DevModel mg, TrajDev tr, i
 
 __device__ inline void fd_cols_body(const auto& m, const auto& L, const auto& C, const auto& X, const Team& T,
                                 TrajDev tr, int P, const double* qfrc_applied, const double* xfrc_applied, CostDev cost, const double* warm_c, const double* cost_c, double* deriv) {
+  STAMP_INIT();
   const int nv = m.nv, nu = m.nu;
   const int nctrl = nu < nv ? nu : nv;  // mjderivative.cpp:78-82 (assumes nv >= nu)
   const int ncol = nctrl + 2 * nv;
@@ -234,6 +237,7 @@ __device__ inline void fd_cols_body(const auto& m, const auto& L, const auto& C,
     else if (kind == 1) dr[nv * nv + i + j * nv] = v;
     else dr[i + j * nv] = v;
   }
+  STAMP_FLUSH();
 }
 
 __global__ __launch_bounds__(TEAM) void k_fd_cols_coop(DevModel mg, WsLayout L, CoopLayout C, CoopAux Xg, TrajDev tr, int P, const double* qfrc_applied, const double* xfrc_applied, CostDev cost, const double* warm_c, const double* cost_c, double* deriv) {
@@ -258,6 +262,7 @@ __global__ __launch_bounds__(TEAM) void k_fd_cols_s(DevModel mg, TrajDev tr, int
 
 __device__ inline void rollout_body(const auto& m, const auto& L, const auto& C, const auto& X, const Team& T,
                                 int S, int A, int P, TrajDev nom, TrajDev out, int out_is_cand, const double* K, const double* k, const double* alphas, TrajDev dinit, const double* qfrc_applied, const double* xfrc_applied, int passive, CostDev cost, double* cost_cand) {
+  STAMP_INIT();
 #ifdef ILQG_STAMPS
   unsigned long long rt0 = __builtin_amdgcn_s_memrealtime(), mt0 = __builtin_amdgcn_s_memtime();
 #endif
@@ -349,6 +354,7 @@ __device__ inline void rollout_body(const auto& m, const auto& L, const auto& C,
     g_stamp_acc[31] += __builtin_amdgcn_s_memtime() - mt0;
   }
 #endif
+  STAMP_FLUSH();
 }
 
 __global__ __launch_bounds__(TEAM) void k_rollout_coop(DevModel mg, WsLayout L, CoopLayout C, CoopAux Xg, int S, int A, int P, TrajDev nom, TrajDev out, int out_is_cand, const double* K, const double* k, const double* alphas, TrajDev dinit, const double* qfrc_applied, const double* xfrc_applied, int passive, CostDev cost, double* cost_cand) {
