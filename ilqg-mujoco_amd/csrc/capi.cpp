@@ -5,6 +5,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <string>
@@ -92,11 +93,13 @@ int check_device_support(const HostModel& m, bool solver, std::string& why) {
     if (!power_ok(m.geom_solimp[5 * g + 4])) { why = "solimp power must be an integer in [1,8]"; return ILQG_ERR_UNSUPPORTED; }
   if (m.opt_disableflags != 0) { why = "disableflags are not supported"; return ILQG_ERR_UNSUPPORTED; }
   if (solver) {
-    if (m.nq != m.nv) {
-      why = "ILQR state x = [qpos; qvel] assumes nq == nv (inc/ilqr.h:90, quirk Q21)";
+    // nq != nv (ball/free joints): the state difference runs in the tangent
+    // space (oracle ora_state_diff), an extension of inc/ilqr.h:90 (quirk Q21)
+    if (m.nu > 32 || m.nu < 1) { why = "nu must be in [1, 32]"; return ILQG_ERR_UNSUPPORTED; }
+    if (backward_lds_bytes(m.nv, m.nu) > 160 * 1024) {
+      why = "the Riccati workspace exceeds one CU's 160 KB of LDS";
       return ILQG_ERR_UNSUPPORTED;
     }
-    if (m.nu > 32 || m.nu < 1) { why = "nu must be in [1, 32]"; return ILQG_ERR_UNSUPPORTED; }
   }
   return ILQG_OK;
 }
@@ -218,6 +221,9 @@ struct ilqg_model {
     X.pmask = h.nv <= 64 ? reinterpret_cast<const unsigned long long*>(static_cast<unsigned char*>(buf.p) + pmask_at)
                          : nullptr;
     C = coop::make_coop_layout(dm, npair);
+    if (getenv("ILQG_VERBOSE"))
+      fprintf(stderr, "ilqg: model nq=%d nv=%d static_id=%d lds/team=%zu B (ws %d + coop %d + image %d doubles, %d ints)\n",
+              h.nq, h.nv, dm.static_id, coop_lds_bytes(L, C), L.nd, C.nd, C.imgd, L.ni + C.ni);
     if (!stream) HIPCHK(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
     dev = device;
     return ILQG_OK;

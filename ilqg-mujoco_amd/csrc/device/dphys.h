@@ -140,6 +140,24 @@ __device__ __forceinline__ void quat_mul(double* r, const double* a, const doubl
   double t3 = a[0] * b[3] + a[1] * b[2] - a[2] * b[1] + a[3] * b[0];
   r[0] = t0; r[1] = t1; r[2] = t2; r[3] = t3;
 }
+// dof j of x_a (-) x_b (oracle ora_state_diff): plain difference for
+// slide/hinge dofs and free-joint translations; quaternion dofs use the
+// first-order log map 2 sign(w) v of conj(q_b) q_a.  For models without
+// ball/free joints this is exactly qpos_a[j] - qpos_b[j].
+template <class M, class PA, class PB>
+__device__ inline double state_diff_dof(const M& m, int j, const PA& qa, const PB& qb) {
+  const int jid = m.dof_jntid[j], t = m.jnt_type[jid], qadr = m.jnt_qposadr[jid], dadr = m.jnt_dofadr[jid];
+  if ((t == JNT_FREE && j >= dadr + 3) || t == JNT_BALL) {
+    const int qo = qadr + (t == JNT_FREE ? 3 : 0), k = j - dadr - (t == JNT_FREE ? 3 : 0);
+    const double c[4] = {qb[qo], -qb[qo + 1], -qb[qo + 2], -qb[qo + 3]};
+    const double a[4] = {qa[qo], qa[qo + 1], qa[qo + 2], qa[qo + 3]};
+    double q[4];
+    quat_mul(q, c, a);
+    const double sg = q[0] < 0 ? -2.0 : 2.0;
+    return sg * q[1 + k];
+  }
+  return qa[qadr + j - dadr] - qb[qadr + j - dadr];
+}
 __device__ inline void rot_vec_quat(double* r, const double* v, const double* q) {
   if (v[0] == 0 && v[1] == 0 && v[2] == 0) {
     r[0] = r[1] = r[2] = 0;

@@ -192,7 +192,7 @@ __global__ __launch_bounds__(LANE_BLOCK) void k_rollout(DevModel m, WsLayout L, 
       const double* us = nom.ctrl + pn * nu;
       const double* Kn = K + pn * nu * nx;
       const double* kn = k + pn * nu;
-      for (int j = 0; j < nv; j++) dx[j] = qpos[j] - xs_q[j];
+      for (int j = 0; j < nv; j++) dx[j] = state_diff_dof(m, j, qpos, xs_q);
       for (int j = 0; j < nv; j++) dx[nv + j] = qvel[j] - xs_v[j];
       for (int i = 0; i < nu; i++) {
         double t = 0;

@@ -316,7 +316,7 @@ __device__ inline void rollout_body(const auto& m, const auto& L, const auto& C,
       }
     }
     if (!passive) {
-      FOR_T(j, nx) dx[j] = j < nv ? qpos[j] - rq[j] : qvel[j - nv] - rv[j - nv];
+      FOR_T(j, nx) dx[j] = j < nv ? state_diff_dof(m, j, qpos, rq) : qvel[j - nv] - rv[j - nv];
       TSYNC();
       FOR_T(i, nu) {
         double t = 0;

@@ -10,6 +10,7 @@
 // over the LDS banks.
 #include <hip/hip_runtime.h>
 
+#include "dphys.h"
 #include "kernels.h"
 
 namespace ilqg {
@@ -102,22 +103,25 @@ __device__ void ldlt_solve(int n, const double* Lm, const int* transp, double* x
     const int f1 = h1 ? e1 : e0, f2 = h2 ? e2 : e0;
 
 template <int NV_, int NU_>
-__global__ __launch_bounds__(BW_THREADS) void k_backward(int nq, int nv_rt, int nu_rt, int P, double dt, double mu,
-                                                         const double* deriv, TrajDev tr, double* Kg, double* kg,
-                                                         double* Vg, double* vg) {
+__global__ __launch_bounds__(BW_THREADS) void k_backward(DevModel m, int nq, int nv_rt, int nu_rt, int P, double dt,
+                                                         double mu, const double* deriv, TrajDev tr, double* Kg,
+                                                         double* kg, double* Vg, double* vg) {
   const int nv = NV_ > 0 ? NV_ : nv_rt;
   const int nu = NU_ > 0 ? NU_ : nu_rt;
   const int s = blockIdx.x, tid = threadIdx.x;
   const int nx = 2 * nv, D = nv * (2 * nv + nu) + 2 * nv + nu;
-  const int LX = nx + 1;  // padded leading dimension of the nx-row matrices
+  // padded leading dimension of the nx-row matrices (unpadded for large nx,
+  // where LDS capacity binds)
+  const int LX = nx <= 32 ? nx + 1 : nx;
+  const bool pref = D <= BW_PF * BW_THREADS;  // FD record prefetched into LDS
   extern __shared__ double sh[];
-  double* V = sh;                 // nx x nx, ld LX
+  // buffers are reused once dead: V holds V_new (V is read only by stage 1),
+  // A holds T4 (A is last read in stage 5)
+  double* V = sh;                 // nx x nx, ld LX; V_new from stage 7
   double* Vs = V + nx * LX;
-  double* A = Vs + nx * LX;
+  double* A = Vs + nx * LX;       // T4 from stage 6
   double* ABK = A + nx * LX;
-  double* T4 = ABK + nx * LX;
-  double* Vn = T4 + nx * LX;
-  double* B = Vn + nx * LX;       // nx x nu, ld LX
+  double* B = ABK + nx * LX;      // nx x nu, ld LX
   double* T6 = B + nu * LX;       // nx x nu, ld LX
   double* T1 = T6 + nu * LX;      // nu x nx, ld nu
   double* T3 = T1 + nu * nx;
@@ -134,8 +138,10 @@ __global__ __launch_bounds__(BW_THREADS) void k_backward(int nq, int nv_rt, int 
   double* kR = kl + nu;
   double* col = kR + nu;
   double* r = col + nu;
-  double* dl = r + nu;  // FD record of the current step (prefetched)
-  int* trn = (int*)(dl + D);
+  double* dl = r + nu;  // FD record of the current step (prefetched), D doubles when pref
+  int* trn = (int*)(dl + (pref ? D : 0));
+  double* T4 = A;
+  double* Vn = V;
 #ifdef ILQG_STAMPS
   unsigned long long bst_prev = 0;
 #endif
@@ -145,7 +151,8 @@ __global__ __launch_bounds__(BW_THREADS) void k_backward(int nq, int nv_rt, int 
     const double* q0 = deriv + ((size_t)s * P + 0) * D + 2 * nv * nv + nv * nu;
     for (int i = tid; i < nx; i += BW_THREADS) v[i] = q0[i];
     const double* d1 = deriv + ((size_t)s * P + (P > 1 ? 1 : 0)) * D;
-    for (int i = tid; i < D; i += BW_THREADS) dl[i] = d1[i];
+    if (pref)
+      for (int i = tid; i < D; i += BW_THREADS) dl[i] = d1[i];
     __syncthreads();
     for (int e = tid; e < nx * nx; e += BW_THREADS) {
       int i = e % nx, j = e / nx;
@@ -158,7 +165,7 @@ __global__ __launch_bounds__(BW_THREADS) void k_backward(int nq, int nv_rt, int 
     const size_t pc = (size_t)s * P + n, pp = pc - 1;
     // prefetch the next step's FD record; consumed at the end of this step
     double pf[BW_PF];
-    if (n + 1 < P) {
+    if (pref && n + 1 < P) {
       const double* dn1 = deriv + (pc + 1) * D;
 #pragma unroll
       for (int t = 0; t < BW_PF; t++) {
@@ -166,7 +173,7 @@ __global__ __launch_bounds__(BW_THREADS) void k_backward(int nq, int nv_rt, int 
         pf[t] = i < D ? dn1[i] : 0.0;
       }
     }
-    const double* dn = dl;
+    const double* dn = pref ? dl : deriv + pc * D;
     // stage 1: symmetrise V, assemble A/B (differentiator.h:66-71,89-92), q, r, c
     for (int e = tid; e < nx * nx; e += BW_THREADS) {
       int i = e % nx, j = e / nx;
@@ -184,9 +191,14 @@ __global__ __launch_bounds__(BW_THREADS) void k_backward(int nq, int nv_rt, int 
     }
     for (int i = tid; i < nx; i += BW_THREADS) {
       q[i] = dn[2 * nv * nv + nv * nu + i];
-      double xp = i < nv ? tr.qpos[pp * nq + i] : tr.qvel[pp * nv + i - nv];
-      double xc = i < nv ? tr.qpos[pc * nq + i] : tr.qvel[pc * nv + i - nv];
-      c[i] = xp - xc;
+      // c = x*_{n-1} (-) x*_n (inc/ilqr.h:154-157; tangent space for quaternion joints)
+      if (i < nv && nq != nv) {
+        c[i] = dev::state_diff_dof(m, i, tr.qpos + pp * nq, tr.qpos + pc * nq);
+      } else {
+        double xp = i < nv ? tr.qpos[pp * nq + i] : tr.qvel[pp * nv + i - nv];
+        double xc = i < nv ? tr.qpos[pc * nq + i] : tr.qvel[pc * nv + i - nv];
+        c[i] = xp - xc;
+      }
     }
     for (int a = tid; a < nu; a += BW_THREADS) r[a] = dn[2 * nv * nv + nv * nu + nx + a];
     __syncthreads();
@@ -333,12 +345,8 @@ __global__ __launch_bounds__(BW_THREADS) void k_backward(int nq, int nv_rt, int 
     for (int e = tid; e < nu * nx; e += BW_THREADS) Kg[pc * nu * nx + e] = Kl[e];
     for (int a = tid; a < nu; a += BW_THREADS) kg[pc * nu + a] = kl[a];
     __syncthreads();
-    for (int e = tid; e < nx * nx; e += BW_THREADS) {
-      int i = e % nx, j = e / nx;
-      V[i + j * LX] = Vn[i + j * LX];
-    }
-    for (int i = tid; i < nx; i += BW_THREADS) v[i] = vn[i];
-    if (n + 1 < P) {
+    for (int i = tid; i < nx; i += BW_THREADS) v[i] = vn[i];  // V already holds V_new
+    if (pref && n + 1 < P) {
 #pragma unroll
       for (int t = 0; t < BW_PF; t++) {
         int i = tid + t * BW_THREADS;
@@ -360,24 +368,32 @@ __global__ __launch_bounds__(BW_THREADS) void k_backward(int nq, int nv_rt, int 
 template <int NV, int NU>
 void launch_t(const DevModel& m, int S, int P, double mu, const double* deriv, TrajDev tr, double* K, double* k,
               double* V, double* v, size_t lds, hipStream_t st) {
-  hipLaunchKernelGGL((k_backward<NV, NU>), dim3(S), dim3(BW_THREADS), lds, st, m.nq, m.nv, m.nu, P, m.opt_timestep,
-                     mu, deriv, tr, K, k, V, v);
+  hipLaunchKernelGGL((k_backward<NV, NU>), dim3(S), dim3(BW_THREADS), lds, st, m, m.nq, m.nv, m.nu, P,
+                     m.opt_timestep, mu, deriv, tr, K, k, V, v);
 }
 
 }  // namespace
 
 size_t backward_lds_bytes(int nv, int nu) {
-  const size_t nx = 2 * (size_t)nv, LX = nx + 1;
+  const size_t nx = 2 * (size_t)nv, LX = nx <= 32 ? nx + 1 : nx;
   const size_t D = (size_t)nv * (2 * nv + nu) + 2 * nv + nu;
-  size_t nd = 6 * nx * LX + 2 * nu * LX + 3 * (size_t)nu * nx + (size_t)nu * nu + 8 * nx + 4 * (size_t)nu + D;
+  const size_t pre = D <= (size_t)BW_PF * BW_THREADS ? D : 0;
+  size_t nd = 4 * nx * LX + 2 * nu * LX + 3 * (size_t)nu * nx + (size_t)nu * nu + 7 * nx + 4 * (size_t)nu + pre;
   return nd * sizeof(double) + (size_t)nu * sizeof(int) + 16;
 }
 
 hipError_t launch_backward(const DevModel& m, int S, int P, double mu, const double* deriv, TrajDev tr, double* K,
                            double* k, double* V, double* v, hipStream_t st) {
-  if (m.nu > 32 || (size_t)m.nv * (2 * m.nv + m.nu) + 2 * m.nv + m.nu > (size_t)BW_PF * BW_THREADS)
-    return hipErrorInvalidValue;  // prefetch registers / LDLT scratch bound
+  if (m.nu > 32) return hipErrorInvalidValue;  // LDLT scratch bound
   const size_t lds = backward_lds_bytes(m.nv, m.nu);
+  if (lds > 160 * 1024) return hipErrorInvalidValue;
+  if (lds > 65536) {
+    const void* kf = m.nv == 6 && m.nu == 3   ? reinterpret_cast<const void*>(k_backward<6, 3>)
+                     : m.nv == 2 && m.nu == 1 ? reinterpret_cast<const void*>(k_backward<2, 1>)
+                                              : reinterpret_cast<const void*>(k_backward<0, 0>);
+    hipError_t e = hipFuncSetAttribute(kf, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    if (e != hipSuccess) return e;
+  }
   if (m.nv == 6 && m.nu == 3) launch_t<6, 3>(m, S, P, mu, deriv, tr, K, k, V, v, lds, st);
   else if (m.nv == 2 && m.nu == 1) launch_t<2, 1>(m, S, P, mu, deriv, tr, K, k, V, v, lds, st);
   else launch_t<0, 0>(m, S, P, mu, deriv, tr, K, k, V, v, lds, st);

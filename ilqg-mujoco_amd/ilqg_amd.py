@@ -145,6 +145,10 @@ PENDULUM_COST = Cost(wq=[1.0, 10.0], wv=[1.0, 10.0], wu=[1.0])
 # keep the torso up (rootz -> 1.25) and level, damp velocities, small effort
 HOPPER_COST = Cost(wq=[0.0, 10.0, 1.0, 0.1, 0.1, 0.1], tq=[0.0, 1.25, 0.0, 0.0, 0.0, 0.0],
                    wv=[0.1] * 6, wu=[0.01] * 3)
+# build-defined humanoid cost (nq=28, nv=27, nu=21): torso height -> 1.4, upright
+# torso (quaternion w -> 1), damped velocities, small effort
+HUMANOID_COST = Cost(wq=[0.0, 0.0, 10.0, 1.0] + [0.0] * 24, tq=[0.0, 0.0, 1.4, 1.0] + [0.0] * 24,
+                     wv=[0.05] * 27, wu=[0.001] * 21)
 
 
 class Model:

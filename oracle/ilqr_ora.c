@@ -293,9 +293,51 @@ void ora_ldlt_solve(int n, const mjtNum* L, const int* transp, mjtNum* x) {
 /* ---- one Riccati step, ilqr.h:150-174 (quirks Q13-Q18), fixed order ----
    In: V (nx*nx col-major, updated in place), v (nx), deriv (D), xprev/xcur
    (x*_{n-1}, x*_n, 2nv each), dt, mu.  Out: K (nu*nx col-major), k (nu). */
+/* x_a (-) x_b in the tangent space (2nv entries).  Equal, operation for
+   operation, to the reference's x_a - x_b on [qpos; qvel] when the model has
+   no ball/free joints (nq == nv, inc/ilqr.h:90).  Quaternion blocks (an
+   extension: the reference does not support them, quirk Q21) use the
+   first-order log map 2 sign(w) v of qdif = conj(q_b) q_a, with no
+   transcendental function so host and device agree bit for bit. */
+static void ora_quat_diff(mjtNum* d, const mjtNum* qa, const mjtNum* qb) {
+  mjtNum c[4] = {qb[0], -qb[1], -qb[2], -qb[3]}, q[4];
+  q[0] = c[0] * qa[0] - c[1] * qa[1] - c[2] * qa[2] - c[3] * qa[3];
+  q[1] = c[0] * qa[1] + c[1] * qa[0] + c[2] * qa[3] - c[3] * qa[2];
+  q[2] = c[0] * qa[2] - c[1] * qa[3] + c[2] * qa[0] + c[3] * qa[1];
+  q[3] = c[0] * qa[3] + c[1] * qa[2] - c[2] * qa[1] + c[3] * qa[0];
+  mjtNum s = q[0] < 0 ? -2.0 : 2.0;
+  d[0] = s * q[1];
+  d[1] = s * q[2];
+  d[2] = s * q[3];
+}
+void ora_state_diff(const mjModel* m, const mjtNum* qa, const mjtNum* va, const mjtNum* qb, const mjtNum* vb,
+                    mjtNum* dx) {
+  int nv = m->nv;
+  for (int j = 0; j < m->njnt; j++) {
+    int qadr = m->jnt_qposadr[j], dadr = m->jnt_dofadr[j], t = m->jnt_type[j];
+    if (t == mjJNT_FREE) {
+      for (int k = 0; k < 3; k++) dx[dadr + k] = qa[qadr + k] - qb[qadr + k];
+      ora_quat_diff(dx + dadr + 3, qa + qadr + 3, qb + qadr + 3);
+    } else if (t == mjJNT_BALL) {
+      ora_quat_diff(dx + dadr, qa + qadr, qb + qadr);
+    } else {
+      dx[dadr] = qa[qadr] - qb[qadr];
+    }
+  }
+  for (int i = 0; i < nv; i++) dx[nv + i] = va[i] - vb[i];
+}
+
 void ora_riccati_step(int nv, int nu, mjtNum dt, mjtNum mu, const mjtNum* deriv,
                       const mjtNum* xprev, const mjtNum* xcur, mjtNum* V, mjtNum* v,
                       mjtNum* K, mjtNum* kff) {
+  mjtNum c[256];
+  for (int i = 0; i < 2 * nv; i++) c[i] = xprev[i] - xcur[i];
+  ora_riccati_step_c(nv, nu, dt, mu, deriv, c, V, v, K, kff);
+}
+
+/* the step with c = x*_{n-1} (-) x*_n supplied */
+void ora_riccati_step_c(int nv, int nu, mjtNum dt, mjtNum mu, const mjtNum* deriv, const mjtNum* cin,
+                        mjtNum* V, mjtNum* v, mjtNum* K, mjtNum* kff) {
   int nx = 2 * nv;
   mjtNum *A = malloc(sizeof(mjtNum) * nx * nx), *B = malloc(sizeof(mjtNum) * nx * nu);
   mjtNum *Vs = malloc(sizeof(mjtNum) * nx * nx), *T1 = malloc(sizeof(mjtNum) * nu * nx);
@@ -314,7 +356,7 @@ void ora_riccati_step(int nv, int nu, mjtNum dt, mjtNum mu, const mjtNum* deriv,
   for (int j = 0; j < nx; j++)
     for (int i = 0; i < nx; i++) Vs[i + j * nx] = (V[i + j * nx] + V[j + i * nx]) / 2;
   ora_assemble_AB(nv, nu, dt, deriv, A, B);
-  for (int i = 0; i < nx; i++) c[i] = xprev[i] - xcur[i];
+  for (int i = 0; i < nx; i++) c[i] = cin[i];
   for (int i = 0; i < nx; i++) Vs[i + i * nx] += mu;
   /* T1 = B'V */
   for (int j = 0; j < nx; j++)
@@ -454,11 +496,11 @@ void ora_ilqr_forwardPass(ora_ilqr* s) {
   int nx = s->nx, nu = s->nu;
   mjtNum dx[128];
   for (int n = s->N; n >= 0; n--) {
-    const mjtNum* xs = s->dArray[n]->qpos; /* qpos,qvel contiguous */
+    const mjtNum* xs = s->dArray[n]->qpos;
     const mjtNum* us = s->dArray[n]->ctrl;
     const mjtNum* K = s->K + (size_t)n * nu * nx;
     const mjtNum* k = s->k + (size_t)n * nu;
-    for (int j = 0; j < nx; j++) dx[j] = s->d->qpos[j] - xs[j];
+    ora_state_diff(s->m, s->d->qpos, s->d->qvel, xs, s->dArray[n]->qvel, dx);
     for (int a = 0; a < nu; a++) {
       mjtNum t = 0;
       for (int j = 0; j < nx; j++) t += K[a + j * nu] * dx[j];
@@ -487,9 +529,11 @@ void ora_ilqr_backwardPass(ora_ilqr* s) {
   for (int n = 1; n <= s->N; n++) {
     s->cout_lines += 2; /* ilqr.h:146-147 -> counted null sink */
     ora_ilqr_fd_point(s, n);
-    ora_riccati_step(nv, nu, dt, s->mu, s->deriv + (size_t)n * s->D, s->dArray[n - 1]->qpos,
-                     s->dArray[n]->qpos, s->V, s->v, s->K + (size_t)n * nu * nx,
-                     s->k + (size_t)n * nu);
+    mjtNum c[256];
+    ora_state_diff(s->m, s->dArray[n - 1]->qpos, s->dArray[n - 1]->qvel, s->dArray[n]->qpos,
+                   s->dArray[n]->qvel, c);
+    ora_riccati_step_c(nv, nu, dt, s->mu, s->deriv + (size_t)n * s->D, c, s->V, s->v,
+                       s->K + (size_t)n * nu * nx, s->k + (size_t)n * nu);
   }
 }
 

@@ -50,6 +50,11 @@ void ora_riccati_step(int nv, int nu, mjtNum dt, mjtNum mu, const mjtNum* deriv,
                       const mjtNum* xprev, const mjtNum* xcur, mjtNum* V, mjtNum* v,
                       mjtNum* K, mjtNum* kff);
 
+void ora_riccati_step_c(int nv, int nu, mjtNum dt, mjtNum mu, const mjtNum* deriv, const mjtNum* c,
+                        mjtNum* V, mjtNum* v, mjtNum* K, mjtNum* kff);
+void ora_state_diff(const mjModel* m, const mjtNum* qa, const mjtNum* va, const mjtNum* qb, const mjtNum* vb,
+                    mjtNum* dx);
+
 ora_ilqr* ora_ilqr_create(mjModel* m, const mjData* dmain, int N, stepCostFn_t cost, ora_calc_fn calc);
 void ora_ilqr_free(ora_ilqr* s);
 void ora_ilqr_setDInit(ora_ilqr* s, const mjData* dinit);

@@ -255,9 +255,6 @@ def test_edge_cases(ia, ora):
     exact(g.gains()[0][0], il.arrays()["K"], "H=1 K")
     with pytest.raises(ia.IlqgError):
         ia.ILQR(m, dmain, 0, ia.HOPPER_COST)
-    hum = ia.Model.load(model_path("humanoid"))
-    with pytest.raises(ia.IlqgError, match="nq == nv"):
-        ia.ILQR(hum, hum.reset_state(1), 10, ia.Cost())
 
 
 def test_generic_kernels_unbundled_model(ia, ora):
@@ -281,3 +278,31 @@ def test_generic_kernels_unbundled_model(ia, ora):
     exact(gt.qpos.reshape(ot["qpos"].shape), ot["qpos"], "traj.qpos")
     exact(g.gains()[0][0], oa["K"], "K")
     exact(g.deriv()[0], oa["deriv"], "deriv")
+
+
+def test_humanoid_iterate_tangent_space(ia, ora):
+    """humanoid iLQR (free joint, nq=28 != nv=27).  The
+    state difference runs in the tangent space (quaternion dofs by the
+    first-order log map, oracle ora_state_diff); FD, Riccati (nx=54, nu=21,
+    unpadded LDS layout, FD records read from HBM) and rollout match the
+    oracle bit for bit.  Parity vs a reference is unpinned by construction: the
+    reference does not support nq != nv (inc/ilqr.h:90)."""
+    m, om = setup(ia, ora, "humanoid", ia.HUMANOID_COST)
+    st = m.reset_state(1)
+    st.qpos[0, 2] = 1.4  # humanoid.xml:49-50 initial height
+    m.step(st, 5)
+    dstate = _state_dict(st, 0)
+    il = _oracle_ilqr(ora, om, dstate, 6, "ora_cost_desc_fn", 1)
+    g = ia.ILQR(m, st, 6, ia.HUMANOID_COST)
+    g.iterate()
+    g.synchronize()
+    ot, oa, gt = il.traj(), il.arrays(), g.traj()
+    for k in ("qpos", "qvel", "warm", "ctrl"):
+        exact(getattr(gt, k).reshape(ot[k].shape), ot[k], f"traj.{k}")
+    K, k = g.gains()
+    exact(g.deriv()[0], oa["deriv"], "deriv")
+    exact(K[0], oa["K"], "K")
+    exact(k[0], oa["k"], "k")
+    V, v = g.value()
+    exact(V[0], oa["V"], "V")
+    exact(v[0], oa["v"], "v")
