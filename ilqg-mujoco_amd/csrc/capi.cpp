@@ -121,7 +121,8 @@ struct ilqg_model {
   int dev = -1;
   DevBuf buf;
   DevModel dm{};
-  WsLayout L{};
+  WsLayout L{};   // lane-per-evaluation layout
+  WsLayout Lc{};  // cooperative layout (union scratch)
   coop::CoopAux X{};
   coop::CoopLayout C{};
   hipStream_t stream = nullptr;
@@ -215,6 +216,7 @@ struct ilqg_model {
     dm.img_bytes = (int)img.size();
     dm.static_id = use_static() ? static_id : 0;
     L = make_layout(dm);
+    Lc = make_layout(dm, npair);
     X.isanc = reinterpret_cast<const int*>(static_cast<unsigned char*>(buf.p) + isanc_at);
     X.pair = reinterpret_cast<const int*>(static_cast<unsigned char*>(buf.p) + pair_at);
     X.npair = npair;
@@ -223,7 +225,7 @@ struct ilqg_model {
     C = coop::make_coop_layout(dm, npair);
     if (getenv("ILQG_VERBOSE"))
       fprintf(stderr, "ilqg: model nq=%d nv=%d static_id=%d lds/team=%zu B (ws %d + coop %d + image %d doubles, %d ints)\n",
-              h.nq, h.nv, dm.static_id, coop_lds_bytes(L, C), L.nd, C.nd, C.imgd, L.ni + C.ni);
+              h.nq, h.nv, dm.static_id, coop_lds_bytes(Lc, C), Lc.nd, C.nd, C.imgd, Lc.ni + C.ni);
     if (!stream) HIPCHK(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
     dev = device;
     return ILQG_OK;
@@ -379,7 +381,7 @@ int ilqg_model_qpos0(const ilqg_model* m, double* q) {
 static bool coop_ok(const ilqg_model* m) {
   const HostModel& h = m->host;
   const int rec = h.nq + h.nv + 2 * h.nu + 2 * h.nv * h.nu;
-  return use_coop() && coop_lds_bytes(m->L, m->C) <= kMaxLds && rec <= 4 * 64;
+  return use_coop() && coop_lds_bytes(m->Lc, m->C) <= kMaxLds && rec <= 4 * 64;
 }
 
 int ilqg_model_static_key(const ilqg_model* m, int* key, int cap, int* n) {
@@ -511,9 +513,9 @@ int ilqg_fd_batch(const ilqg_model* mc, int n, const double* qpos, const double*
   TrajDev st{s.time.as<double>(), s.qpos.as<double>(), s.qvel.as<double>(), s.warm.as<double>(), s.ctrl.as<double>()};
   WsDev ws{s.wsd.as<double>(), s.wsi.as<int>(), lanes};
   if (coop_ok(m)) {
-    HIPCHK(launch_fd_centre_coop(m->dm, m->L, m->C, m->X, st, n, 1, s.qa.as<double>(), s.xf.as<double>(), cd,
+    HIPCHK(launch_fd_centre_coop(m->dm, m->Lc, m->C, m->X, st, n, 1, s.qa.as<double>(), s.xf.as<double>(), cd,
                                  s.warm_c.as<double>(), s.cost_c.as<double>(), m->stream));
-    HIPCHK(launch_fd_cols_coop(m->dm, m->L, m->C, m->X, st, n, 1, s.qa.as<double>(), s.xf.as<double>(), cd,
+    HIPCHK(launch_fd_cols_coop(m->dm, m->Lc, m->C, m->X, st, n, 1, s.qa.as<double>(), s.xf.as<double>(), cd,
                                s.warm_c.as<double>(), s.cost_c.as<double>(), s.out.as<double>(), m->stream));
   } else {
     HIPCHK(launch_fd_centre(m->dm, m->L, ws, st, n, 1, s.qa.as<double>(), s.xf.as<double>(), cd,
@@ -710,7 +712,7 @@ int ilqg_forward(ilqg_solver* s) {
   TrajDev outv = multi ? s->tview(s->cand) : nom;
   HIPCHK(s->timed(0, [&] {
     if (coop_ok(m))
-      return launch_rollout_coop(m->dm, m->L, m->C, m->X, s->S, s->A, s->P, nom, outv, multi ? 1 : 0,
+      return launch_rollout_coop(m->dm, m->Lc, m->C, m->X, s->S, s->A, s->P, nom, outv, multi ? 1 : 0,
                                  s->K.as<double>(), s->k.as<double>(), s->alphas.as<double>(), di,
                                  s->qfrc_applied.as<double>(), s->xfrc_applied.as<double>(), 0, s->cview(),
                                  s->cost_cand.as<double>(), s->stream);
@@ -732,7 +734,7 @@ int ilqg_fd_sweep(ilqg_solver* s) {
   const int npts = s->S * s->P;
   HIPCHK(s->timed(2, [&] {
     if (coop_ok(m))
-      return launch_fd_centre_coop(m->dm, m->L, m->C, m->X, nom, npts, s->P, s->qfrc_applied.as<double>(),
+      return launch_fd_centre_coop(m->dm, m->Lc, m->C, m->X, nom, npts, s->P, s->qfrc_applied.as<double>(),
                                    s->xfrc_applied.as<double>(), s->cview(), s->warm_c.as<double>(),
                                    s->cost_c.as<double>(), s->stream);
     return launch_fd_centre(m->dm, m->L, s->ws(), nom, npts, s->P, s->qfrc_applied.as<double>(),
@@ -741,7 +743,7 @@ int ilqg_fd_sweep(ilqg_solver* s) {
   }));
   HIPCHK(s->timed(3, [&] {
     if (coop_ok(m))
-      return launch_fd_cols_coop(m->dm, m->L, m->C, m->X, nom, npts, s->P, s->qfrc_applied.as<double>(),
+      return launch_fd_cols_coop(m->dm, m->Lc, m->C, m->X, nom, npts, s->P, s->qfrc_applied.as<double>(),
                                  s->xfrc_applied.as<double>(), s->cview(), s->warm_c.as<double>(),
                                  s->cost_c.as<double>(), s->deriv.as<double>(), s->stream);
     return launch_fd_cols(m->dm, m->L, s->ws(), nom, npts, s->P, s->qfrc_applied.as<double>(),

@@ -463,7 +463,7 @@ __device__ inline void collision(const auto& m, const auto& L, const auto& C, co
   double* gxmat = T.w + L.gxmat;
   double* con = T.w + L.con;
   int* coni = T.iw + L.coni;
-  double* pcon = T.c + C.pcon;
+  double* pcon = T.w + L.pcon;
   int* pcnt = T.ci + C.pcnt;
   FOR_T(p, X.npair) {
     int g1 = X.pair[2 * p], g2 = X.pair[2 * p + 1];
@@ -569,7 +569,7 @@ __device__ inline void make_constraint(const auto& m, const auto& L, const auto&
   int* efc_id = T.iw + L.efc_id;
   int* rsub = T.ci + C.rsub;
   int* jcnt = T.ci + C.jcnt;
-  double* jc = T.c + C.jc;
+  double* jc = T.w + L.jc;
   double* scom = T.w + L.scom;
   double* cdof = T.w + L.cdof;
   const int ncon = T.iw[L.ncon];
@@ -687,10 +687,9 @@ __device__ inline void make_constraint(const auto& m, const auto& L, const auto&
       K = -tc / (dmax * dmax);
       B = -dr / dmax;
     }
-    KBIP[4 * i] = K;
-    KBIP[4 * i + 1] = B;
-    KBIP[4 * i + 2] = imp;
-    KBIP[4 * i + 3] = 0;
+    KBIP[L.kstr * i] = K;
+    KBIP[L.kstr * i + 1] = B;
+    KBIP[L.kstr * i + 2] = imp;
     double R = maxd(MINVAL, (1 - imp) * dA / imp);
     efc_D[i] = 1 / R;
   }
@@ -801,7 +800,7 @@ __device__ inline void fwd_velocity(const auto& m, const auto& L, const auto& C,
   double* pos = T.w + L.efc_pos;
   double* mar = T.w + L.efc_margin;
   FOR_T(i, nefc) {
-    double k0 = KBIP[4 * i], k1 = KBIP[4 * i + 1], k2 = KBIP[4 * i + 2];
+    double k0 = KBIP[L.kstr * i], k1 = KBIP[L.kstr * i + 1], k2 = KBIP[L.kstr * i + 2];
     double v = tdot(J + i * nv, qvel, nv);
     efc_vel[i] = v;
     aref[i] = -k1 * v - k0 * k2 * (pos[i] - mar[i]);

@@ -50,17 +50,25 @@ struct WsLayout {
   int efc_J, efc_pos, efc_margin, efc_D, efc_KBIP, efc_aref, efc_vel, efc_force, efc_b;
   int cvel, cdof_dot, qfrc_passive, qfrc_bias, afrc, qfrc_act, qfrc_smooth, qacc_smooth, qfrc_con;
   int s_rne, s_con, s_newton, s_euler, s_rk4, s_fd;
+  int pcon, jc;  // cooperative layout only: per-pair contacts, contact-frame jacobians
+  int kstr;      // stride of efc_KBIP rows (4 lane layout, 3 cooperative)
   int nd;
   int coni, efc_type, efc_id, efc_state, ncon, nefc;
   int ni;
 };
 
+// npair < 0: the lane-per-evaluation layout (dphys.h).  npair >= 0: the
+// cooperative layout (dcoop.h), where scratch that is dead after
+// make_constraint (contacts, per-pair candidates, contact-frame jacobians)
+// shares storage with scratch first written afterwards (RNE, com velocities,
+// Newton, Euler, efc_b/efc_vel): less LDS per team, more teams per CU.
 template <class M>
-constexpr WsLayout make_layout(const M& m) {
+constexpr WsLayout make_layout(const M& m, int npair = -1) {
   WsLayout L{};
   int o = 0;
   const int nq = m.nq, nv = m.nv, nu = m.nu, nb = m.nbody, nj = m.njnt, ng = m.ngeom;
   const int nc = m.maxcon > 0 ? m.maxcon : 1, ne = m.maxefc > 0 ? m.maxefc : 1;
+  const bool coop = npair >= 0;
   auto take = [&](int n) { int r = o; o += n; return r; };
   L.qpos = take(nq); L.qvel = take(nv); L.ctrl = take(nu); L.qacc = take(nv); L.warm = take(nv);
   L.qfrc_applied = take(nv); L.xfrc_applied = take(6 * nb); L.time = take(1);
@@ -69,19 +77,39 @@ constexpr WsLayout make_layout(const M& m) {
   L.gxmat = take(9 * ng); L.scom = take(3 * nb); L.cdof = take(6 * nv); L.cinert = take(10 * nb);
   L.crb = take(10 * nb); L.qM = take(nv * nv); L.qLD = take(nv * nv); L.qLDinv = take(nv);
   L.amom = take(nu * nv);
-  L.con = take(CON_ND * nc);
+  L.kstr = coop ? 3 : 4;
+  if (!coop) L.con = take(CON_ND * nc);
   L.efc_J = take(ne * nv); L.efc_pos = take(ne); L.efc_margin = take(ne); L.efc_D = take(ne);
-  L.efc_KBIP = take(4 * ne); L.efc_aref = take(ne); L.efc_vel = take(ne); L.efc_force = take(ne);
-  L.efc_b = take(ne);
+  L.efc_KBIP = take(L.kstr * ne); L.efc_aref = take(ne);
+  if (!coop) L.efc_vel = take(ne);
+  L.efc_force = take(ne);
+  if (!coop) L.efc_b = take(ne);
   L.cvel = take(6 * nb); L.cdof_dot = take(6 * nv); L.qfrc_passive = take(nv); L.qfrc_bias = take(nv);
   L.afrc = take(nu); L.qfrc_act = take(nv); L.qfrc_smooth = take(nv); L.qacc_smooth = take(nv);
   L.qfrc_con = take(nv);
-  L.s_rne = take(12 * nb);
-  L.s_con = take(10 * nv);
-  L.s_newton = take(4 * nv + nv * nv + 2 * ne);
-  L.s_euler = take(2 * nv + 2 * nv * nv);
+  if (!coop) {
+    L.s_rne = take(12 * nb);
+    L.s_con = take(10 * nv);
+    L.s_newton = take(4 * nv + nv * nv + 2 * ne);
+    L.s_euler = take(2 * nv + 2 * nv * nv);
+  }
   L.s_rk4 = take(2 * nv + 4 * (nq + nv) + 4 * nv);
   L.s_fd = take(2 * nv);
+  if (coop) {
+    const int u = o;
+    int a = u;  // position-stage view
+    L.con = a; a += CON_ND * nc;
+    L.pcon = a; a += 14 * (npair > 0 ? npair : 1);
+    L.jc = a; a += 3 * nv * nc;
+    int b = u;  // velocity / constraint / integration view
+    L.s_rne = b; b += 12 * nb;
+    L.s_con = b; b += 10 * nv;
+    L.s_newton = b; b += 4 * nv + nv * nv + 2 * ne;
+    L.s_euler = b; b += 2 * nv + 2 * nv * nv;
+    L.efc_b = b; b += ne;
+    L.efc_vel = b; b += ne;
+    o = a > b ? a : b;
+  }
   L.nd = o;
   int oi = 0;
   L.coni = oi; oi += CON_NI * nc;
@@ -113,8 +141,8 @@ constexpr CoopLayout make_coop_layout(const M& m, int npair) {
   C.qloc = o; o += 4 * m.njnt;
   C.buf6 = o; o += 6 * m.nv;
   C.ftmp = o; o += m.nv;
-  C.pcon = o; o += 14 * (npair > 0 ? npair : 1);
-  C.jc = o; o += 3 * m.nv * nc;
+  C.pcon = 0;  // in the cooperative WsLayout (union scratch)
+  C.jc = 0;
   C.cterm = o; o += ne;
   C.rtmp = o; o += 6 * m.nbody;
   C.bc = o; o += 8;

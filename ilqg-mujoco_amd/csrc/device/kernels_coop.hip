@@ -146,7 +146,7 @@ __global__ __launch_bounds__(TEAM) void k_fd_centre_coop(DevModel mg, WsLayout L
 // model-specific instance (static_models.h): compile-time sizes, tables and LDS layout
 template <class SM, class SX>
 __global__ __launch_bounds__(TEAM) void k_fd_centre_s(DevModel mg, TrajDev tr, int P, const double* qfrc_applied, const double* xfrc_applied, CostDev cost, double* warm_c, double* cost_c) {
-  static constexpr WsLayout L = make_layout(SM{});
+  static constexpr WsLayout L = make_layout(SM{}, SX::npair);
   static constexpr CoopLayout C = make_coop_layout(SM{}, SX::npair);
   static constexpr SX X{};
   Team T = make_team(L, C);
@@ -251,7 +251,7 @@ __global__ __launch_bounds__(TEAM) void k_fd_cols_coop(DevModel mg, WsLayout L, 
 // model-specific instance (static_models.h): compile-time sizes, tables and LDS layout
 template <class SM, class SX>
 __global__ __launch_bounds__(TEAM) void k_fd_cols_s(DevModel mg, TrajDev tr, int P, const double* qfrc_applied, const double* xfrc_applied, CostDev cost, const double* warm_c, const double* cost_c, double* deriv) {
-  static constexpr WsLayout L = make_layout(SM{});
+  static constexpr WsLayout L = make_layout(SM{}, SX::npair);
   static constexpr CoopLayout C = make_coop_layout(SM{}, SX::npair);
   static constexpr SX X{};
   Team T = make_team(L, C);
@@ -368,7 +368,7 @@ __global__ __launch_bounds__(TEAM) void k_rollout_coop(DevModel mg, WsLayout L, 
 // model-specific instance (static_models.h): compile-time sizes, tables and LDS layout
 template <class SM, class SX>
 __global__ __launch_bounds__(TEAM) void k_rollout_s(DevModel mg, int S, int A, int P, TrajDev nom, TrajDev out, int out_is_cand, const double* K, const double* k, const double* alphas, TrajDev dinit, const double* qfrc_applied, const double* xfrc_applied, int passive, CostDev cost, double* cost_cand) {
-  static constexpr WsLayout L = make_layout(SM{});
+  static constexpr WsLayout L = make_layout(SM{}, SX::npair);
   static constexpr CoopLayout C = make_coop_layout(SM{}, SX::npair);
   static constexpr SX X{};
   Team T = make_team(L, C);
