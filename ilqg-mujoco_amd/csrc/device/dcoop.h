@@ -40,7 +40,7 @@ __device__ unsigned long long g_newton_calls;  // all workgroups: solver calls
 __shared__ unsigned long long s_stamp_acc[24], s_stamp_cnt[24], s_stamp_prev;
 #define STAMP(id)                                                            \
   do {                                                                       \
-    if (T.tid == 0 && blockIdx.x == 0) {                                     \
+    if (threadIdx.x == 0 && blockIdx.x == 0) {                               \
       unsigned long long t_ = __builtin_amdgcn_s_memtime();                  \
       if ((id) >= 0) {                                                       \
         s_stamp_acc[(id) < 0 ? 0 : (id)] += t_ - s_stamp_prev;               \
@@ -51,14 +51,14 @@ __shared__ unsigned long long s_stamp_acc[24], s_stamp_cnt[24], s_stamp_prev;
   } while (0)
 #define STAMP_INIT()                                                         \
   do {                                                                       \
-    if (T.tid == 0 && blockIdx.x == 0) {                                     \
+    if (threadIdx.x == 0 && blockIdx.x == 0) {                               \
       for (int i_ = 0; i_ < 24; i_++) s_stamp_acc[i_] = s_stamp_cnt[i_] = 0; \
       s_stamp_prev = __builtin_amdgcn_s_memtime();                           \
     }                                                                        \
   } while (0)
 #define STAMP_FLUSH()                                                        \
   do {                                                                       \
-    if (T.tid == 0 && blockIdx.x == 0)                                       \
+    if (threadIdx.x == 0 && blockIdx.x == 0)                                 \
       for (int i_ = 0; i_ < 24; i_++) {                                      \
         g_stamp_acc[i_] += s_stamp_acc[i_];                                  \
         g_stamp_cnt[i_] += s_stamp_cnt[i_];                                  \
@@ -696,19 +696,23 @@ __device__ inline void make_constraint(const auto& m, const auto& L, const auto&
   TSYNC();
 }
 
-__device__ inline void fwd_position(const auto& m, const auto& L, const auto& C, const auto& X,
-                                    const Team& T) {
-  kinematics(m, L, C, T);
-  STAMP(14 - 14 + 0);
-  com_pos(m, L, T);
-  STAMP(1);
-  // transmission: actuator_moment
+// transmission: actuator_moment (joint transmissions)
+__device__ inline void transmission(const auto& m, const auto& L, const Team& T) {
   double* amom = T.w + L.amom;
   FOR_T(e, m.nu * m.nv) {
     int i = e / m.nv, k = e % m.nv;
     int j = m.actuator_trnid[i];
     amom[e] = (k == m.jnt_dofadr[j]) ? m.actuator_gear[i] : 0.0;
   }
+}
+
+__device__ inline void fwd_position(const auto& m, const auto& L, const auto& C, const auto& X,
+                                    const Team& T) {
+  kinematics(m, L, C, T);
+  STAMP(14 - 14 + 0);
+  com_pos(m, L, T);
+  STAMP(1);
+  transmission(m, L, T);
   crb(m, L, C, X, T);
   STAMP(2);
   factor_ld(m, X, T, T.w + L.qM, T.w + L.qLD, T.w + L.qLDinv, T.c + C.ftmp);
@@ -720,13 +724,16 @@ __device__ inline void fwd_position(const auto& m, const auto& L, const auto& C,
 }
 
 // ------------------------------------------------------ velocity stage ---
-__device__ inline void fwd_velocity(const auto& m, const auto& L, const auto& C, const Team& T) {
+// part 0: the whole stage; 1: com velocities + RNE (primary wave of a
+// two-wave step); 2: passive forces + constraint reference (helper wave)
+__device__ inline void fwd_velocity(const auto& m, const auto& L, const auto& C, const Team& T, int part = 0) {
   const int nv = m.nv, nb = m.nbody;
   double* cvelw = T.w + L.cvel;
   double* cdof = T.w + L.cdof;
   double* cdd = T.w + L.cdof_dot;
   double* qvel = T.w + L.qvel;
   double* qpos = T.w + L.qpos;
+  if (part != 2) {
   // com velocities.  The recursion cvel_i = cvel_parent + sum_dof cdof*qvel is
   // component-wise, so it runs as 6 parallel chains (lane k = component k);
   // each dof's pre-update cvel is recorded (s_con) and the cdof_dot cross
@@ -778,6 +785,8 @@ __device__ inline void fwd_velocity(const auto& m, const auto& L, const auto& C,
       for (int q = 0; q < 6; q++) cdd[6 * d + q] = r[q];
     }
   }
+  }
+  if (part != 1) {
   // passive forces: one lane per dof (hinge/slide springs; ball/free rejected on the host)
   double* qp = T.w + L.qfrc_passive;
   FOR_T(i, nv) {
@@ -805,7 +814,9 @@ __device__ inline void fwd_velocity(const auto& m, const auto& L, const auto& C,
     efc_vel[i] = v;
     aref[i] = -k1 * v - k0 * k2 * (pos[i] - mar[i]);
   }
+  }
   TSYNC();
+  if (part == 2) return;
   // RNE: per (body, component) dof-velocity terms, then the chain per component
   double* rt = T.c + C.rtmp;
   double* cacc = T.w + L.s_rne;
@@ -1439,30 +1450,45 @@ __device__ inline int any_bad(const Team& T, const auto& C, const double* x, int
   return bad != 0ull;
 }
 
-__device__ inline void euler(const auto& m, const auto& L, const auto& C, const auto& X,
-                             const Team& T) {
+// Euler with implicit joint damping (MuJoCo mj_Euler): qacc_e = (M + h D)^-1 M qacc.
+// Split so a helper wave can factor M + h D (a function of qM only) while the
+// primary wave is still in the velocity stage; the factor is the same numbers.
+__device__ inline bool euler_damped(const auto& m, const Team& T) {
+  const int nv = m.nv;
+  unsigned long long dmask = 0;
+  for (int i0 = 0; i0 < nv; i0 += TEAM_SIZE) dmask |= __ballot(i0 + T.tid < nv && m.dof_damping[i0 + T.tid] > 0);
+  return dmask != 0ull;
+}
+__device__ inline void euler_prefactor(const auto& m, const auto& L, const auto& C, const auto& X, const Team& T) {
   const int nv = m.nv;
   double* s = T.w + L.s_euler;
-  double *qacc = s, *qH = s + nv, *qHLD = s + nv + nv * nv, *qHinv = s + nv + 2 * nv * nv;
+  double *qH = s + nv, *qHLD = s + nv + nv * nv, *qHinv = s + nv + 2 * nv * nv;
+  double* qM = T.w + L.qM;
+  if (!euler_damped(m, T)) return;
+  FOR_T(e, nv * nv) {
+    int i = e / nv, j = e % nv;
+    double v = qM[e];
+    if (i == j) v += m.opt_timestep * m.dof_damping[i];
+    qH[e] = v;
+  }
+  TSYNC();
+  factor_ld(m, X, T, qH, qHLD, qHinv, T.c + C.ftmp);
+}
+__device__ inline void euler_finish(const auto& m, const auto& L, const auto& C, const auto& X, const Team& T,
+                                    bool factored) {
+  const int nv = m.nv;
+  double* s = T.w + L.s_euler;
+  double *qacc = s, *qHLD = s + nv + nv * nv, *qHinv = s + nv + 2 * nv * nv;
   double* qM = T.w + L.qM;
   double* dq = T.w + L.qacc;
   double* qvel = T.w + L.qvel;
-  unsigned long long dmask = 0;
-  for (int i0 = 0; i0 < nv; i0 += TEAM_SIZE) dmask |= __ballot(i0 + T.tid < nv && m.dof_damping[i0 + T.tid] > 0);
-  const bool dmp = dmask != 0ull;
-  if (!dmp) {
+  if (!euler_damped(m, T)) {
     FOR_T(i, nv) qacc[i] = dq[i];
     TSYNC();
   } else {
     FOR_T(i, nv) qacc[i] = tdot(qM + i * nv, dq, nv);
-    FOR_T(e, nv * nv) {
-      int i = e / nv, j = e % nv;
-      double v = qM[e];
-      if (i == j) v += m.opt_timestep * m.dof_damping[i];
-      qH[e] = v;
-    }
     TSYNC();
-    factor_ld(m, X, T, qH, qHLD, qHinv, T.c + C.ftmp);
+    if (!factored) euler_prefactor(m, L, C, X, T);
     solve_ld(m, X, T, qHLD, qHinv, qacc);
   }
   const double h = m.opt_timestep;
@@ -1471,6 +1497,9 @@ __device__ inline void euler(const auto& m, const auto& L, const auto& C, const 
   integrate_pos(m, T, T.w + L.qpos, qvel, h);
   if (T.tid == 0) T.w[L.time] += h;
   TSYNC();
+}
+__device__ inline void euler(const auto& m, const auto& L, const auto& C, const auto& X, const Team& T) {
+  euler_finish(m, L, C, X, T, false);
 }
 
 __device__ inline void rk4(const auto& m, const auto& L, const auto& C, const auto& X, const Team& T,
@@ -1554,6 +1583,55 @@ __device__ inline void step(const auto& m, const auto& L, const auto& C, const a
   else
     euler(m, L, C, X, T);
   STAMP(9);
+}
+
+// mj_step by a two-wave team (rollout kernels): wave 0 runs the dependency
+// chain, wave 1 takes the branches off it -- collision beside com_pos,
+// make_constraint beside crb + factor_ld(M), passive forces + constraint
+// reference + the Euler factor of M + h D beside com velocities + RNE.  Every
+// quantity is still computed by the same code, so results are unchanged;
+// both waves pass the same __syncthreads sequence.
+__device__ inline void step_dual(const auto& m, const auto& L, const auto& C, const auto& X, const Team& T,
+                                 int wave) {
+  const bool A = wave == 0;
+  const bool eul = m.opt_integrator != 1;
+  if (A) {
+    if (any_bad(T, C, T.w + L.qpos, m.nq)) reset_data(m, L, T);
+    if (any_bad(T, C, T.w + L.qvel, m.nv)) reset_data(m, L, T);
+    kinematics(m, L, C, T);
+  }
+  __syncthreads();
+  if (A) com_pos(m, L, T);
+  else collision(m, L, C, X, T);
+  __syncthreads();
+  if (A) {
+    transmission(m, L, T);
+    crb(m, L, C, X, T);
+    factor_ld(m, X, T, T.w + L.qM, T.w + L.qLD, T.w + L.qLDinv, T.c + C.ftmp);
+  } else {
+    make_constraint(m, L, C, X, T);
+  }
+  __syncthreads();
+  if (A) {
+    fwd_velocity(m, L, C, T, 1);
+  } else {
+    fwd_velocity(m, L, C, T, 2);
+    if (eul) euler_prefactor(m, L, C, X, T);
+  }
+  __syncthreads();
+  if (A) {
+    fwd_acceleration(m, L, X, T);
+    fwd_constraint(m, L, C, X, T, m.opt_iterations, m.opt_tolerance);
+    bool reset = false;
+    if (any_bad(T, C, T.w + L.qacc, m.nv)) {
+      reset = true;
+      reset_data(m, L, T);
+      forward_skip(m, L, C, X, T, STAGE_NONE, m.opt_iterations, m.opt_tolerance);
+    }
+    if (!eul) rk4(m, L, C, X, T, m.opt_iterations, m.opt_tolerance);
+    else euler_finish(m, L, C, X, T, !reset);
+  }
+  __syncthreads();
 }
 
 }  // namespace coop

@@ -25,7 +25,7 @@ __device__ inline Team make_team(const auto& L, const auto& C) {
   T.c = lds + L.nd;
   T.iw = reinterpret_cast<int*>(lds + L.nd + C.nd + C.imgd);
   T.ci = T.iw + L.ni;
-  T.tid = threadIdx.x;
+  T.tid = threadIdx.x & (TEAM - 1);  // lane within this wave (two-wave teams: one Team per wave)
   T.nt = TEAM;  // every cooperative kernel is launched with one 64-lane wavefront
   return T;
 }
@@ -261,7 +261,9 @@ __global__ __launch_bounds__(TEAM) void k_fd_cols_s(DevModel mg, TrajDev tr, int
 }
 
 __device__ inline void rollout_body(const auto& m, const auto& L, const auto& C, const auto& X, const Team& T,
-                                int S, int A, int P, TrajDev nom, TrajDev out, int out_is_cand, const double* K, const double* k, const double* alphas, TrajDev dinit, const double* qfrc_applied, const double* xfrc_applied, int passive, CostDev cost, double* cost_cand) {
+                                int S, int A, int P, TrajDev nom, TrajDev out, int out_is_cand, const double* K, const double* k, const double* alphas, TrajDev dinit, const double* qfrc_applied, const double* xfrc_applied, int passive, CostDev cost, double* cost_cand, int wave) {
+  // wave < 0: one-wave team; 0/1: primary/helper wave of a two-wave team (step_dual)
+  const bool prim = wave <= 0;
   STAMP_INIT();
 #ifdef ILQG_STAMPS
   unsigned long long rt0 = __builtin_amdgcn_s_memrealtime(), mt0 = __builtin_amdgcn_s_memtime();
@@ -304,41 +306,45 @@ __device__ inline void rollout_body(const auto& m, const auto& L, const auto& C,
   const double alpha = alphas ? alphas[a] : 1.0;
   const int ob = out_is_cand ? lane : s;
   double c = 0;
+  if (wave >= 0) __syncthreads();
   for (int n = P - 1; n >= 0; n--) {
     const bool pre = !passive && n > 0;
-    if (pre) {
-      // issue the next point's loads now; their latency hides behind this step
-      const size_t pn1 = (size_t)s * P + (n - 1);
+    if (prim) {
+      if (pre) {
+        // issue the next point's loads now; their latency hides behind this step
+        const size_t pn1 = (size_t)s * P + (n - 1);
 #pragma unroll
-      for (int q = 0; q < PFR; q++) {
-        const int t = T.tid + q * TEAM;
-        pf[q] = t < R ? fetch(pn1, t) : 0.0;
+        for (int q = 0; q < PFR; q++) {
+          const int t = T.tid + q * TEAM;
+          pf[q] = t < R ? fetch(pn1, t) : 0.0;
+        }
       }
-    }
-    if (!passive) {
-      FOR_T(j, nx) dx[j] = j < nv ? state_diff_dof(m, j, qpos, rq) : qvel[j - nv] - rv[j - nv];
-      TSYNC();
-      FOR_T(i, nu) {
-        double t = 0;
-        for (int j = 0; j < nx; j++) t += rK[i + j * nu] * dx[j];
-        ctrl[i] = (t + alpha * rk[i]) + ru[i];
+      if (!passive) {
+        FOR_T(j, nx) dx[j] = j < nv ? state_diff_dof(m, j, qpos, rq) : qvel[j - nv] - rv[j - nv];
+        TSYNC();
+        FOR_T(i, nu) {
+          double t = 0;
+          for (int j = 0; j < nx; j++) t += rK[i + j * nu] * dx[j];
+          ctrl[i] = (t + alpha * rk[i]) + ru[i];
+        }
+        TSYNC();
+      }
+      const size_t po = (size_t)ob * P + n;
+      FOR_T(i, nq) out.qpos[po * nq + i] = qpos[i];
+      FOR_T(i, nv) {
+        out.qvel[po * nv + i] = qvel[i];
+        out.warm[po * nv + i] = warm[i];
+      }
+      FOR_T(i, nu) out.ctrl[po * nu + i] = ctrl[i];
+      if (T.tid == 0) {
+        out.time[po] = T.w[L.time];
+        c += step_cost(m, cl, qpos, qvel, ctrl);
       }
       TSYNC();
     }
-    const size_t po = (size_t)ob * P + n;
-    FOR_T(i, nq) out.qpos[po * nq + i] = qpos[i];
-    FOR_T(i, nv) {
-      out.qvel[po * nv + i] = qvel[i];
-      out.warm[po * nv + i] = warm[i];
-    }
-    FOR_T(i, nu) out.ctrl[po * nu + i] = ctrl[i];
-    if (T.tid == 0) {
-      out.time[po] = T.w[L.time];
-      c += step_cost(m, cl, qpos, qvel, ctrl);
-    }
-    TSYNC();
-    step(m, L, C, X, T);
-    if (pre) {
+    if (wave < 0) step(m, L, C, X, T);
+    else step_dual(m, L, C, X, T, wave);
+    if (prim && pre) {
 #pragma unroll
       for (int q = 0; q < PFR; q++) {
         const int t = T.tid + q * TEAM;
@@ -347,9 +353,9 @@ __device__ inline void rollout_body(const auto& m, const auto& L, const auto& C,
       TSYNC();
     }
   }
-  if (T.tid == 0 && cost_cand) cost_cand[lane] = c;
+  if (prim && T.tid == 0 && cost_cand) cost_cand[lane] = c;
 #ifdef ILQG_STAMPS
-  if (T.tid == 0 && blockIdx.x == 0) {
+  if (prim && T.tid == 0 && blockIdx.x == 0) {
     g_stamp_acc[30] += __builtin_amdgcn_s_memrealtime() - rt0;
     g_stamp_acc[31] += __builtin_amdgcn_s_memtime() - mt0;
   }
@@ -362,7 +368,7 @@ __global__ __launch_bounds__(TEAM) void k_rollout_coop(DevModel mg, WsLayout L, 
   DevModel m;
   CoopAux X;
   stage_model(mg, Xg, L, C, T, m, X);
-  rollout_body(m, L, C, X, T, S, A, P, nom, out, out_is_cand, K, k, alphas, dinit, qfrc_applied, xfrc_applied, passive, cost, cost_cand);
+  rollout_body(m, L, C, X, T, S, A, P, nom, out, out_is_cand, K, k, alphas, dinit, qfrc_applied, xfrc_applied, passive, cost, cost_cand, -1);
 }
 
 // model-specific instance (static_models.h): compile-time sizes, tables and LDS layout
@@ -374,7 +380,28 @@ __global__ __launch_bounds__(TEAM) void k_rollout_s(DevModel mg, int S, int A, i
   Team T = make_team(L, C);
   SM m;
   stage_model_s(mg, L, C, T, m);
-  rollout_body(m, L, C, X, T, S, A, P, nom, out, out_is_cand, K, k, alphas, dinit, qfrc_applied, xfrc_applied, passive, cost, cost_cand);
+  rollout_body(m, L, C, X, T, S, A, P, nom, out, out_is_cand, K, k, alphas, dinit, qfrc_applied, xfrc_applied, passive, cost, cost_cand, -1);
+}
+
+// two-wave teams (step_dual): 128 threads per (seed, candidate)
+__global__ __launch_bounds__(2 * TEAM) void k_rollout2_coop(DevModel mg, WsLayout L, CoopLayout C, CoopAux Xg, int S, int A, int P, TrajDev nom, TrajDev out, int out_is_cand, const double* K, const double* k, const double* alphas, TrajDev dinit, const double* qfrc_applied, const double* xfrc_applied, int passive, CostDev cost, double* cost_cand) {
+  Team T = make_team(L, C);
+  DevModel m;
+  CoopAux X;
+  stage_model(mg, Xg, L, C, T, m, X);
+  rollout_body(m, L, C, X, T, S, A, P, nom, out, out_is_cand, K, k, alphas, dinit, qfrc_applied, xfrc_applied,
+               passive, cost, cost_cand, (int)(threadIdx.x / TEAM));
+}
+template <class SM, class SX>
+__global__ __launch_bounds__(2 * TEAM) void k_rollout2_s(DevModel mg, int S, int A, int P, TrajDev nom, TrajDev out, int out_is_cand, const double* K, const double* k, const double* alphas, TrajDev dinit, const double* qfrc_applied, const double* xfrc_applied, int passive, CostDev cost, double* cost_cand) {
+  static constexpr WsLayout L = make_layout(SM{}, SX::npair);
+  static constexpr CoopLayout C = make_coop_layout(SM{}, SX::npair);
+  static constexpr SX X{};
+  Team T = make_team(L, C);
+  SM m;
+  stage_model_s(mg, L, C, T, m);
+  rollout_body(m, L, C, X, T, S, A, P, nom, out, out_is_cand, K, k, alphas, dinit, qfrc_applied, xfrc_applied,
+               passive, cost, cost_cand, (int)(threadIdx.x / TEAM));
 }
 
 template <typename K>
@@ -385,6 +412,16 @@ hipError_t allow_lds(K kern, size_t lds) {
 }
 
 }  // namespace
+
+// rollouts on two-wave teams (step_dual); ILQG_DUAL=0 selects one-wave teams (A/B)
+static bool use_dual() {
+  static int v = -1;
+  if (v < 0) {
+    const char* e = getenv("ILQG_DUAL");
+    v = (e && e[0] == '0') ? 0 : 1;
+  }
+  return v == 1;
+}
 
 size_t coop_lds_bytes(const WsLayout& L, const CoopLayout& C) {
   return (size_t)(L.nd + C.nd + C.imgd) * sizeof(double) + (size_t)(L.ni + C.ni) * sizeof(int);
@@ -452,6 +489,27 @@ hipError_t launch_rollout_coop(const DevModel& m, const WsLayout& L, const CoopL
                                hipStream_t st) {
   const size_t lds = coop_lds_bytes(L, C);
   hipError_t e;
+  if (use_dual()) {
+#define ILQG_CASE(id, SMT, SXT)                                                                                 \
+  case id:                                                                                                      \
+    e = allow_lds(k_rollout2_s<stat::SMT, stat::SXT>, lds);                                                     \
+    if (e != hipSuccess) return e;                                                                              \
+    hipLaunchKernelGGL((k_rollout2_s<stat::SMT, stat::SXT>), dim3(S * A), dim3(2 * TEAM), lds, st, m, S, A, P,   \
+                       nominal, out, out_is_cand, K, k, alphas, dinit, qfrc_applied, xfrc_applied, passive, cost, \
+                       cost_cand);                                                                              \
+    return hipGetLastError();
+    switch (m.static_id) {
+      ILQG_STATIC_MODELS(ILQG_CASE)
+      default:
+        break;
+    }
+#undef ILQG_CASE
+    e = allow_lds(k_rollout2_coop, lds);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(k_rollout2_coop, dim3(S * A), dim3(2 * TEAM), lds, st, m, L, C, X, S, A, P, nominal, out,
+                       out_is_cand, K, k, alphas, dinit, qfrc_applied, xfrc_applied, passive, cost, cost_cand);
+    return hipGetLastError();
+  }
 #define ILQG_CASE(id, SMT, SXT)                                                                                 \
   case id:                                                                                                      \
     e = allow_lds(k_rollout_s<stat::SMT, stat::SXT>, lds);                                                      \
