@@ -625,9 +625,14 @@ int ilqg_solver_init(ilqg_solver* s, const double* time, const double* qpos, con
     HIPCHK(hipMemcpy(s->xfrc_applied.p, xfrc_applied, (size_t)s->S * 6 * h.nbody * 8, hipMemcpyHostToDevice));
   // ILQR ctor: passive rollout with constant ctrl into dArray[N..0]
   TrajDev nom = s->tview(s->traj), di = s->tview(s->dinit);
-  HIPCHK(launch_rollout(m->dm, m->L, s->ws(), s->S, 1, s->P, nom, nom, 0, s->K.as<double>(), s->k.as<double>(),
-                        nullptr, di, s->qfrc_applied.as<double>(), s->xfrc_applied.as<double>(), 1, s->cview(),
-                        nullptr, s->stream));
+  if (coop_ok(m))
+    HIPCHK(launch_rollout_coop(m->dm, m->Lc, m->C, m->X, s->S, 1, s->P, nom, nom, 0, s->K.as<double>(),
+                               s->k.as<double>(), nullptr, di, s->qfrc_applied.as<double>(),
+                               s->xfrc_applied.as<double>(), 1, s->cview(), nullptr, s->stream));
+  else
+    HIPCHK(launch_rollout(m->dm, m->L, s->ws(), s->S, 1, s->P, nom, nom, 0, s->K.as<double>(), s->k.as<double>(),
+                          nullptr, di, s->qfrc_applied.as<double>(), s->xfrc_applied.as<double>(), 1, s->cview(),
+                          nullptr, s->stream));
   HIPCHK(hipStreamSynchronize(s->stream));
   // setDInit(dmain) as the MPC driver does before iterating (src/inverted_pendulum/inverted_pendulum.cpp:21)
   s->initialized = true;

@@ -8,8 +8,10 @@ the corrected figure is an upper-side estimate, not an exact byte count.
 Usage: python tools/pmc_summary.py gpurun_out/prof profiles/pmc_traffic.json"""
 import collections, csv, json, re, sys
 
-GROUPS = {"rollout": ("k_rollout_coop",), "fd_sweep": ("k_fd_centre_coop", "k_fd_cols_coop"),
-          "backward": ("k_backward",), "select": ("k_select",)}
+# kernel-name alternatives per group (model-specific *_s, two-wave *2*, generic *_coop)
+GROUPS = {"rollout": (("k_rollout2_s", "k_rollout_s", "k_rollout2_coop", "k_rollout_coop"),),
+          "fd_sweep": (("k_fd_centre_s", "k_fd_centre_coop"), ("k_fd_cols_s", "k_fd_cols_coop")),
+          "backward": (("k_backward",),), "select": (("k_select",),)}
 
 
 def per_kernel(path, counter):
@@ -17,7 +19,7 @@ def per_kernel(path, counter):
     for r in csv.DictReader(open(path)):
         if r["Counter_Name"] != counter:
             continue
-        mm = re.search(r"::(k_[a-z_]+)\(", r["Kernel_Name"])
+        mm = re.search(r"::(k_[a-z0-9_]+)[<(]", r["Kernel_Name"])
         if mm:
             agg[mm.group(1)].append(float(r["Counter_Value"]) * 1024.0)
     return agg
@@ -36,9 +38,10 @@ def main(src, dst):
         kern[k] = {"launches_seen": len(f), "fetch_bytes_raw": fa, "fetch_bytes_x2": 2 * fa, "write_bytes": wa,
                    "traffic_bytes": 2 * fa + wa}
     out = {"per_kernel": kern, "note": "FETCH_SIZE doubled per the gfx950 calibration; KiB->bytes x1024"}
-    for g, ks in GROUPS.items():
-        if all(k in kern for k in ks):
-            out[g] = sum(kern[k]["traffic_bytes"] for k in ks)
+    for g, alts in GROUPS.items():
+        picks = [next((k for k in a if k in kern), None) for a in alts]
+        if all(picks):
+            out[g] = sum(kern[k]["traffic_bytes"] for k in picks)
     json.dump(out, open(dst, "w"), indent=1)
     print(json.dumps(out, indent=1))
 
