@@ -33,33 +33,37 @@ struct Team {
 // workgroup 0, lane 0, accumulated in LDS (a global read-modify-write per
 // stamp would itself wait on memory) and flushed once at kernel end
 #ifdef ILQG_STAMPS
-__device__ unsigned long long g_stamp_acc[32];
-__device__ unsigned long long g_stamp_cnt[32];
+#define STAMP_N 44
+__device__ unsigned long long g_stamp_acc[48];
+__device__ unsigned long long g_stamp_cnt[48];
 __device__ unsigned long long g_newton_iters;  // all workgroups: Newton iterations
 __device__ unsigned long long g_newton_calls;  // all workgroups: solver calls
-__shared__ unsigned long long s_stamp_acc[24], s_stamp_cnt[24], s_stamp_prev;
-#define STAMP(id)                                                            \
+__shared__ unsigned long long s_stamp_acc[STAMP_N], s_stamp_cnt[STAMP_N], s_stamp_prev, s_stamp_prevb;
+#define STAMP_AT(lane, prev, id)                                             \
   do {                                                                       \
-    if (threadIdx.x == 0 && blockIdx.x == 0) {                               \
+    if (threadIdx.x == (lane) && blockIdx.x == 0) {                          \
       unsigned long long t_ = __builtin_amdgcn_s_memtime();                  \
       if ((id) >= 0) {                                                       \
-        s_stamp_acc[(id) < 0 ? 0 : (id)] += t_ - s_stamp_prev;               \
+        s_stamp_acc[(id) < 0 ? 0 : (id)] += t_ - prev;                       \
         s_stamp_cnt[(id) < 0 ? 0 : (id)]++;                                  \
       }                                                                      \
-      s_stamp_prev = t_;                                                     \
+      prev = t_;                                                             \
     }                                                                        \
   } while (0)
+// wave 0 lane 0; STAMPB: lane 0 of the helper wave of a two-wave team
+#define STAMP(id) STAMP_AT(0, s_stamp_prev, id)
+#define STAMPB(id) STAMP_AT(64, s_stamp_prevb, id)
 #define STAMP_INIT()                                                         \
   do {                                                                       \
     if (threadIdx.x == 0 && blockIdx.x == 0) {                               \
-      for (int i_ = 0; i_ < 24; i_++) s_stamp_acc[i_] = s_stamp_cnt[i_] = 0; \
-      s_stamp_prev = __builtin_amdgcn_s_memtime();                           \
+      for (int i_ = 0; i_ < STAMP_N; i_++) s_stamp_acc[i_] = s_stamp_cnt[i_] = 0; \
+      s_stamp_prev = s_stamp_prevb = __builtin_amdgcn_s_memtime();           \
     }                                                                        \
   } while (0)
 #define STAMP_FLUSH()                                                        \
   do {                                                                       \
     if (threadIdx.x == 0 && blockIdx.x == 0)                                 \
-      for (int i_ = 0; i_ < 24; i_++) {                                      \
+      for (int i_ = 0; i_ < STAMP_N; i_++) {                                 \
         g_stamp_acc[i_] += s_stamp_acc[i_];                                  \
         g_stamp_cnt[i_] += s_stamp_cnt[i_];                                  \
       }                                                                      \
@@ -68,6 +72,7 @@ __shared__ unsigned long long s_stamp_acc[24], s_stamp_cnt[24], s_stamp_prev;
 #define STAMP(id) \
   do {            \
   } while (0)
+#define STAMPB(id) STAMP(id)
 #define STAMP_INIT() STAMP(-1)
 #define STAMP_FLUSH() STAMP(-1)
 #endif
@@ -1592,36 +1597,71 @@ __device__ inline void step(const auto& m, const auto& L, const auto& C, const a
 // quantity is still computed by the same code, so results are unchanged;
 // both waves pass the same __syncthreads sequence.
 __device__ inline void step_dual(const auto& m, const auto& L, const auto& C, const auto& X, const Team& T,
-                                 int wave) {
+                                 int wave, auto&& pre) {
   const bool A = wave == 0;
   const bool eul = m.opt_integrator != 1;
+  STAMP(-1);
+  STAMPB(-1);
+  // `pre` (the caller's per-step work that reads the state before the step:
+  // control law, trajectory record) runs on the helper wave beside the
+  // kinematics.  mj_checkPos/Vel resets the state, so on a bad state it runs
+  // first, as in the one-wave order; both waves test the same LDS state.
+  const bool bad = any_bad(T, C, T.w + L.qpos, m.nq) || any_bad(T, C, T.w + L.qvel, m.nv);
+  if (bad) {
+    if (!A) pre();
+    __syncthreads();
+    if (A) reset_data(m, L, T);
+  }
   if (A) {
-    if (any_bad(T, C, T.w + L.qpos, m.nq)) reset_data(m, L, T);
-    if (any_bad(T, C, T.w + L.qvel, m.nv)) reset_data(m, L, T);
     kinematics(m, L, C, T);
+    STAMP(0);
+  } else if (!bad) {
+    pre();
+    STAMPB(41);
   }
   __syncthreads();
-  if (A) com_pos(m, L, T);
-  else collision(m, L, C, X, T);
+  STAMP(24);
+  STAMPB(32);
+  if (A) {
+    com_pos(m, L, T);
+    STAMP(1);
+  } else {
+    collision(m, L, C, X, T);
+    STAMPB(33);
+  }
   __syncthreads();
+  STAMP(25);
+  STAMPB(34);
   if (A) {
     transmission(m, L, T);
     crb(m, L, C, X, T);
+    STAMP(2);
     factor_ld(m, X, T, T.w + L.qM, T.w + L.qLD, T.w + L.qLDinv, T.c + C.ftmp);
+    STAMP(3);
   } else {
     make_constraint(m, L, C, X, T);
+    STAMPB(35);
   }
   __syncthreads();
+  STAMP(26);
+  STAMPB(36);
   if (A) {
     fwd_velocity(m, L, C, T, 1);
+    STAMP(6);
   } else {
     fwd_velocity(m, L, C, T, 2);
+    STAMPB(37);
     if (eul) euler_prefactor(m, L, C, X, T);
+    STAMPB(38);
   }
   __syncthreads();
+  STAMP(27);
+  STAMPB(39);
   if (A) {
     fwd_acceleration(m, L, X, T);
+    STAMP(7);
     fwd_constraint(m, L, C, X, T, m.opt_iterations, m.opt_tolerance);
+    STAMP(8);
     bool reset = false;
     if (any_bad(T, C, T.w + L.qacc, m.nv)) {
       reset = true;
@@ -1630,8 +1670,11 @@ __device__ inline void step_dual(const auto& m, const auto& L, const auto& C, co
     }
     if (!eul) rk4(m, L, C, X, T, m.opt_iterations, m.opt_tolerance);
     else euler_finish(m, L, C, X, T, !reset);
+    STAMP(9);
   }
   __syncthreads();
+  STAMP(28);
+  STAMPB(40);
 }
 
 }  // namespace coop

@@ -305,59 +305,74 @@ __device__ inline void rollout_body(const auto& m, const auto& L, const auto& C,
   }
   const double alpha = alphas ? alphas[a] : 1.0;
   const int ob = out_is_cand ? lane : s;
+  // the wave that runs the control law and writes the record: the helper wave
+  // of a two-wave team (beside the primary's kinematics), else the only wave
+  const bool ctl = wave != 0;
   double c = 0;
-  if (wave >= 0) __syncthreads();
-  for (int n = P - 1; n >= 0; n--) {
+  // control law u = u* + alpha k + K (x - x*) for point n, its record and cost
+  // (ilqr.h:116-133); the next point's nominal record is prefetched first
+  auto pre_step = [&](int n) {
     const bool pre = !passive && n > 0;
-    if (prim) {
-      if (pre) {
-        // issue the next point's loads now; their latency hides behind this step
-        const size_t pn1 = (size_t)s * P + (n - 1);
+    if (pre) {
+      const size_t pn1 = (size_t)s * P + (n - 1);
 #pragma unroll
-        for (int q = 0; q < PFR; q++) {
-          const int t = T.tid + q * TEAM;
-          pf[q] = t < R ? fetch(pn1, t) : 0.0;
-        }
+      for (int q = 0; q < PFR; q++) {
+        const int t = T.tid + q * TEAM_SIZE;
+        pf[q] = t < R ? fetch(pn1, t) : 0.0;
       }
-      if (!passive) {
-        FOR_T(j, nx) dx[j] = j < nv ? state_diff_dof(m, j, qpos, rq) : qvel[j - nv] - rv[j - nv];
-        TSYNC();
-        FOR_T(i, nu) {
-          double t = 0;
-          for (int j = 0; j < nx; j++) t += rK[i + j * nu] * dx[j];
-          ctrl[i] = (t + alpha * rk[i]) + ru[i];
-        }
-        TSYNC();
-      }
-      const size_t po = (size_t)ob * P + n;
-      FOR_T(i, nq) out.qpos[po * nq + i] = qpos[i];
-      FOR_T(i, nv) {
-        out.qvel[po * nv + i] = qvel[i];
-        out.warm[po * nv + i] = warm[i];
-      }
-      FOR_T(i, nu) out.ctrl[po * nu + i] = ctrl[i];
-      if (T.tid == 0) {
-        out.time[po] = T.w[L.time];
-        c += step_cost(m, cl, qpos, qvel, ctrl);
+    }
+    if (!passive) {
+      FOR_T(j, nx) dx[j] = j < nv ? state_diff_dof(m, j, qpos, rq) : qvel[j - nv] - rv[j - nv];
+      TSYNC();
+      FOR_T(i, nu) {
+        double t = 0;
+        for (int j = 0; j < nx; j++) t += rK[i + j * nu] * dx[j];
+        ctrl[i] = (t + alpha * rk[i]) + ru[i];
       }
       TSYNC();
     }
-    if (wave < 0) step(m, L, C, X, T);
-    else step_dual(m, L, C, X, T, wave);
-    if (prim && pre) {
+    const size_t po = (size_t)ob * P + n;
+    FOR_T(i, nq) out.qpos[po * nq + i] = qpos[i];
+    FOR_T(i, nv) {
+      out.qvel[po * nv + i] = qvel[i];
+      out.warm[po * nv + i] = warm[i];
+    }
+    FOR_T(i, nu) out.ctrl[po * nu + i] = ctrl[i];
+    if (T.tid == 0) {
+      out.time[po] = T.w[L.time];
+      c += step_cost(m, cl, qpos, qvel, ctrl);
+    }
+    TSYNC();
+  };
+  // the prefetched record replaces the current one once the step no longer reads it
+  auto park = [&](int n) {
+    if (!passive && n > 0) {
 #pragma unroll
       for (int q = 0; q < PFR; q++) {
-        const int t = T.tid + q * TEAM;
+        const int t = T.tid + q * TEAM_SIZE;
         if (t < R) rec[t] = pf[q];
       }
       TSYNC();
     }
+  };
+  if (wave >= 0) __syncthreads();
+  for (int n = P - 1; n >= 0; n--) {
+    if (wave < 0) {
+      pre_step(n);
+      step(m, L, C, X, T);
+      park(n);
+    } else {
+      step_dual(m, L, C, X, T, wave, [&]() {
+        pre_step(n);
+        park(n);
+      });
+    }
   }
-  if (prim && T.tid == 0 && cost_cand) cost_cand[lane] = c;
+  if (ctl && T.tid == 0 && cost_cand) cost_cand[lane] = c;
 #ifdef ILQG_STAMPS
   if (prim && T.tid == 0 && blockIdx.x == 0) {
-    g_stamp_acc[30] += __builtin_amdgcn_s_memrealtime() - rt0;
-    g_stamp_acc[31] += __builtin_amdgcn_s_memtime() - mt0;
+    g_stamp_acc[46] += __builtin_amdgcn_s_memrealtime() - rt0;
+    g_stamp_acc[47] += __builtin_amdgcn_s_memtime() - mt0;
   }
 #endif
   STAMP_FLUSH();
@@ -535,17 +550,17 @@ hipError_t launch_rollout_coop(const DevModel& m, const WsLayout& L, const CoopL
 
 #ifdef ILQG_STAMPS
 extern "C" int ilqg_debug_stamps(unsigned long long* acc, unsigned long long* cnt, int reset) {
-  if (hipMemcpyFromSymbol(acc, HIP_SYMBOL(ilqg::coop::g_stamp_acc), sizeof(unsigned long long) * 32) != hipSuccess)
+  if (hipMemcpyFromSymbol(acc, HIP_SYMBOL(ilqg::coop::g_stamp_acc), sizeof(unsigned long long) * 48) != hipSuccess)
     return 3;
-  if (hipMemcpyFromSymbol(cnt, HIP_SYMBOL(ilqg::coop::g_stamp_cnt), sizeof(unsigned long long) * 32) != hipSuccess)
+  if (hipMemcpyFromSymbol(cnt, HIP_SYMBOL(ilqg::coop::g_stamp_cnt), sizeof(unsigned long long) * 48) != hipSuccess)
     return 3;
   unsigned long long nw[2];
   (void)hipMemcpyFromSymbol(&nw[0], HIP_SYMBOL(ilqg::coop::g_newton_iters), 8);
   (void)hipMemcpyFromSymbol(&nw[1], HIP_SYMBOL(ilqg::coop::g_newton_calls), 8);
-  acc[28] = nw[0];
-  acc[29] = nw[1];
+  acc[44] = nw[0];
+  acc[45] = nw[1];
   if (reset) {
-    unsigned long long z[32] = {0};
+    unsigned long long z[48] = {0};
     (void)hipMemcpyToSymbol(HIP_SYMBOL(ilqg::coop::g_newton_iters), z, 8);
     (void)hipMemcpyToSymbol(HIP_SYMBOL(ilqg::coop::g_newton_calls), z, 8);
     (void)hipMemcpyToSymbol(HIP_SYMBOL(ilqg::coop::g_stamp_acc), z, sizeof(z));

@@ -9,9 +9,13 @@ NAMES = {0: "kinematics", 1: "com_pos", 2: "trn+crb", 3: "factor_ld(M)", 4: "col
          6: "fwd_velocity", 7: "fwd_acceleration", 8: "fwd_constraint(newton)", 9: "integrator",
          11: " kin: joint quats", 12: " kin: lane-0 chain", 13: " kin: body frames", 14: " nt: chol solve",
          15: " nt: Mv,Jv", 16: " nt: linesearch", 17: " nt: update", 18: " nt: cost+grad", 19: " nt: hessian",
-         20: "empty sync", 21: "empty sync 2"}
+         20: "empty sync", 21: "empty sync 2",
+         24: "A: barrier 1 (wait for B)", 25: "A: barrier 2", 26: "A: barrier 3", 27: "A: barrier 4", 28: "A: barrier 5",
+         32: "B: barrier 1 (wait for A kinematics)", 33: "B: collision", 34: "B: barrier 2", 35: "B: make_constraint",
+         36: "B: barrier 3", 37: "B: passive+aref", 38: "B: euler prefactor", 39: "B: barrier 4 (A accel..euler)",
+         40: "B: barrier 5", 41: "B: control law + record"}
 L = ia.lib()
-acc = (ctypes.c_ulonglong * 32)(); cnt = (ctypes.c_ulonglong * 32)()
+acc = (ctypes.c_ulonglong * 48)(); cnt = (ctypes.c_ulonglong * 48)()
 m = ia.Model.load(workloads.model_file(sys.argv[1] if len(sys.argv) > 1 else "hopper"))
 dmain = workloads.hopper_dmain(m, 1) if m.nv == 6 else workloads.pendulum_dmain(m, 1)
 g = ia.ILQR(m, dmain, 500 if m.nv == 6 else 200, ia.HOPPER_COST if m.nv == 6 else ia.PENDULUM_COST)
@@ -23,17 +27,17 @@ for what, fn in (("rollout (1 seed)", g.forward_pass), ("fd sweep", g.fd_sweep))
     fn(); g.synchronize()
     tm = g.timing()
     L.ilqg_debug_stamps(acc, cnt, 1)
-    tot = sum(acc[i] for i in range(10))
+    tot = sum(acc[i] for i in list(range(10)) + list(range(24, 29)))
     ms = sum(v[0] for v in tm.values())
-    print(f"== {what}: block 0, lane 0, total {tot} ticks (stages 0-9); kernel time {ms:.3f} ms "
+    print(f"== {what}: block 0, lane 0, total {tot} ticks (wave-0 stages + barriers); kernel time {ms:.3f} ms "
           f"-> {tot / (ms * 1e3):.0f} ticks/us if the stages were all of it")
-    if acc[29]:
-        print(f"   Newton (all workgroups): {acc[29]} solves, {acc[28]} iterations, "
-              f"{acc[28] / acc[29]:.2f} iterations per solve")
-    if acc[30]:
-        print(f"   block 0 lifetime: {acc[30] / 100:.0f} us realtime, {acc[31]} memtime ticks "
-              f"-> shader clock {acc[31] / (acc[30] / 100) :.0f} MHz")
-    for i in range(22):
+    if acc[45]:
+        print(f"   Newton (all workgroups): {acc[45]} solves, {acc[44]} iterations, "
+              f"{acc[44] / acc[45]:.2f} iterations per solve")
+    if acc[46]:
+        print(f"   block 0 lifetime: {acc[46] / 100:.0f} us realtime, {acc[47]} memtime ticks "
+              f"-> shader clock {acc[47] / (acc[46] / 100) :.0f} MHz")
+    for i in range(44):
         if cnt[i]:
             print(f"  {NAMES[i]:24s} calls {cnt[i]:6d}  cycles/call {acc[i]/cnt[i]:9.0f}  share {acc[i]/max(tot,1):6.1%}")
 
