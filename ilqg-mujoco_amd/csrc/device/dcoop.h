@@ -88,6 +88,115 @@ __device__ __forceinline__ double tdot(const double* a, const double* b, int n) 
 }
 
 // ------------------------------------------------------ position stage ---
+// model traits with compile-time sizes and tables (static_models.h)
+template <class M>
+concept StaticModel = requires { std::integral_constant<int, M::nbody>{}; };
+
+// rot_vec_quat / normalize4 with their special cases as selects instead of
+// branches: the same doubles in every case (the general formula is computed
+// and discarded where MuJoCo takes the shortcut), no exec-mask round trips on
+// the serial chain
+__device__ __forceinline__ void rot_vec_quat_sel(double* r, const double* v, const double* q) {
+  const bool vz = v[0] == 0 && v[1] == 0 && v[2] == 0;
+  const bool qi = q[0] == 1 && q[1] == 0 && q[2] == 0 && q[3] == 0;
+  const double t0 = q[0] * v[0] + q[2] * v[2] - q[3] * v[1];
+  const double t1 = q[0] * v[1] + q[3] * v[0] - q[1] * v[2];
+  const double t2 = q[0] * v[2] + q[1] * v[1] - q[2] * v[0];
+  const double r0 = v[0] + 2 * (q[2] * t2 - q[3] * t1);
+  const double r1 = v[1] + 2 * (q[3] * t0 - q[1] * t2);
+  const double r2 = v[2] + 2 * (q[1] * t1 - q[2] * t0);
+  r[0] = vz ? 0.0 : (qi ? v[0] : r0);
+  r[1] = vz ? 0.0 : (qi ? v[1] : r1);
+  r[2] = vz ? 0.0 : (qi ? v[2] : r2);
+}
+__device__ __forceinline__ void normalize4_sel(double* q) {
+  const double norm = sqrt(q[0] * q[0] + q[1] * q[1] + q[2] * q[2] + q[3] * q[3]);
+  const bool tiny = norm < MINVAL;
+  const bool scale = !tiny && fabs(norm - 1) > MINVAL;
+  const double inv = 1 / norm;
+  const double s0 = q[0] * inv, s1 = q[1] * inv, s2 = q[2] * inv, s3 = q[3] * inv;
+  q[0] = tiny ? 1.0 : (scale ? s0 : q[0]);
+  q[1] = tiny ? 0.0 : (scale ? s1 : q[1]);
+  q[2] = tiny ? 0.0 : (scale ? s2 : q[2]);
+  q[3] = tiny ? 0.0 : (scale ? s3 : q[3]);
+}
+
+// The kinematic chain of a compile-time model on lane 0 with every body frame
+// in registers: all model constants and joint inputs are loaded up front (one
+// LDS wait), the tree walk is unrolled, the frames are stored at the end.
+// Same operations in the same order as the loop in kinematics().
+template <class M>
+__device__ inline void kin_chain_static(const M& m, const double* qpos, const double* qloc, double* xpos,
+                                        double* xquat, double* xanchor, double* xaxis) {
+  constexpr int NB = M::nbody, NJ = M::njnt;
+  double bpos[NB][3], bquat[NB][4], jpos[NJ > 0 ? NJ : 1][3], jaxis[NJ > 0 ? NJ : 1][3];
+  double qv[NJ > 0 ? NJ : 1][7], ql[NJ > 0 ? NJ : 1][4];
+  sfor<1, NB>(SLAM(ii) {
+    constexpr int i = SK(ii);
+    ldm<3>(bpos[i], m.body_pos + 3 * i);
+    ldm<4>(bquat[i], m.body_quat + 4 * i);
+  });
+  sfor<0, NJ>(SLAM(jj) {
+    constexpr int j = SK(jj);
+    constexpr int type = M::jnt_type[j], qadr = M::jnt_qposadr[j];
+    ldm<3>(jpos[j], m.jnt_pos + 3 * j);
+    ldm<3>(jaxis[j], m.jnt_axis + 3 * j);
+    if constexpr (type == JNT_FREE) {
+      sfor<0, 7>(SLAM(kk) { qv[j][SK(kk)] = qpos[qadr + SK(kk)]; });
+    } else if constexpr (type == JNT_SLIDE) {
+      qv[j][0] = qpos[qadr] - m.qpos0[qadr];
+    } else {
+      ldm<4>(ql[j], qloc + 4 * j);
+    }
+  });
+  double xp[NB][3], xq[NB][4];
+  xp[0][0] = xp[0][1] = xp[0][2] = 0;
+  xq[0][0] = 1;
+  xq[0][1] = xq[0][2] = xq[0][3] = 0;
+  sfor<1, NB>(SLAM(ii) {
+    constexpr int i = SK(ii);
+    constexpr int pid = M::body_parentid[i];
+    double tmp[3];
+    rot_vec_quat_sel(tmp, bpos[i], xq[pid]);
+    xp[i][0] = xp[pid][0] + tmp[0];
+    xp[i][1] = xp[pid][1] + tmp[1];
+    xp[i][2] = xp[pid][2] + tmp[2];
+    quat_mul(xq[i], xq[pid], bquat[i]);
+    sfor<0, M::body_jntnum[i]>(SLAM(jj) {
+      constexpr int jid = M::body_jntadr[i] + SK(jj);
+      constexpr int type = M::jnt_type[jid];
+      if constexpr (type == JNT_FREE) {
+        xp[i][0] = qv[jid][0]; xp[i][1] = qv[jid][1]; xp[i][2] = qv[jid][2];
+        xq[i][0] = qv[jid][3]; xq[i][1] = qv[jid][4]; xq[i][2] = qv[jid][5]; xq[i][3] = qv[jid][6];
+        normalize4_sel(xq[i]);
+        for (int k = 0; k < 3; k++) { xanchor[3 * jid + k] = xp[i][k]; xaxis[3 * jid + k] = jaxis[jid][k]; }
+      } else {
+        double anc[3], ax[3];
+        rot_vec_quat_sel(anc, jpos[jid], xq[i]);
+        anc[0] += xp[i][0]; anc[1] += xp[i][1]; anc[2] += xp[i][2];
+        rot_vec_quat_sel(ax, jaxis[jid], xq[i]);
+        if constexpr (type == JNT_SLIDE) {
+          const double dq = qv[jid][0];
+          xp[i][0] += ax[0] * dq; xp[i][1] += ax[1] * dq; xp[i][2] += ax[2] * dq;
+        } else {
+          quat_mul(xq[i], xq[i], ql[jid]);
+          rot_vec_quat_sel(tmp, jpos[jid], xq[i]);
+          xp[i][0] = anc[0] - tmp[0];
+          xp[i][1] = anc[1] - tmp[1];
+          xp[i][2] = anc[2] - tmp[2];
+        }
+        for (int k = 0; k < 3; k++) { xanchor[3 * jid + k] = anc[k]; xaxis[3 * jid + k] = ax[k]; }
+      }
+    });
+    normalize4_sel(xq[i]);
+  });
+  sfor<0, NB>(SLAM(ii) {
+    constexpr int i = SK(ii);
+    for (int k = 0; k < 3; k++) xpos[3 * i + k] = xp[i][k];
+    for (int k = 0; k < 4; k++) xquat[4 * i + k] = xq[i][k];
+  });
+}
+
 __device__ inline void kinematics(const auto& m, const auto& L, const auto& C, const Team& T) {
   double* qpos = T.w + L.qpos;
   double* xpos = T.w + L.xpos;
@@ -115,7 +224,10 @@ __device__ inline void kinematics(const auto& m, const auto& L, const auto& C, c
   TSYNC();
   STAMP(11);
   // the kinematic chain: lane 0
-  if (T.tid == 0) {
+  using MT = std::remove_cvref_t<decltype(m)>;
+  if constexpr (StaticModel<MT>) {
+    if (T.tid == 0) kin_chain_static(m, qpos, qloc, xpos, xquat, xanchor, xaxis);
+  } else if (T.tid == 0) {
     xpos[0] = xpos[1] = xpos[2] = 0;
     xquat[0] = 1; xquat[1] = xquat[2] = xquat[3] = 0;
     for (int i = 1; i < m.nbody; i++) {

@@ -497,12 +497,23 @@ hipError_t launch_fd_cols_coop(const DevModel& m, const WsLayout& L, const CoopL
   return hipGetLastError();
 }
 
+// LDS a rollout workgroup reserves: its workspace, or (ILQG_ROLLOUT_LDS) more,
+// so that no FD team can share its CU
+static size_t rollout_lds(size_t need) {
+  static long pad = -1;
+  if (pad < 0) {
+    const char* e = getenv("ILQG_ROLLOUT_LDS");
+    pad = e ? atol(e) : 0;
+  }
+  return (size_t)pad > need ? (size_t)pad : need;
+}
+
 hipError_t launch_rollout_coop(const DevModel& m, const WsLayout& L, const CoopLayout& C, const CoopAux& X, int S,
                                int A, int P, TrajDev nominal, TrajDev out, int out_is_cand, const double* K,
                                const double* k, const double* alphas, TrajDev dinit, const double* qfrc_applied,
                                const double* xfrc_applied, int passive, CostDev cost, double* cost_cand,
                                hipStream_t st) {
-  const size_t lds = coop_lds_bytes(L, C);
+  const size_t lds = rollout_lds(coop_lds_bytes(L, C));
   hipError_t e;
   if (use_dual()) {
 #define ILQG_CASE(id, SMT, SXT)                                                                                 \
