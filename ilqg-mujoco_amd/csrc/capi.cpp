@@ -80,6 +80,11 @@ bool use_coop() {
 }
 constexpr size_t kMaxLds = 160 * 1024;
 
+static int getenv_int(const char* name, int dflt) {
+  const char* e = getenv(name);
+  return e && *e ? atoi(e) : dflt;
+}
+
 int check_device_support(const HostModel& m, bool solver, std::string& why) {
   for (int j = 0; j < m.njnt; j++)
     if ((m.jnt_type[j] == 0 || m.jnt_type[j] == 1) && m.jnt_stiffness[j] != 0) {
@@ -239,10 +244,14 @@ struct ilqg_solver {
   const ilqg_model* model = nullptr;
   ilqg_solver_opts opts{};
   int S = 0, A = 0, P = 0, D = 0, nx = 0, ncol = 0;
+  // FD records at a padded stride Dp (whole 128-byte lines: handoff.h); the
+  // fused sweep (fd_fused) also streams the backward pass behind the FD teams
+  int Dp = 0, WCp = 0, lag = 0, nvt = 0, cv = 0;
+  bool fused = false;
   hipStream_t stream = nullptr;
   DevBuf traj[5], cand[5], dinit[5];
   DevBuf qfrc_applied, xfrc_applied, K, k, deriv, warm_c, cost_c, V, v, cost_cand, cost_sel, sel, alphas, cost;
-  DevBuf wsd, wsi;
+  DevBuf wsd, wsi, cw, sync, fault;
   int nlanes = 0;
   std::vector<double> host_alphas;
   bool initialized = false;
@@ -384,6 +393,27 @@ static bool coop_ok(const ilqg_model* m) {
   return use_coop() && coop_lds_bytes(m->Lc, m->C) <= kMaxLds && rec <= 4 * 64;
 }
 
+// fused FD sweep (kernels_coop.hip k_fd_fused_*): cooperative models whose
+// centre warm start fits one lane per dof and whose FD record fits the
+// backward role's prefetch registers
+static bool fused_ok(const ilqg_model* m) {
+  const HostModel& h = m->host;
+  const int D = h.nv * (2 * h.nv + h.nu) + 2 * h.nv + h.nu;
+  return coop_ok(m) && h.nv <= 64 && D <= 512 && getenv_int("ILQG_FUSED", 1) != 0;
+}
+static int round16(int n) { return (n + 15) / 16 * 16; }
+// qvel columns per V team, and the lag (points) between a centre team and its column teams.
+// Default lag = P: every centre team is issued first, so column teams never wait on
+// a centre still running (hopper bench, MI355X: lag 8 -> 12.9 ms, 64 -> 11.5, P -> 10.6)
+static int fd_cv() { return std::max(1, getenv_int("ILQG_FD_CV", 3)); }
+static int fd_lag(int S, int P) {
+  (void)S;
+  const int l = getenv_int("ILQG_FD_LAG", P);
+  return std::max(0, std::min(l, P));
+}
+// sync block: ticket, pad x3, cflag[npts], done[npts] (u32), padded to 16 bytes
+static size_t sync_bytes(size_t npts) { return ((4 + 2 * npts) * 4 + 15) / 16 * 16; }
+
 int ilqg_model_static_key(const ilqg_model* m, int* key, int cap, int* n) {
   if (!m || !n) return fail(ILQG_ERR_ARG, "null argument");
   *n = (int)m->key.size();
@@ -512,16 +542,37 @@ int ilqg_fd_batch(const ilqg_model* mc, int n, const double* qpos, const double*
              c + 3 * nq + 3 * nv, c + 3 * nq + 3 * nv + nu, c + 3 * nq + 3 * nv + 2 * nu};
   TrajDev st{s.time.as<double>(), s.qpos.as<double>(), s.qvel.as<double>(), s.warm.as<double>(), s.ctrl.as<double>()};
   WsDev ws{s.wsd.as<double>(), s.wsi.as<int>(), lanes};
-  if (coop_ok(m)) {
+  if (fused_ok(m)) {
+    // n points as n one-point trajectories through the fused sweep (no backward roles)
+    const int Dp = round16(D), WCp = round16(h.nv + 1), cv = fd_cv();
+    DevBuf cw, sy, fl, outp;
+    HIPCHK(cw.alloc((size_t)n * WCp * 8));
+    HIPCHK(sy.alloc(sync_bytes(n)));
+    HIPCHK(fl.alloc(16));
+    HIPCHK(outp.alloc((size_t)n * Dp * 8));
+    HIPCHK(hipMemsetAsync(fl.p, 0, 16, m->stream));
+    HIPCHK(hipMemsetAsync(sy.p, 0, sync_bytes(n), m->stream));
+    FdFused a{};
+    a.tr = st; a.S = n; a.P = 1; a.nB = 0; a.lag = fd_lag(n, 1); a.cv = cv; a.nvt = (h.nv + cv - 1) / cv;
+    a.Dp = Dp; a.WCp = WCp; a.qfrc_applied = s.qa.as<double>(); a.xfrc_applied = s.xf.as<double>(); a.cost = cd;
+    a.cw = cw.as<double>(); a.deriv = outp.as<double>(); a.sync = sy.as<unsigned>(); a.fault = fl.as<unsigned>();
+    HIPCHK(launch_fd_fused_coop(m->dm, m->Lc, m->C, m->X, a, m->stream));
+    HIPCHK(hipStreamSynchronize(m->stream));
+    unsigned flt = 0;
+    HIPCHK(hipMemcpy(&flt, fl.p, 4, hipMemcpyDeviceToHost));
+    if (flt) return fail(ILQG_ERR_HIP, "fused FD sweep: a hand-off wait timed out");
+    HIPCHK(hipMemcpy2D(deriv, (size_t)D * 8, outp.p, (size_t)Dp * 8, (size_t)D * 8, n, hipMemcpyDeviceToHost));
+    return ILQG_OK;
+  } else if (coop_ok(m)) {
     HIPCHK(launch_fd_centre_coop(m->dm, m->Lc, m->C, m->X, st, n, 1, s.qa.as<double>(), s.xf.as<double>(), cd,
                                  s.warm_c.as<double>(), s.cost_c.as<double>(), m->stream));
     HIPCHK(launch_fd_cols_coop(m->dm, m->Lc, m->C, m->X, st, n, 1, s.qa.as<double>(), s.xf.as<double>(), cd,
-                               s.warm_c.as<double>(), s.cost_c.as<double>(), s.out.as<double>(), m->stream));
+                               s.warm_c.as<double>(), s.cost_c.as<double>(), s.out.as<double>(), D, m->stream));
   } else {
     HIPCHK(launch_fd_centre(m->dm, m->L, ws, st, n, 1, s.qa.as<double>(), s.xf.as<double>(), cd,
                             s.warm_c.as<double>(), s.cost_c.as<double>(), m->stream));
     HIPCHK(launch_fd_cols(m->dm, m->L, ws, st, n, 1, s.qa.as<double>(), s.xf.as<double>(), cd,
-                          s.warm_c.as<double>(), s.cost_c.as<double>(), s.out.as<double>(), m->stream));
+                          s.warm_c.as<double>(), s.cost_c.as<double>(), s.out.as<double>(), D, m->stream));
   }
   HIPCHK(hipStreamSynchronize(m->stream));
   HIPCHK(hipMemcpy(deriv, s.out.p, (size_t)n * D * 8, hipMemcpyDeviceToHost));
@@ -548,6 +599,12 @@ int ilqg_solver_create(const ilqg_model* mc, const ilqg_solver_opts* o, const il
   s->nx = 2 * h.nv;
   s->D = h.nv * (2 * h.nv + h.nu) + 2 * h.nv + h.nu;
   s->ncol = std::min(h.nu, h.nv) + 2 * h.nv;
+  s->Dp = round16(s->D);
+  s->WCp = round16(h.nv + 1);
+  s->fused = fused_ok(m);
+  s->cv = fd_cv();
+  s->nvt = (h.nv + s->cv - 1) / s->cv;
+  s->lag = fd_lag(o->nseed, o->horizon + 1);
   s->host_alphas.assign(o->nalpha, 1.0);
   if (o->alphas) std::copy(o->alphas, o->alphas + o->nalpha, s->host_alphas.begin());
   s->opts.alphas = nullptr;
@@ -570,7 +627,12 @@ int ilqg_solver_create(const ilqg_model* mc, const ilqg_solver_opts* o, const il
   ALLOC(s->xfrc_applied, S * 6 * h.nbody * 8);
   ALLOC(s->K, S * P * h.nu * s->nx * 8);  // zero-initialised gains (quirk Q12)
   ALLOC(s->k, S * P * h.nu * 8);
-  ALLOC(s->deriv, S * P * s->D * 8);
+  ALLOC(s->deriv, S * P * s->Dp * 8);
+  if (s->fused) {
+    ALLOC(s->cw, S * P * s->WCp * 8);
+    ALLOC(s->sync, sync_bytes(S * P));
+  }
+  ALLOC(s->fault, 16);
   ALLOC(s->warm_c, S * P * h.nv * 8);
   ALLOC(s->cost_c, S * P * 8);
   ALLOC(s->V, S * s->nx * s->nx * 8);
@@ -682,14 +744,16 @@ int ilqg_solver_get_gains(ilqg_solver* s, double* K, double* k) {
 int ilqg_solver_get_deriv(ilqg_solver* s, double* deriv) {
   if (!s || !deriv) return fail(ILQG_ERR_ARG, "bad argument");
   HIPCHK(hipStreamSynchronize(s->stream));
-  HIPCHK(hipMemcpy(deriv, s->deriv.p, s->deriv.n, hipMemcpyDeviceToHost));
+  HIPCHK(hipMemcpy2D(deriv, (size_t)s->D * 8, s->deriv.p, (size_t)s->Dp * 8, (size_t)s->D * 8, (size_t)s->S * s->P,
+                     hipMemcpyDeviceToHost));
   return ILQG_OK;
 }
 
 int ilqg_solver_set_deriv(ilqg_solver* s, const double* deriv) {
   if (!s || !deriv) return fail(ILQG_ERR_ARG, "bad argument");
   HIPCHK(hipStreamSynchronize(s->stream));
-  HIPCHK(hipMemcpy(s->deriv.p, deriv, s->deriv.n, hipMemcpyHostToDevice));
+  HIPCHK(hipMemcpy2D(s->deriv.p, (size_t)s->Dp * 8, deriv, (size_t)s->D * 8, (size_t)s->D * 8, (size_t)s->S * s->P,
+                     hipMemcpyHostToDevice));
   return ILQG_OK;
 }
 
@@ -732,11 +796,45 @@ int ilqg_forward(ilqg_solver* s) {
   return ILQG_OK;
 }
 
+// the fused sweep's launch: its hand-off words zeroed on the stream first
+static hipError_t fused_launch(ilqg_solver* s, bool with_backward) {
+  const ilqg_model* m = s->model;
+  hipError_t e = hipMemsetAsync(s->sync.p, 0, s->sync.n, s->stream);
+  if (e != hipSuccess) return e;
+  FdFused a{};
+  a.tr = s->tview(s->traj);
+  a.S = s->S;
+  a.P = s->P;
+  a.nB = with_backward ? s->S : 0;
+  a.lag = s->lag;
+  a.nvt = s->nvt;
+  a.cv = s->cv;
+  a.Dp = s->Dp;
+  a.WCp = s->WCp;
+  a.qfrc_applied = s->qfrc_applied.as<double>();
+  a.xfrc_applied = s->xfrc_applied.as<double>();
+  a.cost = s->cview();
+  a.cw = s->cw.as<double>();
+  a.deriv = s->deriv.as<double>();
+  a.sync = s->sync.as<unsigned>();
+  a.fault = s->fault.as<unsigned>();
+  a.mu = s->opts.mu;
+  a.K = s->K.as<double>();
+  a.k = s->k.as<double>();
+  a.V = s->V.as<double>();
+  a.v = s->v.as<double>();
+  return launch_fd_fused_coop(m->dm, m->Lc, m->C, m->X, a, s->stream);
+}
+
 int ilqg_fd_sweep(ilqg_solver* s) {
   if (!s || !s->initialized) return fail(ILQG_ERR_ARG, "solver not initialised");
   const ilqg_model* m = s->model;
   TrajDev nom = s->tview(s->traj);
   const int npts = s->S * s->P;
+  if (s->fused) {
+    HIPCHK(s->timed(3, [&] { return fused_launch(s, false); }));
+    return ILQG_OK;
+  }
   HIPCHK(s->timed(2, [&] {
     if (coop_ok(m))
       return launch_fd_centre_coop(m->dm, m->Lc, m->C, m->X, nom, npts, s->P, s->qfrc_applied.as<double>(),
@@ -750,10 +848,10 @@ int ilqg_fd_sweep(ilqg_solver* s) {
     if (coop_ok(m))
       return launch_fd_cols_coop(m->dm, m->Lc, m->C, m->X, nom, npts, s->P, s->qfrc_applied.as<double>(),
                                  s->xfrc_applied.as<double>(), s->cview(), s->warm_c.as<double>(),
-                                 s->cost_c.as<double>(), s->deriv.as<double>(), s->stream);
+                                 s->cost_c.as<double>(), s->deriv.as<double>(), s->Dp, s->stream);
     return launch_fd_cols(m->dm, m->L, s->ws(), nom, npts, s->P, s->qfrc_applied.as<double>(),
                           s->xfrc_applied.as<double>(), s->cview(), s->warm_c.as<double>(), s->cost_c.as<double>(),
-                          s->deriv.as<double>(), s->stream);
+                          s->deriv.as<double>(), s->Dp, s->stream);
   }));
   return ILQG_OK;
 }
@@ -762,7 +860,7 @@ int ilqg_backward(ilqg_solver* s) {
   if (!s || !s->initialized) return fail(ILQG_ERR_ARG, "solver not initialised");
   const ilqg_model* m = s->model;
   HIPCHK(s->timed(4, [&] {
-    return launch_backward(m->dm, s->S, s->P, s->opts.mu, s->deriv.as<double>(), s->tview(s->traj),
+    return launch_backward(m->dm, s->S, s->P, s->opts.mu, s->deriv.as<double>(), s->Dp, s->tview(s->traj),
                            s->K.as<double>(), s->k.as<double>(), s->V.as<double>(), s->v.as<double>(), s->stream);
   }));
   return ILQG_OK;
@@ -771,6 +869,11 @@ int ilqg_backward(ilqg_solver* s) {
 int ilqg_iterate(ilqg_solver* s) {
   int rc = ilqg_forward(s);
   if (rc) return rc;
+  if (s->fused) {
+    // FD sweep with the Riccati recursion of every seed streamed behind it (one launch)
+    HIPCHK(s->timed(5, [&] { return fused_launch(s, true); }));
+    return ILQG_OK;
+  }
   rc = ilqg_fd_sweep(s);
   if (rc) return rc;
   return ilqg_backward(s);
@@ -779,6 +882,9 @@ int ilqg_iterate(ilqg_solver* s) {
 int ilqg_synchronize(ilqg_solver* s) {
   if (!s) return fail(ILQG_ERR_ARG, "null solver");
   HIPCHK(hipStreamSynchronize(s->stream));
+  unsigned flt = 0;
+  HIPCHK(hipMemcpy(&flt, s->fault.p, 4, hipMemcpyDeviceToHost));
+  if (flt) return fail(ILQG_ERR_HIP, "fused FD sweep: a hand-off wait timed out");
   return ILQG_OK;
 }
 

@@ -122,33 +122,13 @@ __device__ __forceinline__ void normalize4_sel(double* q) {
 }
 
 // The kinematic chain of a compile-time model on lane 0 with every body frame
-// in registers: all model constants and joint inputs are loaded up front (one
-// LDS wait), the tree walk is unrolled, the frames are stored at the end.
-// Same operations in the same order as the loop in kinematics().
+// in registers (no store->load round trip through LDS between a body and its
+// children): the tree walk is unrolled with compile-time parent indices and
+// joint types.  Same operations in the same order as the loop in kinematics().
 template <class M>
 __device__ inline void kin_chain_static(const M& m, const double* qpos, const double* qloc, double* xpos,
                                         double* xquat, double* xanchor, double* xaxis) {
-  constexpr int NB = M::nbody, NJ = M::njnt;
-  double bpos[NB][3], bquat[NB][4], jpos[NJ > 0 ? NJ : 1][3], jaxis[NJ > 0 ? NJ : 1][3];
-  double qv[NJ > 0 ? NJ : 1][7], ql[NJ > 0 ? NJ : 1][4];
-  sfor<1, NB>(SLAM(ii) {
-    constexpr int i = SK(ii);
-    ldm<3>(bpos[i], m.body_pos + 3 * i);
-    ldm<4>(bquat[i], m.body_quat + 4 * i);
-  });
-  sfor<0, NJ>(SLAM(jj) {
-    constexpr int j = SK(jj);
-    constexpr int type = M::jnt_type[j], qadr = M::jnt_qposadr[j];
-    ldm<3>(jpos[j], m.jnt_pos + 3 * j);
-    ldm<3>(jaxis[j], m.jnt_axis + 3 * j);
-    if constexpr (type == JNT_FREE) {
-      sfor<0, 7>(SLAM(kk) { qv[j][SK(kk)] = qpos[qadr + SK(kk)]; });
-    } else if constexpr (type == JNT_SLIDE) {
-      qv[j][0] = qpos[qadr] - m.qpos0[qadr];
-    } else {
-      ldm<4>(ql[j], qloc + 4 * j);
-    }
-  });
+  constexpr int NB = M::nbody;
   double xp[NB][3], xq[NB][4];
   xp[0][0] = xp[0][1] = xp[0][2] = 0;
   xq[0][0] = 1;
@@ -156,31 +136,38 @@ __device__ inline void kin_chain_static(const M& m, const double* qpos, const do
   sfor<1, NB>(SLAM(ii) {
     constexpr int i = SK(ii);
     constexpr int pid = M::body_parentid[i];
-    double tmp[3];
-    rot_vec_quat_sel(tmp, bpos[i], xq[pid]);
+    double tmp[3], bpos[3], bquat[4];
+    ldm<3>(bpos, m.body_pos + 3 * i);
+    ldm<4>(bquat, m.body_quat + 4 * i);
+    rot_vec_quat_sel(tmp, bpos, xq[pid]);
     xp[i][0] = xp[pid][0] + tmp[0];
     xp[i][1] = xp[pid][1] + tmp[1];
     xp[i][2] = xp[pid][2] + tmp[2];
-    quat_mul(xq[i], xq[pid], bquat[i]);
+    quat_mul(xq[i], xq[pid], bquat);
     sfor<0, M::body_jntnum[i]>(SLAM(jj) {
       constexpr int jid = M::body_jntadr[i] + SK(jj);
-      constexpr int type = M::jnt_type[jid];
+      constexpr int type = M::jnt_type[jid], qadr = M::jnt_qposadr[jid];
+      double jpos[3], jaxis[3];
+      ldm<3>(jpos, m.jnt_pos + 3 * jid);
+      ldm<3>(jaxis, m.jnt_axis + 3 * jid);
       if constexpr (type == JNT_FREE) {
-        xp[i][0] = qv[jid][0]; xp[i][1] = qv[jid][1]; xp[i][2] = qv[jid][2];
-        xq[i][0] = qv[jid][3]; xq[i][1] = qv[jid][4]; xq[i][2] = qv[jid][5]; xq[i][3] = qv[jid][6];
+        for (int k = 0; k < 3; k++) xp[i][k] = qpos[qadr + k];
+        for (int k = 0; k < 4; k++) xq[i][k] = qpos[qadr + 3 + k];
         normalize4_sel(xq[i]);
-        for (int k = 0; k < 3; k++) { xanchor[3 * jid + k] = xp[i][k]; xaxis[3 * jid + k] = jaxis[jid][k]; }
+        for (int k = 0; k < 3; k++) { xanchor[3 * jid + k] = xp[i][k]; xaxis[3 * jid + k] = jaxis[k]; }
       } else {
         double anc[3], ax[3];
-        rot_vec_quat_sel(anc, jpos[jid], xq[i]);
+        rot_vec_quat_sel(anc, jpos, xq[i]);
         anc[0] += xp[i][0]; anc[1] += xp[i][1]; anc[2] += xp[i][2];
-        rot_vec_quat_sel(ax, jaxis[jid], xq[i]);
+        rot_vec_quat_sel(ax, jaxis, xq[i]);
         if constexpr (type == JNT_SLIDE) {
-          const double dq = qv[jid][0];
+          const double dq = qpos[qadr] - m.qpos0[qadr];
           xp[i][0] += ax[0] * dq; xp[i][1] += ax[1] * dq; xp[i][2] += ax[2] * dq;
         } else {
-          quat_mul(xq[i], xq[i], ql[jid]);
-          rot_vec_quat_sel(tmp, jpos[jid], xq[i]);
+          double ql[4];
+          ldm<4>(ql, qloc + 4 * jid);
+          quat_mul(xq[i], xq[i], ql);
+          rot_vec_quat_sel(tmp, jpos, xq[i]);
           xp[i][0] = anc[0] - tmp[0];
           xp[i][1] = anc[1] - tmp[1];
           xp[i][2] = anc[2] - tmp[2];
@@ -189,12 +176,12 @@ __device__ inline void kin_chain_static(const M& m, const double* qpos, const do
       }
     });
     normalize4_sel(xq[i]);
-  });
-  sfor<0, NB>(SLAM(ii) {
-    constexpr int i = SK(ii);
     for (int k = 0; k < 3; k++) xpos[3 * i + k] = xp[i][k];
     for (int k = 0; k < 4; k++) xquat[4 * i + k] = xq[i][k];
   });
+  for (int k = 0; k < 3; k++) xpos[k] = 0;
+  xquat[0] = 1;
+  xquat[1] = xquat[2] = xquat[3] = 0;
 }
 
 __device__ inline void kinematics(const auto& m, const auto& L, const auto& C, const Team& T) {
@@ -1515,6 +1502,25 @@ __device__ inline void forward_skip(const auto& m, const auto& L, const auto& C,
   if (skipstage < STAGE_POS) fwd_position(m, L, C, X, T);
   if (skipstage < STAGE_VEL) fwd_velocity(m, L, C, T);
   STAMP(6);
+  fwd_acceleration(m, L, X, T);
+  STAMP(7);
+  fwd_constraint(m, L, C, X, T, maxiter, tol);
+  STAMP(8);
+}
+
+// forward_skip split at the warm start: the position and velocity stages never
+// read qacc_warmstart, the acceleration stage's constraint solve does
+__device__ inline void forward_posvel(const auto& m, const auto& L, const auto& C, const auto& X, const Team& T,
+                                      int skipstage) {
+  STAMP(-1);
+  TSYNC();
+  if (skipstage < STAGE_POS) fwd_position(m, L, C, X, T);
+  if (skipstage < STAGE_VEL) fwd_velocity(m, L, C, T);
+  STAMP(6);
+}
+__device__ inline void forward_acc(const auto& m, const auto& L, const auto& C, const auto& X, const Team& T,
+                                   int maxiter, double tol) {
+  STAMP(-1);
   fwd_acceleration(m, L, X, T);
   STAMP(7);
   fwd_constraint(m, L, C, X, T, maxiter, tol);

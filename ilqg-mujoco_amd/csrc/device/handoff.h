@@ -1,0 +1,67 @@
+// In-launch hand-offs between workgroups (gfx950: 8 XCDs with private L2s,
+// per-CU L1s never refreshed by other CUs' stores).
+//
+// Protocol (MI355X_MICROARCH.md "inter-workgroup visibility", Valid forms,
+// first row): the producer stores every handed-off word write-through (sc1,
+// an 8-byte relaxed agent-scope atomic store), drains them with
+// s_waitcnt vmcnt(0), then ONE lane signals with an agent-scope atomic (a
+// counter add or a flag store).  The consumer polls that word relaxed (sc1
+// load, bounded, with s_sleep) and reads every handed-off word with sc1 loads
+// (L1 bypassed).  Handed-off records are padded to whole 128-byte lines that
+// nothing reads before they are published in the launch, so no stale copy of
+// them can sit in any cache.  Every polled word is zeroed before each launch.
+#pragma once
+#include <hip/hip_runtime.h>
+
+namespace ilqg {
+
+typedef __attribute__((address_space(1))) unsigned gu32;
+typedef __attribute__((address_space(1))) unsigned long long gu64;
+
+// ~2^22 polls of >= 256 cycles: seconds, far beyond any legitimate wait; a
+// timed-out wait sets *fault (reported by ilqg_synchronize) and gives up, so a
+// broken producer can never hang the GPU
+constexpr unsigned HANDOFF_SPIN_LIMIT = 1u << 22;
+
+__device__ __forceinline__ double ld_sc1(const double* p) {
+  return __longlong_as_double(
+      (long long)__hip_atomic_load((gu64*)(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+}
+__device__ __forceinline__ void st_sc1(double* p, double v) {
+  __hip_atomic_store((gu64*)(p), (unsigned long long)__double_as_longlong(v), __ATOMIC_RELAXED,
+                     __HIP_MEMORY_SCOPE_AGENT);
+}
+// every storing wave, after its sc1 payload stores and before the signal
+__device__ __forceinline__ void drain_stores() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+
+// wave-uniform: every lane polls the same word until it reaches `target`
+__device__ inline bool bw_wait_geq(const unsigned* w, unsigned target, unsigned* fault) {
+  for (unsigned spins = 0;; spins++) {
+    // after one timed-out wait every later one gives up at once
+    if ((spins & 255) == 255 && fault &&
+        __builtin_amdgcn_readfirstlane(__hip_atomic_load((gu32*)(fault), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)))
+      return false;
+    const unsigned v = __builtin_amdgcn_readfirstlane(
+        __hip_atomic_load((gu32*)(w), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+    if (v >= target) break;
+    if (spins > HANDOFF_SPIN_LIMIT) {
+      if (fault && (threadIdx.x & 63) == 0) __hip_atomic_fetch_or((gu32*)(fault), 1u, __ATOMIC_RELAXED,
+                                                                 __HIP_MEMORY_SCOPE_AGENT);
+      return false;
+    }
+    __builtin_amdgcn_s_sleep(4);
+  }
+  // keep the payload's loads below the poll
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  return true;
+}
+
+// one lane signals for the (single-wave) team after drain_stores()
+__device__ __forceinline__ void signal_add(unsigned* w) {
+  __hip_atomic_fetch_add((gu32*)(w), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void signal_set(unsigned* w, unsigned v) {
+  __hip_atomic_store((gu32*)(w), v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+}  // namespace ilqg

@@ -35,7 +35,7 @@ hipError_t launch_fd_centre(const DevModel& m, const WsLayout& L, WsDev ws, Traj
 // FD columns: npts * (nctrl + 2nv) lanes, writes deriv[npts][D]
 hipError_t launch_fd_cols(const DevModel& m, const WsLayout& L, WsDev ws, TrajDev tr, int npts, int P,
                           const double* qfrc_applied, const double* xfrc_applied, CostDev cost,
-                          const double* warm_c, const double* cost_c, double* deriv, hipStream_t st);
+                          const double* warm_c, const double* cost_c, double* deriv, int Ds, hipStream_t st);
 // rollout: S*A lanes; passive=1 keeps ctrl (ILQR ctor), else u = K dx + alpha k + u*
 hipError_t launch_rollout(const DevModel& m, const WsLayout& L, WsDev ws, int S, int A, int P, TrajDev nominal,
                           TrajDev out, int out_is_cand, const double* K, const double* k, const double* alphas,
@@ -45,8 +45,9 @@ hipError_t launch_rollout(const DevModel& m, const WsLayout& L, WsDev ws, int S,
 hipError_t launch_select(const DevModel& m, int S, int A, int P, int mode, int copy_cand, const double* cost_cand,
                          int* sel, double* cost_sel, TrajDev cand, TrajDev nominal, TrajDev dinit, hipStream_t st);
 // Riccati backward pass, one workgroup per seed
-hipError_t launch_backward(const DevModel& m, int S, int P, double mu, const double* deriv, TrajDev tr, double* K,
-                           double* k, double* V, double* v, hipStream_t st);
+// deriv records at stride Ds (>= D) doubles
+hipError_t launch_backward(const DevModel& m, int S, int P, double mu, const double* deriv, int Ds, TrajDev tr,
+                           double* K, double* k, double* V, double* v, hipStream_t st);
 // n independent states: nstep mj_step each (in place)
 hipError_t launch_step(const DevModel& m, const WsLayout& L, WsDev ws, TrajDev st_, int n, int nstep,
                        const double* qfrc_applied, const double* xfrc_applied, hipStream_t st);
@@ -55,6 +56,25 @@ hipError_t launch_forward(const DevModel& m, const WsLayout& L, WsDev ws, TrajDe
                           const double* qfrc_applied, const double* xfrc_applied, double* qacc, hipStream_t st);
 
 size_t backward_lds_bytes(int nv, int nu);
+
+// fused FD sweep + streamed backward pass (kernels_coop.hip)
+struct FdFused {
+  TrajDev tr;
+  int S, P;
+  int nB;        // backward roles (S, or 0 for the sweep alone)
+  int lag;       // points between a centre team and its column teams
+  int nvt, cv;   // qvel teams per point, columns per qvel team
+  int Dp, WCp;   // padded record strides (doubles, multiples of 16 = 128 B)
+  const double* qfrc_applied;
+  const double* xfrc_applied;
+  CostDev cost;
+  double* cw;      // [S*P][WCp]: centre warm start (nv) + centre cost
+  double* deriv;   // [S*P][Dp]
+  unsigned* sync;  // [4 + 2 S P]: ticket, pad, cflag[S*P], done[S*P]; zeroed before each launch
+  unsigned* fault; // set by a timed-out wait
+  double mu;
+  double *K, *k, *V, *v;
+};
 
 }  // namespace ilqg
 
@@ -68,7 +88,9 @@ hipError_t launch_fd_centre_coop(const DevModel& m, const WsLayout& L, const coo
 hipError_t launch_fd_cols_coop(const DevModel& m, const WsLayout& L, const coop::CoopLayout& C,
                                const coop::CoopAux& X, TrajDev tr, int npts, int P, const double* qfrc_applied,
                                const double* xfrc_applied, CostDev cost, const double* warm_c, const double* cost_c,
-                               double* deriv, hipStream_t st);
+                               double* deriv, int Ds, hipStream_t st);
+hipError_t launch_fd_fused_coop(const DevModel& m, const WsLayout& L, const coop::CoopLayout& C,
+                                const coop::CoopAux& X, const FdFused& a, hipStream_t st);
 hipError_t launch_rollout_coop(const DevModel& m, const WsLayout& L, const coop::CoopLayout& C,
                                const coop::CoopAux& X, int S, int A, int P, TrajDev nominal, TrajDev out,
                                int out_is_cand, const double* K, const double* k, const double* alphas, TrajDev dinit,

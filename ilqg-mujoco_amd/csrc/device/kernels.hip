@@ -92,7 +92,7 @@ __global__ __launch_bounds__(LANE_BLOCK) void k_fd_centre(DevModel m, WsLayout L
 __global__ __launch_bounds__(LANE_BLOCK) void k_fd_cols(DevModel m, WsLayout L, WsDev ws, TrajDev tr, int npts,
                                                         int P, const double* qfrc_applied, const double* xfrc_applied,
                                                         CostDev cost, const double* warm_c, const double* cost_c,
-                                                        double* deriv) {
+                                                        double* deriv, int Ds) {
   const int nv = m.nv, nu = m.nu;
   const int nctrl = nu < nv ? nu : nv;  // mjderivative.cpp:78-82 (assumes nv >= nu)
   const int ncol = nctrl + 2 * nv;
@@ -100,8 +100,7 @@ __global__ __launch_bounds__(LANE_BLOCK) void k_fd_cols(DevModel m, WsLayout L, 
   if (lane >= npts * ncol) return;
   int pt = lane / ncol, col = lane % ncol, seed = pt / P;
   Lane ln{ws.d + lane, ws.i + lane, (size_t)ws.nlanes};
-  const int D = nv * (2 * nv + nu) + 2 * nv + nu;
-  double* dr = deriv + (size_t)pt * D;
+  double* dr = deriv + (size_t)pt * Ds;  // record stride Ds >= D
   const double* wc = warm_c + (size_t)pt * nv;
   const double costCenter = cost_c[pt];
   SPd qpos = ln.D(L.qpos), qvel = ln.D(L.qvel), ctrl = ln.D(L.ctrl), warm = ln.D(L.warm), qacc = ln.D(L.qacc);
@@ -299,12 +298,12 @@ hipError_t launch_fd_centre(const DevModel& m, const WsLayout& L, WsDev ws, Traj
 
 hipError_t launch_fd_cols(const DevModel& m, const WsLayout& L, WsDev ws, TrajDev tr, int npts, int P,
                           const double* qfrc_applied, const double* xfrc_applied, CostDev cost, const double* warm_c,
-                          const double* cost_c, double* deriv, hipStream_t st) {
+                          const double* cost_c, double* deriv, int Ds, hipStream_t st) {
   int nctrl = m.nu < m.nv ? m.nu : m.nv;
   long lanes = (long)npts * (nctrl + 2 * m.nv);
   if (lanes <= 0) return hipSuccess;
   hipLaunchKernelGGL(k_fd_cols, dim3(nblk(lanes, LANE_BLOCK)), dim3(LANE_BLOCK), 0, st, m, L, ws, tr, npts, P,
-                     qfrc_applied, xfrc_applied, cost, warm_c, cost_c, deriv);
+                     qfrc_applied, xfrc_applied, cost, warm_c, cost_c, deriv, Ds);
   return hipGetLastError();
 }
 

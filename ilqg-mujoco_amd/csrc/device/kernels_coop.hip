@@ -3,8 +3,12 @@
 //   k_fd_centre_coop  src/mjderivative.cpp:61-75   one workgroup per trajectory point
 //   k_fd_cols_coop    src/mjderivative.cpp:78-206  one workgroup per (point, column)
 //   k_rollout_coop    inc/ilqr.h:116-130           one workgroup per (seed, alpha)
+#include <algorithm>
+
 #include "dcoop.h"
+#include "handoff.h"
 #include "kernels.h"
+#include "riccati.h"
 #include "static_models.h"
 
 namespace ilqg {
@@ -16,6 +20,9 @@ constexpr double FD_EPS = 1e-6;  // mjderivative.cpp:39
 constexpr int FD_NITER = 30;     // mjderivative.cpp:37
 constexpr int FD_NWARMUP = 3;    // mjderivative.cpp:38
 constexpr int TEAM = TEAM_SIZE;
+// FD teams: at least 2 waves per SIMD (<= 256 VGPRs), so LDS (6 teams per CU
+// for the hopper) and not registers bounds the sweep's occupancy
+constexpr int FD_WAVES_PER_EU = 2;
 
 // LDS: [workspace doubles][coop doubles][model image][workspace ints][coop ints]
 __device__ inline Team make_team(const auto& L, const auto& C) {
@@ -135,7 +142,7 @@ __device__ inline void fd_centre_body(const auto& m, const auto& L, const auto& 
   STAMP_FLUSH();
 }
 
-__global__ __launch_bounds__(TEAM) void k_fd_centre_coop(DevModel mg, WsLayout L, CoopLayout C, CoopAux Xg, TrajDev tr, int P, const double* qfrc_applied, const double* xfrc_applied, CostDev cost, double* warm_c, double* cost_c) {
+__global__ __launch_bounds__(TEAM, FD_WAVES_PER_EU) void k_fd_centre_coop(DevModel mg, WsLayout L, CoopLayout C, CoopAux Xg, TrajDev tr, int P, const double* qfrc_applied, const double* xfrc_applied, CostDev cost, double* warm_c, double* cost_c) {
   Team T = make_team(L, C);
   DevModel m;
   CoopAux X;
@@ -145,7 +152,7 @@ __global__ __launch_bounds__(TEAM) void k_fd_centre_coop(DevModel mg, WsLayout L
 
 // model-specific instance (static_models.h): compile-time sizes, tables and LDS layout
 template <class SM, class SX>
-__global__ __launch_bounds__(TEAM) void k_fd_centre_s(DevModel mg, TrajDev tr, int P, const double* qfrc_applied, const double* xfrc_applied, CostDev cost, double* warm_c, double* cost_c) {
+__global__ __launch_bounds__(TEAM, FD_WAVES_PER_EU) void k_fd_centre_s(DevModel mg, TrajDev tr, int P, const double* qfrc_applied, const double* xfrc_applied, CostDev cost, double* warm_c, double* cost_c) {
   static constexpr WsLayout L = make_layout(SM{}, SX::npair);
   static constexpr CoopLayout C = make_coop_layout(SM{}, SX::npair);
   static constexpr SX X{};
@@ -156,14 +163,13 @@ __global__ __launch_bounds__(TEAM) void k_fd_centre_s(DevModel mg, TrajDev tr, i
 }
 
 __device__ inline void fd_cols_body(const auto& m, const auto& L, const auto& C, const auto& X, const Team& T,
-                                TrajDev tr, int P, const double* qfrc_applied, const double* xfrc_applied, CostDev cost, const double* warm_c, const double* cost_c, double* deriv) {
+                                TrajDev tr, int P, const double* qfrc_applied, const double* xfrc_applied, CostDev cost, const double* warm_c, const double* cost_c, double* deriv, int Ds) {
   STAMP_INIT();
   const int nv = m.nv, nu = m.nu;
   const int nctrl = nu < nv ? nu : nv;  // mjderivative.cpp:78-82 (assumes nv >= nu)
   const int ncol = nctrl + 2 * nv;
   const int pt = blockIdx.x / ncol, col = blockIdx.x % ncol;
-  const int D = nv * (2 * nv + nu) + 2 * nv + nu;
-  double* dr = deriv + (size_t)pt * D;
+  double* dr = deriv + (size_t)pt * Ds;  // record stride Ds >= D
   const double* wc = warm_c + (size_t)pt * nv;
   const double costCenter = cost_c[pt];
   double* qpos = T.w + L.qpos;
@@ -240,24 +246,242 @@ __device__ inline void fd_cols_body(const auto& m, const auto& L, const auto& C,
   STAMP_FLUSH();
 }
 
-__global__ __launch_bounds__(TEAM) void k_fd_cols_coop(DevModel mg, WsLayout L, CoopLayout C, CoopAux Xg, TrajDev tr, int P, const double* qfrc_applied, const double* xfrc_applied, CostDev cost, const double* warm_c, const double* cost_c, double* deriv) {
+__global__ __launch_bounds__(TEAM, FD_WAVES_PER_EU) void k_fd_cols_coop(DevModel mg, WsLayout L, CoopLayout C, CoopAux Xg, TrajDev tr, int P, const double* qfrc_applied, const double* xfrc_applied, CostDev cost, const double* warm_c, const double* cost_c, double* deriv, int Ds) {
   Team T = make_team(L, C);
   DevModel m;
   CoopAux X;
   stage_model(mg, Xg, L, C, T, m, X);
-  fd_cols_body(m, L, C, X, T, tr, P, qfrc_applied, xfrc_applied, cost, warm_c, cost_c, deriv);
+  fd_cols_body(m, L, C, X, T, tr, P, qfrc_applied, xfrc_applied, cost, warm_c, cost_c, deriv, Ds);
 }
 
 // model-specific instance (static_models.h): compile-time sizes, tables and LDS layout
 template <class SM, class SX>
-__global__ __launch_bounds__(TEAM) void k_fd_cols_s(DevModel mg, TrajDev tr, int P, const double* qfrc_applied, const double* xfrc_applied, CostDev cost, const double* warm_c, const double* cost_c, double* deriv) {
+__global__ __launch_bounds__(TEAM, FD_WAVES_PER_EU) void k_fd_cols_s(DevModel mg, TrajDev tr, int P, const double* qfrc_applied, const double* xfrc_applied, CostDev cost, const double* warm_c, const double* cost_c, double* deriv, int Ds) {
   static constexpr WsLayout L = make_layout(SM{}, SX::npair);
   static constexpr CoopLayout C = make_coop_layout(SM{}, SX::npair);
   static constexpr SX X{};
   Team T = make_team(L, C);
   SM m;
   stage_model_s(mg, L, C, T, m);
-  fd_cols_body(m, L, C, X, T, tr, P, qfrc_applied, xfrc_applied, cost, warm_c, cost_c, deriv);
+  fd_cols_body(m, L, C, X, T, tr, P, qfrc_applied, xfrc_applied, cost, warm_c, cost_c, deriv, Ds);
+}
+
+// ---- fused FD sweep with the backward pass streamed behind it ------------
+// One launch per sweep.  A workgroup takes a ticket (an atomic counter) when it
+// starts; tickets < nB are backward-pass roles (one per seed), the rest are FD
+// teams in point-major order, terminal point first -- the order the Riccati
+// recursion consumes them (inc/ilqr.h:144):
+//   C(s,p): cpMjData + mj_forward + 2 forwardSkip(VEL) (mjderivative.cpp:61-75),
+//           publishes the centre warm start and cost, then the ctrl columns
+//           (:78-111) on its own position/velocity stages (the reference's
+//           forwardSkip(mjSTAGE_VEL));
+//   V(s,p,k): qvel columns k*cv .. (:114-142) on one position stage
+//           (forwardSkip(mjSTAGE_POS));
+//   Q(s,p,i): qpos column i (:145-206).
+// V and Q teams run their first position/velocity stages before they wait for
+// C's warm start (those stages never read it); the V/Q teams of point p are
+// issued `lag` points after C(p).  A team stores its deriv entries
+// write-through and announces them on done[s,p] (handoff.h); the backward role
+// reads record p once all 1 + nvt + nv teams have announced.  Every evaluation
+// reads exactly the inputs the two-kernel sweep gives it, so the records are
+// bit-identical.  Deadlock-free: a team waits only on work holding a smaller
+// ticket (already running, never waiting), the backward roles only on FD teams
+// (which never wait on them).
+__device__ inline unsigned take_ticket(unsigned* sync) {
+  unsigned t = 0;
+  if ((threadIdx.x & (TEAM - 1)) == 0)
+    t = __hip_atomic_fetch_add((gu32*)sync, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  return __builtin_amdgcn_readfirstlane(t);
+}
+
+// FD item u -> role (0 = C, 1 = V, 2 = Q), seed, point, index; ntm = nvt + nv
+__device__ inline void fd_decode(const FdFused& a, unsigned ntm, unsigned u, int& role, int& s, int& p, int& idx) {
+  const unsigned nC = a.S, nW = a.S * ntm, lag = a.lag, P = a.P;
+  idx = 0;
+  if (u < lag * nC) {
+    role = 0; p = u / nC; s = u % nC;
+    return;
+  }
+  u -= lag * nC;
+  const unsigned blk = nC + nW;
+  unsigned g, o;
+  if (u < (P - lag) * blk) {
+    g = lag + u / blk;
+    o = u % blk;
+    if (o < nC) {
+      role = 0; p = g; s = o;
+      return;
+    }
+    o -= nC;
+  } else {
+    u -= (P - lag) * blk;
+    g = P + u / nW;
+    o = u % nW;
+  }
+  p = g - lag;
+  s = o / ntm;
+  const int w = o % ntm;
+  if (w < a.nvt) { role = 1; idx = w; }
+  else { role = 2; idx = w - a.nvt; }
+}
+
+__device__ inline void fd_fused_body(const auto& m, const auto& L, const auto& C, const auto& X, const Team& T,
+                                     const FdFused& a, unsigned u) {
+  STAMP_INIT();
+  const int nv = m.nv, nu = m.nu, nq = m.nq;
+  const int nctrl = nu < nv ? nu : nv;  // mjderivative.cpp:78-82 (assumes nv >= nu)
+  int role, s, p, idx;
+  fd_decode(a, a.nvt + nv, u, role, s, p, idx);
+  const int pt = s * a.P + p;
+  double* dr = a.deriv + (size_t)pt * a.Dp;
+  double* cwp = a.cw + (size_t)pt * a.WCp;
+  unsigned* cflag = a.sync + 4 + pt;
+  unsigned* done = a.sync + 4 + (size_t)a.S * a.P + pt;
+  double* qpos = T.w + L.qpos;
+  double* qvel = T.w + L.qvel;
+  double* ctrl = T.w + L.ctrl;
+  double* warm = T.w + L.warm;
+  double* qacc = T.w + L.qacc;
+  const int tid = T.tid;
+  const int G = 2 * nv * nv + nv * nu;  // cost-gradient entries: qpos, qvel, ctrl
+  const double* dq = a.tr.qpos + (size_t)pt * nq;
+  load_state(m, L, T, a.tr, pt, s, a.qfrc_applied, a.xfrc_applied);
+  double wc = 0, costCenter = 0;  // centre warm start (lane j holds entry j) and cost
+  auto set_warm = [&]() {
+    if (tid < nv) warm[tid] = wc;
+    TSYNC();
+  };
+  auto get_centre = [&]() {
+    bw_wait_geq(cflag, 1u, a.fault);
+    wc = tid < nv ? ld_sc1(cwp + tid) : 0.0;
+    costCenter = ld_sc1(cwp + nv);
+  };
+  if (role == 0) {
+    forward_skip(m, L, C, X, T, STAGE_NONE, FD_NITER, 0.0);
+    for (int rep = 1; rep < FD_NWARMUP; rep++) forward_skip(m, L, C, X, T, STAGE_VEL, FD_NITER, 0.0);
+    wc = tid < nv ? warm[tid] : 0.0;
+    costCenter = step_cost(m, a.cost, qpos, qvel, ctrl);
+    if (tid < nv) st_sc1(cwp + tid, wc);
+    if (tid == 0) st_sc1(cwp + nv, costCenter);
+    drain_stores();
+    TSYNC();
+    if (tid == 0) signal_set(cflag, 1u);
+    for (int i = 0; i < nctrl; i++) {
+      const double u0 = ctrl[i];
+      TSYNC();
+      if (tid == 0) {
+        ctrl[i] = u0 + FD_EPS;
+        st_sc1(dr + G + 2 * nv + i, (step_cost(m, a.cost, qpos, qvel, ctrl) - costCenter) / FD_EPS);
+      }
+      set_warm();
+      forward_skip(m, L, C, X, T, STAGE_VEL, FD_NITER, 0.0);
+      const double qp = tid < nv ? qacc[tid] : 0.0;
+      if (tid == 0) ctrl[i] = u0 - FD_EPS;
+      set_warm();
+      forward_skip(m, L, C, X, T, STAGE_VEL, FD_NITER, 0.0);
+      if (tid < nv) st_sc1(dr + 2 * nv * nv + i + tid * nu, (qp - qacc[tid]) / (2 * FD_EPS));
+      if (tid == 0) ctrl[i] = u0;
+      TSYNC();
+    }
+  } else if (role == 1) {
+    const int i0 = idx * a.cv, i1 = i0 + a.cv < nv ? i0 + a.cv : nv;
+    for (int i = i0; i < i1; i++) {
+      const double v0 = qvel[i];
+      TSYNC();
+      if (tid == 0) qvel[i] = v0 + FD_EPS;
+      forward_posvel(m, L, C, X, T, i == i0 ? STAGE_NONE : STAGE_POS);
+      if (i == i0) get_centre();
+      if (tid == 0) st_sc1(dr + G + nv + i, (step_cost(m, a.cost, qpos, qvel, ctrl) - costCenter) / FD_EPS);
+      set_warm();
+      forward_acc(m, L, C, X, T, FD_NITER, 0.0);
+      const double qp = tid < nv ? qacc[tid] : 0.0;
+      if (tid == 0) qvel[i] = v0 - FD_EPS;
+      set_warm();
+      forward_skip(m, L, C, X, T, STAGE_POS, FD_NITER, 0.0);
+      if (tid < nv) st_sc1(dr + nv * nv + i + tid * nv, (qp - qacc[tid]) / (2 * FD_EPS));
+      if (tid == 0) qvel[i] = v0;
+      TSYNC();
+    }
+  } else {
+    const int i = idx;
+    const int jid = m.dof_jntid[i];
+    int quatadr = -1, dofpos = 0;
+    if (m.jnt_type[jid] == JNT_BALL) {
+      quatadr = m.jnt_qposadr[jid];
+      dofpos = i - m.jnt_dofadr[jid];
+    } else if (m.jnt_type[jid] == JNT_FREE && i >= m.jnt_dofadr[jid] + 3) {
+      quatadr = m.jnt_qposadr[jid] + 3;
+      dofpos = i - m.jnt_dofadr[jid] - 3;
+    }
+    // qpos (-)/(+) eps along dof i: quaternion dofs by mju_quatIntegrate (mjderivative.cpp:151-168,186-191)
+    auto perturb = [&](double e) {
+      if (tid == 0) {
+        if (quatadr >= 0) {
+          double angvel[3] = {0, 0, 0}, q[4];
+          angvel[dofpos] = e;
+          ldm<4>(q, qpos + quatadr);
+          quat_integrate(q, angvel, 1);
+          for (int k = 0; k < 4; k++) qpos[quatadr + k] = q[k];
+        } else {
+          qpos[m.jnt_qposadr[jid] + i - m.jnt_dofadr[jid]] += e;
+        }
+      }
+    };
+    perturb(FD_EPS);
+    forward_posvel(m, L, C, X, T, STAGE_NONE);
+    get_centre();
+    if (tid == 0) st_sc1(dr + G + i, (step_cost(m, a.cost, qpos, qvel, ctrl) - costCenter) / FD_EPS);
+    set_warm();
+    forward_acc(m, L, C, X, T, FD_NITER, 0.0);
+    const double qp = tid < nv ? qacc[tid] : 0.0;
+    FOR_T(k, nq) qpos[k] = dq[k];
+    TSYNC();
+    perturb(-FD_EPS);
+    set_warm();
+    forward_skip(m, L, C, X, T, STAGE_NONE, FD_NITER, 0.0);
+    if (tid < nv) st_sc1(dr + i + tid * nv, (qp - qacc[tid]) / (2 * FD_EPS));
+  }
+  drain_stores();
+  TSYNC();
+  if (tid == 0) signal_add(done);
+  STAMP_FLUSH();
+}
+
+template <int NV, int NU, class MD>
+__device__ inline void fd_backward_role(const MD& mg, const FdFused& a, int s) {
+  extern __shared__ double lds[];
+  backward_seed<NV, NU>(mg, mg.nq, mg.nv, mg.nu, a.P, mg.opt_timestep, a.mu, a.deriv, a.Dp, a.tr, a.K, a.k, a.V,
+                        a.v, s, threadIdx.x, lds, a.sync + 4 + (size_t)a.S * a.P, (unsigned)(1 + a.nvt + mg.nv),
+                        a.fault);
+}
+
+__global__ __launch_bounds__(TEAM, FD_WAVES_PER_EU) void k_fd_fused_coop(DevModel mg, WsLayout L, CoopLayout C, CoopAux Xg, FdFused a) {
+  const unsigned t = take_ticket(a.sync);
+  if (t < (unsigned)a.nB) {
+    fd_backward_role<0, 0>(mg, a, (int)t);
+    return;
+  }
+  Team T = make_team(L, C);
+  DevModel m;
+  CoopAux X;
+  stage_model(mg, Xg, L, C, T, m, X);
+  fd_fused_body(m, L, C, X, T, a, t - a.nB);
+}
+
+template <class SM, class SX>
+__global__ __launch_bounds__(TEAM, FD_WAVES_PER_EU) void k_fd_fused_s(DevModel mg, FdFused a) {
+  const unsigned t = take_ticket(a.sync);
+  if (t < (unsigned)a.nB) {
+    fd_backward_role<SM::nv, SM::nu>(mg, a, (int)t);
+    return;
+  }
+  static constexpr WsLayout L = make_layout(SM{}, SX::npair);
+  static constexpr CoopLayout C = make_coop_layout(SM{}, SX::npair);
+  static constexpr SX X{};
+  Team T = make_team(L, C);
+  SM m;
+  stage_model_s(mg, L, C, T, m);
+  fd_fused_body(m, L, C, X, T, a, t - a.nB);
 }
 
 __device__ inline void rollout_body(const auto& m, const auto& L, const auto& C, const auto& X, const Team& T,
@@ -470,7 +694,7 @@ hipError_t launch_fd_centre_coop(const DevModel& m, const WsLayout& L, const Coo
 
 hipError_t launch_fd_cols_coop(const DevModel& m, const WsLayout& L, const CoopLayout& C, const CoopAux& X,
                                TrajDev tr, int npts, int P, const double* qfrc_applied, const double* xfrc_applied,
-                               CostDev cost, const double* warm_c, const double* cost_c, double* deriv,
+                               CostDev cost, const double* warm_c, const double* cost_c, double* deriv, int Ds,
                                hipStream_t st) {
   const int nctrl = m.nu < m.nv ? m.nu : m.nv;
   const long blocks = (long)npts * (nctrl + 2 * m.nv);
@@ -482,7 +706,7 @@ hipError_t launch_fd_cols_coop(const DevModel& m, const WsLayout& L, const CoopL
     e = allow_lds(k_fd_cols_s<stat::SMT, stat::SXT>, lds);                                                      \
     if (e != hipSuccess) return e;                                                                              \
     hipLaunchKernelGGL((k_fd_cols_s<stat::SMT, stat::SXT>), dim3((unsigned)blocks), dim3(TEAM), lds, st, m, tr,  \
-                       P, qfrc_applied, xfrc_applied, cost, warm_c, cost_c, deriv);                             \
+                       P, qfrc_applied, xfrc_applied, cost, warm_c, cost_c, deriv, Ds);                         \
     return hipGetLastError();
   switch (m.static_id) {
     ILQG_STATIC_MODELS(ILQG_CASE)
@@ -493,7 +717,33 @@ hipError_t launch_fd_cols_coop(const DevModel& m, const WsLayout& L, const CoopL
   e = allow_lds(k_fd_cols_coop, coop_lds_bytes(L, C));
   if (e != hipSuccess) return e;
   hipLaunchKernelGGL(k_fd_cols_coop, dim3((unsigned)blocks), dim3(TEAM), coop_lds_bytes(L, C), st, m, L, C, X, tr, P,
-                     qfrc_applied, xfrc_applied, cost, warm_c, cost_c, deriv);
+                     qfrc_applied, xfrc_applied, cost, warm_c, cost_c, deriv, Ds);
+  return hipGetLastError();
+}
+
+hipError_t launch_fd_fused_coop(const DevModel& m, const WsLayout& L, const CoopLayout& C, const CoopAux& X,
+                                const FdFused& a, hipStream_t st) {
+  const long items = (long)a.S * a.P * (1 + a.nvt + m.nv);
+  const long blocks = items + a.nB;
+  if (items <= 0) return hipSuccess;
+  size_t lds = coop_lds_bytes(L, C);
+  if (a.nB > 0) lds = std::max(lds, backward_lds_bytes(m.nv, m.nu));
+  hipError_t e;
+#define ILQG_CASE(id, SMT, SXT)                                                                                 \
+  case id:                                                                                                      \
+    e = allow_lds(k_fd_fused_s<stat::SMT, stat::SXT>, lds);                                                     \
+    if (e != hipSuccess) return e;                                                                              \
+    hipLaunchKernelGGL((k_fd_fused_s<stat::SMT, stat::SXT>), dim3((unsigned)blocks), dim3(TEAM), lds, st, m, a); \
+    return hipGetLastError();
+  switch (m.static_id) {
+    ILQG_STATIC_MODELS(ILQG_CASE)
+    default:
+      break;
+  }
+#undef ILQG_CASE
+  e = allow_lds(k_fd_fused_coop, lds);
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(k_fd_fused_coop, dim3((unsigned)blocks), dim3(TEAM), lds, st, m, L, C, X, a);
   return hipGetLastError();
 }
 

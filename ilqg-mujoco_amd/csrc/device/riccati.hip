@@ -16,9 +16,6 @@
 namespace ilqg {
 namespace {
 
-constexpr int BW_THREADS = 64;  // one wavefront: its barriers compile to nothing
-constexpr int BW_PF = 8;        // prefetch registers per lane: D <= 512
-
 #ifdef ILQG_STAMPS
 __device__ unsigned long long g_bstamp_acc[16];
 __device__ unsigned long long g_bstamp_cnt[16];
@@ -39,337 +36,28 @@ __device__ unsigned long long g_bstamp_cnt[16];
   } while (0)
 #endif
 
-// Eigen-style LDLT with symmetric pivoting (oracle ora_ldlt_factor); lane 0.
-// temp: n doubles of LDS scratch (a private array would live in scratch memory)
-__device__ void ldlt_factor(int n, double* mat, int* transp, double* temp) {
-  for (int k = 0; k < n; k++) {
-    int big = k;
-    double bigv = fabs(mat[k + k * n]);
-    int rs = n - k - 1;
-    for (int i = k + 1; i < n; i++)
-      if (fabs(mat[i + i * n]) > bigv) { bigv = fabs(mat[i + i * n]); big = i; }
-    transp[k] = big;
-    if (k != big) {
-      int s = n - big - 1;
-      double t;
-      for (int j = 0; j < k; j++) { t = mat[k + j * n]; mat[k + j * n] = mat[big + j * n]; mat[big + j * n] = t; }
-      for (int i = 0; i < s; i++) {
-        t = mat[(big + 1 + i) + k * n];
-        mat[(big + 1 + i) + k * n] = mat[(big + 1 + i) + big * n];
-        mat[(big + 1 + i) + big * n] = t;
-      }
-      t = mat[k + k * n]; mat[k + k * n] = mat[big + big * n]; mat[big + big * n] = t;
-      for (int i = k + 1; i < big; i++) { t = mat[i + k * n]; mat[i + k * n] = mat[big + i * n]; mat[big + i * n] = t; }
-    }
-    if (k > 0) {
-      double s = 0;
-      for (int j = 0; j < k; j++) temp[j] = mat[j + j * n] * mat[k + j * n];
-      for (int j = 0; j < k; j++) s += mat[k + j * n] * temp[j];
-      mat[k + k * n] -= s;
-      for (int i = k + 1; i < n; i++) {
-        double si = 0;
-        for (int j = 0; j < k; j++) si += mat[i + j * n] * temp[j];
-        mat[i + k * n] -= si;
-      }
-    }
-    if (k == 0 && !(fabs(mat[0]) > 0)) {
-      for (int j = 0; j < n; j++) transp[j] = j;
-      return;
-    }
-    if (rs > 0 && fabs(mat[k + k * n]) > 0)
-      for (int i = k + 1; i < n; i++) mat[i + k * n] /= mat[k + k * n];
-  }
-}
-__device__ void ldlt_solve(int n, const double* Lm, const int* transp, double* x) {
-  const double tol = 2.2250738585072014e-308;
-  for (int k = 0; k < n; k++) { double t = x[k]; x[k] = x[transp[k]]; x[transp[k]] = t; }
-  for (int i = 0; i < n; i++)
-    for (int j = 0; j < i; j++) x[i] -= Lm[i + j * n] * x[j];
-  for (int i = 0; i < n; i++) {
-    if (fabs(Lm[i + i * n]) > tol) x[i] /= Lm[i + i * n];
-    else x[i] = 0;
-  }
-  for (int i = n - 1; i >= 0; i--)
-    for (int j = i + 1; j < n; j++) x[i] -= Lm[j + i * n] * x[j];
-  for (int k = n - 1; k >= 0; k--) { double t = x[k]; x[k] = x[transp[k]]; x[transp[k]] = t; }
-}
+}  // namespace
+}  // namespace ilqg
 
-// Three independent fixed-order dot products per lane (ILP 3): each output
-// keeps the oracle's summation order, the three chains overlap in the pipe.
-#define ILP3_BEGIN(n)                                    \
-  for (int e0 = tid; e0 < (n); e0 += 3 * BW_THREADS) {   \
-    const int e1 = e0 + BW_THREADS, e2 = e0 + 2 * BW_THREADS; \
-    const bool h1 = e1 < (n), h2 = e2 < (n);             \
-    const int f1 = h1 ? e1 : e0, f2 = h2 ? e2 : e0;
+#include "riccati.h"
+
+namespace ilqg {
+namespace {
 
 template <int NV_, int NU_>
 __global__ __launch_bounds__(BW_THREADS) void k_backward(DevModel m, int nq, int nv_rt, int nu_rt, int P, double dt,
-                                                         double mu, const double* deriv, TrajDev tr, double* Kg,
-                                                         double* kg, double* Vg, double* vg) {
-  const int nv = NV_ > 0 ? NV_ : nv_rt;
-  const int nu = NU_ > 0 ? NU_ : nu_rt;
-  const int s = blockIdx.x, tid = threadIdx.x;
-  const int nx = 2 * nv, D = nv * (2 * nv + nu) + 2 * nv + nu;
-  // padded leading dimension of the nx-row matrices (unpadded for large nx,
-  // where LDS capacity binds)
-  const int LX = nx <= 32 ? nx + 1 : nx;
-  const bool pref = D <= BW_PF * BW_THREADS;  // FD record prefetched into LDS
+                                                         double mu, const double* deriv, int Ds, TrajDev tr,
+                                                         double* Kg, double* kg, double* Vg, double* vg) {
   extern __shared__ double sh[];
-  // buffers are reused once dead: V holds V_new (V is read only by stage 1),
-  // A holds T4 (A is last read in stage 5)
-  double* V = sh;                 // nx x nx, ld LX; V_new from stage 7
-  double* Vs = V + nx * LX;
-  double* A = Vs + nx * LX;       // T4 from stage 6
-  double* ABK = A + nx * LX;
-  double* B = ABK + nx * LX;      // nx x nu, ld LX
-  double* T6 = B + nu * LX;       // nx x nu, ld LX
-  double* T1 = T6 + nu * LX;      // nu x nx, ld nu
-  double* T3 = T1 + nu * nx;
-  double* Kl = T3 + nu * nx;
-  double* Mm = Kl + nu * nx;      // nu x nu
-  double* v = Mm + nu * nu;
-  double* c = v + nx;
-  double* w = c + nx;
-  double* y = w + nx;
-  double* z = y + nx;
-  double* vn = z + nx;
-  double* q = vn + nx;
-  double* kl = q + nx;
-  double* kR = kl + nu;
-  double* col = kR + nu;
-  double* r = col + nu;
-  double* dl = r + nu;  // FD record of the current step (prefetched), D doubles when pref
-  int* trn = (int*)(dl + (pref ? D : 0));
-  double* T4 = A;
-  double* Vn = V;
-#ifdef ILQG_STAMPS
-  unsigned long long bst_prev = 0;
-#endif
-
-  // initV at the terminal point dArray[0], inc/ilqr.h:100-107
-  {
-    const double* q0 = deriv + ((size_t)s * P + 0) * D + 2 * nv * nv + nv * nu;
-    for (int i = tid; i < nx; i += BW_THREADS) v[i] = q0[i];
-    const double* d1 = deriv + ((size_t)s * P + (P > 1 ? 1 : 0)) * D;
-    if (pref)
-      for (int i = tid; i < D; i += BW_THREADS) dl[i] = d1[i];
-    __syncthreads();
-    for (int e = tid; e < nx * nx; e += BW_THREADS) {
-      int i = e % nx, j = e / nx;
-      V[i + j * LX] = v[i] * v[j];
-    }
-    __syncthreads();
-  }
-  BSTAMP(-1);
-  for (int n = 1; n < P; n++) {
-    const size_t pc = (size_t)s * P + n, pp = pc - 1;
-    // prefetch the next step's FD record; consumed at the end of this step
-    double pf[BW_PF];
-    if (pref && n + 1 < P) {
-      const double* dn1 = deriv + (pc + 1) * D;
-#pragma unroll
-      for (int t = 0; t < BW_PF; t++) {
-        int i = tid + t * BW_THREADS;
-        pf[t] = i < D ? dn1[i] : 0.0;
-      }
-    }
-    const double* dn = pref ? dl : deriv + pc * D;
-    // stage 1: symmetrise V, assemble A/B (differentiator.h:66-71,89-92), q, r, c
-    for (int e = tid; e < nx * nx; e += BW_THREADS) {
-      int i = e % nx, j = e / nx;
-      Vs[i + j * LX] = (V[i + j * LX] + V[j + i * LX]) / 2;
-      double val;
-      if (i < nv && j < nv) val = (i == j) ? 1 : 0;
-      else if (i < nv) val = (i == j - nv) ? dt : 0;
-      else if (j < nv) val = dn[(i - nv) + j * nv] * dt;
-      else val = ((i - nv) == (j - nv) ? 1 : 0) + dn[nv * nv + (i - nv) + (j - nv) * nv] * dt;
-      A[i + j * LX] = val;
-    }
-    for (int e = tid; e < nx * nu; e += BW_THREADS) {
-      int i = e % nx, j = e / nx;
-      B[i + j * LX] = (i < nv) ? 0 : dn[2 * nv * nv + (i - nv) + j * nv] * dt;
-    }
-    for (int i = tid; i < nx; i += BW_THREADS) {
-      q[i] = dn[2 * nv * nv + nv * nu + i];
-      // c = x*_{n-1} (-) x*_n (inc/ilqr.h:154-157; tangent space for quaternion joints)
-      if (i < nv && nq != nv) {
-        c[i] = dev::state_diff_dof(m, i, tr.qpos + pp * nq, tr.qpos + pc * nq);
-      } else {
-        double xp = i < nv ? tr.qpos[pp * nq + i] : tr.qvel[pp * nv + i - nv];
-        double xc = i < nv ? tr.qpos[pc * nq + i] : tr.qvel[pc * nv + i - nv];
-        c[i] = xp - xc;
-      }
-    }
-    for (int a = tid; a < nu; a += BW_THREADS) r[a] = dn[2 * nv * nv + nv * nu + nx + a];
-    __syncthreads();
-    for (int i = tid; i < nx; i += BW_THREADS) Vs[i + i * LX] += mu;
-    __syncthreads();
-    BSTAMP(0);
-    // stage 2: T1 = B'V
-    ILP3_BEGIN(nu * nx)
-      double s0 = 0, s1 = 0, s2 = 0;
-      const int a0 = e0 % nu, j0 = e0 / nu, a1 = f1 % nu, j1 = f1 / nu, a2 = f2 % nu, j2 = f2 / nu;
-      for (int kk = 0; kk < nx; kk++) {
-        s0 += B[kk + a0 * LX] * Vs[kk + j0 * LX];
-        s1 += B[kk + a1 * LX] * Vs[kk + j1 * LX];
-        s2 += B[kk + a2 * LX] * Vs[kk + j2 * LX];
-      }
-      T1[e0] = s0;
-      if (h1) T1[e1] = s1;
-      if (h2) T1[e2] = s2;
-    }
-    __syncthreads();
-    BSTAMP(1);
-    // stage 3: Mm = -2 T1 B - 2R ; T3 = T1 A ; w = v + 2 V c
-    for (int e = tid; e < nu * nu; e += BW_THREADS) {
-      int a = e % nu, b = e / nu;
-      double sm = 0;
-      for (int kk = 0; kk < nx; kk++) sm += T1[a + kk * nu] * B[kk + b * LX];
-      Mm[e] = -2 * sm - 2 * (r[a] * r[b]);
-    }
-    ILP3_BEGIN(nu * nx)
-      double s0 = 0, s1 = 0, s2 = 0;
-      const int a0 = e0 % nu, j0 = e0 / nu, a1 = f1 % nu, j1 = f1 / nu, a2 = f2 % nu, j2 = f2 / nu;
-      for (int kk = 0; kk < nx; kk++) {
-        s0 += T1[a0 + kk * nu] * A[kk + j0 * LX];
-        s1 += T1[a1 + kk * nu] * A[kk + j1 * LX];
-        s2 += T1[a2 + kk * nu] * A[kk + j2 * LX];
-      }
-      T3[e0] = s0;
-      if (h1) T3[e1] = s1;
-      if (h2) T3[e2] = s2;
-    }
-    for (int i = tid; i < nx; i += BW_THREADS) {
-      double sm = 0;
-      for (int j = 0; j < nx; j++) sm += Vs[i + j * LX] * c[j];
-      w[i] = v[i] + 2 * sm;
-    }
-    __syncthreads();
-    if (tid == 0) ldlt_factor(nu, Mm, trn, y);  // y is free until stage 5
-    for (int a = tid; a < nu; a += BW_THREADS) {
-      double sm = 0;
-      for (int kk = 0; kk < nx; kk++) sm += B[kk + a * LX] * w[kk];
-      col[a] = sm + r[a];
-    }
-    __syncthreads();
-    BSTAMP(2);
-    // stage 4: K = ldlt.solve(2 T3) column-parallel; k = ldlt.solve(B'w + r), in place in LDS
-    for (int j = tid; j < nx + 1; j += BW_THREADS) {
-      double* x = j < nx ? Kl + j * nu : kl;
-      if (j < nx)
-        for (int a = 0; a < nu; a++) x[a] = 2 * T3[a + j * nu];
-      else
-        for (int a = 0; a < nu; a++) x[a] = col[a];
-      ldlt_solve(nu, Mm, trn, x);
-    }
-    __syncthreads();
-    BSTAMP(3);
-    // stage 5: ABK = A + B K ; T6 = K'R ; y = Bk + c ; kR = k'R
-    for (int e = tid; e < nx * nx; e += BW_THREADS) {
-      int i = e % nx, j = e / nx;
-      double sm = 0;
-      for (int a = 0; a < nu; a++) sm += B[i + a * LX] * Kl[a + j * nu];
-      ABK[i + j * LX] = A[i + j * LX] + sm;
-    }
-    for (int e = tid; e < nx * nu; e += BW_THREADS) {
-      int i = e % nx, b = e / nx;
-      double sm = 0;
-      for (int a = 0; a < nu; a++) sm += Kl[a + i * nu] * (r[a] * r[b]);
-      T6[i + b * LX] = sm;
-    }
-    for (int i = tid; i < nx; i += BW_THREADS) {
-      double sm = 0;
-      for (int a = 0; a < nu; a++) sm += B[i + a * LX] * kl[a];
-      y[i] = sm + c[i];
-    }
-    for (int b = tid; b < nu; b += BW_THREADS) {
-      double sm = 0;
-      for (int a = 0; a < nu; a++) sm += kl[a] * (r[a] * r[b]);
-      kR[b] = sm;
-    }
-    __syncthreads();
-    BSTAMP(4);
-    // stage 6: T4 = ABK' V
-    ILP3_BEGIN(nx * nx)
-      double s0 = 0, s1 = 0, s2 = 0;
-      const int i0 = e0 % nx, j0 = e0 / nx, i1 = f1 % nx, j1 = f1 / nx, i2 = f2 % nx, j2 = f2 / nx;
-      for (int kk = 0; kk < nx; kk++) {
-        s0 += ABK[kk + i0 * LX] * Vs[kk + j0 * LX];
-        s1 += ABK[kk + i1 * LX] * Vs[kk + j1 * LX];
-        s2 += ABK[kk + i2 * LX] * Vs[kk + j2 * LX];
-      }
-      T4[i0 + j0 * LX] = s0;
-      if (h1) T4[i1 + j1 * LX] = s1;
-      if (h2) T4[i2 + j2 * LX] = s2;
-    }
-    __syncthreads();
-    BSTAMP(5);
-    // stage 7: V_new = (T4 ABK + Q) + T6 K
-    ILP3_BEGIN(nx * nx)
-      double a0s = 0, a1s = 0, a2s = 0, b0s = 0, b1s = 0, b2s = 0;
-      const int i0 = e0 % nx, j0 = e0 / nx, i1 = f1 % nx, j1 = f1 / nx, i2 = f2 % nx, j2 = f2 / nx;
-      for (int kk = 0; kk < nx; kk++) {
-        a0s += T4[i0 + kk * LX] * ABK[kk + j0 * LX];
-        a1s += T4[i1 + kk * LX] * ABK[kk + j1 * LX];
-        a2s += T4[i2 + kk * LX] * ABK[kk + j2 * LX];
-      }
-      for (int b = 0; b < nu; b++) {
-        b0s += T6[i0 + b * LX] * Kl[b + j0 * nu];
-        b1s += T6[i1 + b * LX] * Kl[b + j1 * nu];
-        b2s += T6[i2 + b * LX] * Kl[b + j2 * nu];
-      }
-      Vn[i0 + j0 * LX] = (a0s + q[i0] * q[j0]) + b0s;
-      if (h1) Vn[i1 + j1 * LX] = (a1s + q[i1] * q[j1]) + b1s;
-      if (h2) Vn[i2 + j2 * LX] = (a2s + q[i2] * q[j2]) + b2s;
-    }
-    __syncthreads();
-    BSTAMP(6);
-    // stage 8: z = (2y)' V_new ; v_new (reads the NEW V, Q14)
-    for (int j = tid; j < nx; j += BW_THREADS) {
-      double sm = 0;
-      for (int i = 0; i < nx; i++) sm += (2 * y[i]) * Vn[i + j * LX];
-      z[j] = sm;
-    }
-    __syncthreads();
-    for (int j = tid; j < nx; j += BW_THREADS) {
-      double ta = 0, tb = 0, td = 0;
-      for (int i = 0; i < nx; i++) {
-        ta += z[i] * ABK[i + j * LX];
-        tb += v[i] * ABK[i + j * LX];
-      }
-      for (int b = 0; b < nu; b++) td += (2 * kR[b]) * Kl[b + j * nu];
-      vn[j] = ((ta + tb) + q[j]) + td;
-    }
-    BSTAMP(7);
-    // gains out
-    for (int e = tid; e < nu * nx; e += BW_THREADS) Kg[pc * nu * nx + e] = Kl[e];
-    for (int a = tid; a < nu; a += BW_THREADS) kg[pc * nu + a] = kl[a];
-    __syncthreads();
-    for (int i = tid; i < nx; i += BW_THREADS) v[i] = vn[i];  // V already holds V_new
-    if (pref && n + 1 < P) {
-#pragma unroll
-      for (int t = 0; t < BW_PF; t++) {
-        int i = tid + t * BW_THREADS;
-        if (i < D) dl[i] = pf[t];
-      }
-    }
-    __syncthreads();
-    BSTAMP(8);
-  }
-  if (Vg)
-    for (int e = tid; e < nx * nx; e += BW_THREADS) {
-      int i = e % nx, j = e / nx;
-      Vg[(size_t)s * nx * nx + e] = V[i + j * LX];
-    }
-  if (vg)
-    for (int i = tid; i < nx; i += BW_THREADS) vg[(size_t)s * nx + i] = v[i];
+  backward_seed<NV_, NU_>(m, nq, nv_rt, nu_rt, P, dt, mu, deriv, Ds, tr, Kg, kg, Vg, vg, blockIdx.x, threadIdx.x, sh,
+                          nullptr, 0u, nullptr);
 }
 
 template <int NV, int NU>
-void launch_t(const DevModel& m, int S, int P, double mu, const double* deriv, TrajDev tr, double* K, double* k,
-              double* V, double* v, size_t lds, hipStream_t st) {
+void launch_t(const DevModel& m, int S, int P, double mu, const double* deriv, int Ds, TrajDev tr, double* K,
+              double* k, double* V, double* v, size_t lds, hipStream_t st) {
   hipLaunchKernelGGL((k_backward<NV, NU>), dim3(S), dim3(BW_THREADS), lds, st, m, m.nq, m.nv, m.nu, P,
-                     m.opt_timestep, mu, deriv, tr, K, k, V, v);
+                     m.opt_timestep, mu, deriv, Ds, tr, K, k, V, v);
 }
 
 }  // namespace
@@ -382,8 +70,8 @@ size_t backward_lds_bytes(int nv, int nu) {
   return nd * sizeof(double) + (size_t)nu * sizeof(int) + 16;
 }
 
-hipError_t launch_backward(const DevModel& m, int S, int P, double mu, const double* deriv, TrajDev tr, double* K,
-                           double* k, double* V, double* v, hipStream_t st) {
+hipError_t launch_backward(const DevModel& m, int S, int P, double mu, const double* deriv, int Ds, TrajDev tr,
+                           double* K, double* k, double* V, double* v, hipStream_t st) {
   if (m.nu > 32) return hipErrorInvalidValue;  // LDLT scratch bound
   const size_t lds = backward_lds_bytes(m.nv, m.nu);
   if (lds > 160 * 1024) return hipErrorInvalidValue;
@@ -394,9 +82,9 @@ hipError_t launch_backward(const DevModel& m, int S, int P, double mu, const dou
     hipError_t e = hipFuncSetAttribute(kf, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     if (e != hipSuccess) return e;
   }
-  if (m.nv == 6 && m.nu == 3) launch_t<6, 3>(m, S, P, mu, deriv, tr, K, k, V, v, lds, st);
-  else if (m.nv == 2 && m.nu == 1) launch_t<2, 1>(m, S, P, mu, deriv, tr, K, k, V, v, lds, st);
-  else launch_t<0, 0>(m, S, P, mu, deriv, tr, K, k, V, v, lds, st);
+  if (m.nv == 6 && m.nu == 3) launch_t<6, 3>(m, S, P, mu, deriv, Ds, tr, K, k, V, v, lds, st);
+  else if (m.nv == 2 && m.nu == 1) launch_t<2, 1>(m, S, P, mu, deriv, Ds, tr, K, k, V, v, lds, st);
+  else launch_t<0, 0>(m, S, P, mu, deriv, Ds, tr, K, k, V, v, lds, st);
   return hipGetLastError();
 }
 

@@ -63,7 +63,7 @@ EXPORTS = [
     "ilqg_solver_stream", "ilqg_solver_device_costs", "ilqg_solver_set_stream", "ilqg_solver_set_timing",
     "ilqg_solver_get_timing",
 ]
-KERNELS = ("rollout", "select", "fd_centre", "fd_cols", "backward")
+KERNELS = ("rollout", "select", "fd_centre", "fd_cols", "backward", "fd_backward")
 
 _lib = None
 
@@ -384,8 +384,8 @@ class ILQR:
 
     def timing(self):
         """{kernel: (total_ms, launches)} since the last call (HIP events on the launch stream)"""
-        ms = (ctypes.c_double * 5)()
-        n = (ctypes.c_int * 5)()
+        ms = (ctypes.c_double * len(KERNELS))()
+        n = (ctypes.c_int * len(KERNELS))()
         _check(lib().ilqg_solver_get_timing(self._h, ms, n), "get_timing")
         return {k: (ms[i], n[i]) for i, k in enumerate(KERNELS)}
 

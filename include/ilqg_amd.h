@@ -140,8 +140,10 @@ void* ilqg_solver_stream(ilqg_solver* s); /* hipStream_t */
    e.g. torch's current stream) instead of the solver's own; NULL restores it */
 int ilqg_solver_set_stream(ilqg_solver* s, void* stream);
 /* per-kernel HIP-event timing of the hot path, recorded on the launch stream:
-   index 0 rollout, 1 select, 2 fd_centre, 3 fd_cols, 4 backward */
-#define ILQG_NKERNEL 5
+   index 0 rollout, 1 select, 2 fd_centre, 3 fd_cols (or the fused sweep run
+   alone), 4 backward, 5 fd_backward (the fused sweep with the backward pass
+   streamed behind it: ilqg_iterate on cooperative models) */
+#define ILQG_NKERNEL 6
 int ilqg_solver_set_timing(ilqg_solver* s, int enable);
 /* synchronises; returns summed device ms and launch counts per kernel, then resets */
 int ilqg_solver_get_timing(ilqg_solver* s, double* ms, int* launches);

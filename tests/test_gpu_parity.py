@@ -306,3 +306,37 @@ def test_humanoid_iterate_tangent_space(ia, ora):
     V, v = g.value()
     exact(V[0], oa["V"], "V")
     exact(v[0], oa["v"], "v")
+
+
+@pytest.mark.parametrize("env", [{"ILQG_FUSED": "0"}, {"ILQG_FD_LAG": "0"}, {"ILQG_FD_LAG": "1"},
+                                 {"ILQG_FD_LAG": "7", "ILQG_FD_CV": "1"}, {"ILQG_FD_CV": "6"}])
+def test_fused_sweep_schedules(ia, ora, env, monkeypatch):
+    """The fused FD sweep + streamed backward pass (k_fd_fused_s): every hand-off
+    schedule (centre lag, qvel columns per team) and the two-kernel sweep give the
+    oracle's iterate bit for bit (seeds x points x columns vary the ticket order)"""
+    import workloads
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
+    m, om = setup(ia, ora, "hopper", ia.HOPPER_COST)
+    S, H = 3, 40
+    dmain = workloads.hopper_dmain(m, S, sigma=0.01)
+    g = ia.ILQR(m, dmain, H, ia.HOPPER_COST)
+    g.iterate()
+    g.iterate()
+    g.synchronize()
+    gt, (K, k), D = g.traj(), g.gains(), g.deriv()
+    V, v = g.value()
+    P = H + 1
+    for s in range(S):
+        il = _oracle_ilqr(ora, om, _state_dict(dmain, s), H, "ora_cost_desc_fn", 2)
+        oa = il.arrays()
+        exact(gt.qpos[s * P:(s + 1) * P], il.traj()["qpos"], f"seed {s} qpos")
+        exact(K[s], oa["K"], f"seed {s} K")
+        exact(k[s], oa["k"], f"seed {s} k")
+        exact(D[s], oa["deriv"], f"seed {s} deriv")
+        exact(V[s], oa["V"], f"seed {s} V")
+        exact(v[s], oa["v"], f"seed {s} v")
+    # the sweep alone (no backward roles) writes the same records
+    g.fd_sweep()
+    g.synchronize()
+    exact(g.deriv(), D, "fd_sweep alone vs iterate's fused records")
