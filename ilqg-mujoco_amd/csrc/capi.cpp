@@ -246,7 +246,7 @@ struct ilqg_solver {
   int S = 0, A = 0, P = 0, D = 0, nx = 0, ncol = 0;
   // FD records at a padded stride Dp (whole 128-byte lines: handoff.h); the
   // fused sweep (fd_fused) also streams the backward pass behind the FD teams
-  int Dp = 0, WCp = 0, lag = 0, nvt = 0, cv = 0;
+  int Dp = 0, WCp = 0, lag = 0, nvt = 0, cv = 0, nut = 0;
   bool fused = false;
   hipStream_t stream = nullptr;
   DevBuf traj[5], cand[5], dinit[5];
@@ -256,6 +256,27 @@ struct ilqg_solver {
   std::vector<double> host_alphas;
   bool initialized = false;
   hipStream_t own_stream = nullptr;
+  // seed groups (ilqg_solver_set_groups): contiguous seed ranges; each group's
+  // rollout runs on its own stream (rs) so one group's latency-bound rollout
+  // overlaps another group's FD sweep; the sweeps run on fs (one stream shared
+  // by the groups -- they take turns -- unless ILQG_GROUP_TOKEN=0).  Optional
+  // CU masks (ILQG_ROLL_CUS) keep the rollout and sweep streams on disjoint CUs:
+  // without them a running sweep refills every CU slot it frees and a rollout
+  // launched behind it cannot start until the sweep has drained.
+  // (A split variant -- the Riccati recursion as a launch of its own on a third
+  // stream, streaming a concurrent sweep launch's records -- deadlocked when the
+  // two streams shared a hardware queue: HIP does not guarantee that two
+  // launches run concurrently, so every producer/consumer pair stays inside one
+  // ticketed launch.)
+  struct Group {
+    int s0 = 0, ns = 0;
+    hipStream_t rs = nullptr, fs = nullptr;
+    hipEvent_t costs = nullptr, fd = nullptr;
+    unsigned* sync = nullptr;
+  };
+  std::vector<Group> groups;  // empty: one group, on `stream`
+  hipStream_t fstream = nullptr;  // shared sweep stream
+  hipEvent_t ev_start = nullptr;
   bool timing = false;
   std::vector<std::pair<hipEvent_t, hipEvent_t>> ev[ILQG_NKERNEL];
   std::vector<hipEvent_t> event_pool;
@@ -272,15 +293,16 @@ struct ilqg_solver {
   }
   // record an event pair around a launch when timing is on
   template <typename F>
-  hipError_t timed(int kind, F&& launch) {
+  hipError_t timed(int kind, F&& launch, hipStream_t st = nullptr) {
     if (!timing) return launch();
+    if (!st) st = stream;
     hipEvent_t a = get_event(), b = get_event();
     if (!a || !b) return hipErrorOutOfMemory;
-    hipError_t e = hipEventRecord(a, stream);
+    hipError_t e = hipEventRecord(a, st);
     if (e != hipSuccess) return e;
     e = launch();
     if (e != hipSuccess) return e;
-    e = hipEventRecord(b, stream);
+    e = hipEventRecord(b, st);
     ev[kind].emplace_back(a, b);
     return e;
   }
@@ -295,7 +317,30 @@ struct ilqg_solver {
                    c + 3 * nq + 3 * nv, c + 3 * nq + 3 * nv + nu, c + 3 * nq + 3 * nv + 2 * nu};
   }
   WsDev ws() const { return WsDev{wsd.as<double>(), wsi.as<int>(), nlanes}; }
+  void free_groups() {
+    for (auto& g : groups) {
+      if (g.rs) (void)hipStreamDestroy(g.rs);
+      if (g.fs && g.fs != fstream) (void)hipStreamDestroy(g.fs);
+      for (hipEvent_t e : {g.costs, g.fd})
+        if (e) (void)hipEventDestroy(e);
+    }
+    groups.clear();
+    if (fstream) (void)hipStreamDestroy(fstream);
+    fstream = nullptr;
+  }
+  // every stream the solver launches on
+  hipError_t sync_all() {
+    hipError_t e = hipStreamSynchronize(stream);
+    for (auto& g : groups) {
+      if (e == hipSuccess) e = hipStreamSynchronize(g.rs);
+      if (e == hipSuccess) e = hipStreamSynchronize(g.fs);
+    }
+    return e;
+  }
   ~ilqg_solver() {
+    (void)sync_all();
+    free_groups();
+    if (ev_start) (void)hipEventDestroy(ev_start);
     for (auto& v : ev)
       for (auto& p : v) {
         (void)hipEventDestroy(p.first);
@@ -405,7 +450,9 @@ static int round16(int n) { return (n + 15) / 16 * 16; }
 // qvel columns per V team, and the lag (points) between a centre team and its column teams.
 // Default lag = P: every centre team is issued first, so column teams never wait on
 // a centre still running (hopper bench, MI355X: lag 8 -> 12.9 ms, 64 -> 11.5, P -> 10.6)
-static int fd_cv() { return std::max(1, getenv_int("ILQG_FD_CV", 3)); }
+static int fd_cv() { return std::max(1, getenv_int("ILQG_FD_CV", 1)); }
+// ctrl columns on teams of their own (1) or on the centre team (0)
+static int fd_nut(const HostModel& h) { return getenv_int("ILQG_FD_USPLIT", 1) ? std::min(h.nu, h.nv) : 0; }
 static int fd_lag(int S, int P) {
   (void)S;
   const int l = getenv_int("ILQG_FD_LAG", P);
@@ -553,7 +600,7 @@ int ilqg_fd_batch(const ilqg_model* mc, int n, const double* qpos, const double*
     HIPCHK(hipMemsetAsync(fl.p, 0, 16, m->stream));
     HIPCHK(hipMemsetAsync(sy.p, 0, sync_bytes(n), m->stream));
     FdFused a{};
-    a.tr = st; a.S = n; a.P = 1; a.nB = 0; a.lag = fd_lag(n, 1); a.cv = cv; a.nvt = (h.nv + cv - 1) / cv;
+    a.tr = st; a.S = n; a.P = 1; a.nB = 0; a.lag = fd_lag(n, 1); a.cv = cv; a.nvt = (h.nv + cv - 1) / cv; a.nut = fd_nut(h);
     a.Dp = Dp; a.WCp = WCp; a.qfrc_applied = s.qa.as<double>(); a.xfrc_applied = s.xf.as<double>(); a.cost = cd;
     a.cw = cw.as<double>(); a.deriv = outp.as<double>(); a.sync = sy.as<unsigned>(); a.fault = fl.as<unsigned>();
     HIPCHK(launch_fd_fused_coop(m->dm, m->Lc, m->C, m->X, a, m->stream));
@@ -604,6 +651,7 @@ int ilqg_solver_create(const ilqg_model* mc, const ilqg_solver_opts* o, const il
   s->fused = fused_ok(m);
   s->cv = fd_cv();
   s->nvt = (h.nv + s->cv - 1) / s->cv;
+  s->nut = fd_nut(h);
   s->lag = fd_lag(o->nseed, o->horizon + 1);
   s->host_alphas.assign(o->nalpha, 1.0);
   if (o->alphas) std::copy(o->alphas, o->alphas + o->nalpha, s->host_alphas.begin());
@@ -630,7 +678,7 @@ int ilqg_solver_create(const ilqg_model* mc, const ilqg_solver_opts* o, const il
   ALLOC(s->deriv, S * P * s->Dp * 8);
   if (s->fused) {
     ALLOC(s->cw, S * P * s->WCp * 8);
-    ALLOC(s->sync, sync_bytes(S * P));
+    ALLOC(s->sync, sync_bytes(S * P) + S * 32);  // + per-seed-group header and padding
   }
   ALLOC(s->fault, 16);
   ALLOC(s->warm_c, S * P * h.nv * 8);
@@ -667,10 +715,11 @@ static int upload_state(ilqg_solver* s, DevBuf* dst, size_t npts, const double* 
   const HostModel& h = s->model->host;
   const double* src[5] = {time, qpos, qvel, warm, ctrl};
   const size_t fld[5] = {1, (size_t)h.nq, (size_t)h.nv, (size_t)h.nv, (size_t)h.nu};
+  HIPCHK(s->sync_all());  // no group still reading the buffers being replaced
   for (int f = 0; f < 5; f++)
     if (src[f]) HIPCHK(hipMemcpyAsync(dst[f].p, src[f], npts * fld[f] * 8, hipMemcpyHostToDevice, s->stream));
     else HIPCHK(hipMemsetAsync(dst[f].p, 0, npts * fld[f] * 8, s->stream));
-  HIPCHK(hipStreamSynchronize(s->stream));
+  HIPCHK(s->sync_all());
   return ILQG_OK;
 }
 
@@ -695,7 +744,7 @@ int ilqg_solver_init(ilqg_solver* s, const double* time, const double* qpos, con
     HIPCHK(launch_rollout(m->dm, m->L, s->ws(), s->S, 1, s->P, nom, nom, 0, s->K.as<double>(), s->k.as<double>(),
                           nullptr, di, s->qfrc_applied.as<double>(), s->xfrc_applied.as<double>(), 1, s->cview(),
                           nullptr, s->stream));
-  HIPCHK(hipStreamSynchronize(s->stream));
+  HIPCHK(s->sync_all());
   // setDInit(dmain) as the MPC driver does before iterating (src/inverted_pendulum/inverted_pendulum.cpp:21)
   s->initialized = true;
   return upload_state(s, s->dinit, s->S, time, qpos, qvel, warm, ctrl);
@@ -719,7 +768,7 @@ int ilqg_solver_get_traj(ilqg_solver* s, double* time, double* qpos, double* qve
   const HostModel& h = s->model->host;
   double* dst[5] = {time, qpos, qvel, warm, ctrl};
   const size_t fld[5] = {1, (size_t)h.nq, (size_t)h.nv, (size_t)h.nv, (size_t)h.nu};
-  HIPCHK(hipStreamSynchronize(s->stream));
+  HIPCHK(s->sync_all());
   for (int f = 0; f < 5; f++)
     if (dst[f]) HIPCHK(hipMemcpy(dst[f], s->traj[f].p, (size_t)s->S * s->P * fld[f] * 8, hipMemcpyDeviceToHost));
   return ILQG_OK;
@@ -727,7 +776,7 @@ int ilqg_solver_get_traj(ilqg_solver* s, double* time, double* qpos, double* qve
 
 int ilqg_solver_set_gains(ilqg_solver* s, const double* K, const double* k) {
   if (!s) return fail(ILQG_ERR_ARG, "null solver");
-  HIPCHK(hipStreamSynchronize(s->stream));
+  HIPCHK(s->sync_all());
   if (K) HIPCHK(hipMemcpy(s->K.p, K, s->K.n, hipMemcpyHostToDevice));
   if (k) HIPCHK(hipMemcpy(s->k.p, k, s->k.n, hipMemcpyHostToDevice));
   return ILQG_OK;
@@ -735,7 +784,7 @@ int ilqg_solver_set_gains(ilqg_solver* s, const double* K, const double* k) {
 
 int ilqg_solver_get_gains(ilqg_solver* s, double* K, double* k) {
   if (!s) return fail(ILQG_ERR_ARG, "null solver");
-  HIPCHK(hipStreamSynchronize(s->stream));
+  HIPCHK(s->sync_all());
   if (K) HIPCHK(hipMemcpy(K, s->K.p, s->K.n, hipMemcpyDeviceToHost));
   if (k) HIPCHK(hipMemcpy(k, s->k.p, s->k.n, hipMemcpyDeviceToHost));
   return ILQG_OK;
@@ -743,7 +792,7 @@ int ilqg_solver_get_gains(ilqg_solver* s, double* K, double* k) {
 
 int ilqg_solver_get_deriv(ilqg_solver* s, double* deriv) {
   if (!s || !deriv) return fail(ILQG_ERR_ARG, "bad argument");
-  HIPCHK(hipStreamSynchronize(s->stream));
+  HIPCHK(s->sync_all());
   HIPCHK(hipMemcpy2D(deriv, (size_t)s->D * 8, s->deriv.p, (size_t)s->Dp * 8, (size_t)s->D * 8, (size_t)s->S * s->P,
                      hipMemcpyDeviceToHost));
   return ILQG_OK;
@@ -751,7 +800,7 @@ int ilqg_solver_get_deriv(ilqg_solver* s, double* deriv) {
 
 int ilqg_solver_set_deriv(ilqg_solver* s, const double* deriv) {
   if (!s || !deriv) return fail(ILQG_ERR_ARG, "bad argument");
-  HIPCHK(hipStreamSynchronize(s->stream));
+  HIPCHK(s->sync_all());
   HIPCHK(hipMemcpy2D(s->deriv.p, (size_t)s->Dp * 8, deriv, (size_t)s->D * 8, (size_t)s->D * 8, (size_t)s->S * s->P,
                      hipMemcpyHostToDevice));
   return ILQG_OK;
@@ -759,7 +808,7 @@ int ilqg_solver_set_deriv(ilqg_solver* s, const double* deriv) {
 
 int ilqg_solver_get_value(ilqg_solver* s, double* V, double* v) {
   if (!s) return fail(ILQG_ERR_ARG, "null solver");
-  HIPCHK(hipStreamSynchronize(s->stream));
+  HIPCHK(s->sync_all());
   if (V) HIPCHK(hipMemcpy(V, s->V.p, s->V.n, hipMemcpyDeviceToHost));
   if (v) HIPCHK(hipMemcpy(v, s->v.p, s->v.n, hipMemcpyDeviceToHost));
   return ILQG_OK;
@@ -767,63 +816,95 @@ int ilqg_solver_get_value(ilqg_solver* s, double* V, double* v) {
 
 int ilqg_solver_get_costs(ilqg_solver* s, double* cost, int* selected) {
   if (!s) return fail(ILQG_ERR_ARG, "null solver");
-  HIPCHK(hipStreamSynchronize(s->stream));
+  HIPCHK(s->sync_all());
   if (cost) HIPCHK(hipMemcpy(cost, s->cost_cand.p, s->cost_cand.n, hipMemcpyDeviceToHost));
   if (selected) HIPCHK(hipMemcpy(selected, s->sel.p, s->sel.n, hipMemcpyDeviceToHost));
   return ILQG_OK;
 }
 
+// a contiguous seed range [s0, s0+ns) of the solver, launched on `st`; every
+// per-seed array is seed-major, so a range is the same kernels on offset pointers
+struct SeedRange {
+  int s0, ns;
+  hipStream_t st;
+  unsigned* sync;  // the range's own hand-off block (fused sweep)
+};
+static SeedRange whole(ilqg_solver* s) { return {0, s->S, s->stream, s->sync.as<unsigned>()}; }
+static TrajDev toff(TrajDev t, size_t pts, const HostModel& h) {
+  return TrajDev{t.time + pts, t.qpos + pts * h.nq, t.qvel + pts * h.nv, t.warm + pts * h.nv, t.ctrl + pts * h.nu};
+}
+
+// rollout of every (seed, alpha) candidate of the range, then selection + setDInit.
+// before_select: an event the selection waits on (its outputs may still be read there)
+static hipError_t forward_range(ilqg_solver* s, const SeedRange& r, hipEvent_t before_select) {
+  const ilqg_model* m = s->model;
+  const HostModel& h = m->host;
+  const size_t s0 = r.s0, P = s->P, A = s->A, nx = s->nx;
+  TrajDev nom = toff(s->tview(s->traj), s0 * P, h), di = toff(s->tview(s->dinit), s0, h);
+  const bool multi = s->A > 1;
+  TrajDev outv = multi ? toff(s->tview(s->cand), s0 * A * P, h) : nom;
+  const double* K = s->K.as<double>() + s0 * P * h.nu * nx;
+  const double* k = s->k.as<double>() + s0 * P * h.nu;
+  const double* qa = s->qfrc_applied.as<double>() + s0 * h.nv;
+  const double* xf = s->xfrc_applied.as<double>() + s0 * 6 * h.nbody;
+  double* cc = s->cost_cand.as<double>() + s0 * A;
+  hipError_t e = s->timed(0, [&] {
+    if (coop_ok(m))
+      return launch_rollout_coop(m->dm, m->Lc, m->C, m->X, r.ns, s->A, s->P, nom, outv, multi ? 1 : 0, K, k,
+                                 s->alphas.as<double>(), di, qa, xf, 0, s->cview(), cc, r.st);
+    return launch_rollout(m->dm, m->L, s->ws(), r.ns, s->A, s->P, nom, outv, multi ? 1 : 0, K, k,
+                          s->alphas.as<double>(), di, qa, xf, 0, s->cview(), cc, r.st);
+  }, r.st);
+  if (e != hipSuccess) return e;
+  if (before_select) {
+    e = hipStreamWaitEvent(r.st, before_select, 0);
+    if (e != hipSuccess) return e;
+  }
+  return s->timed(1, [&] {
+    return launch_select(m->dm, r.ns, s->A, s->P, s->opts.select_mode, multi ? 1 : 0, cc, s->sel.as<int>() + s0,
+                         s->cost_sel.as<double>() + s0, outv, nom, di, r.st);
+  }, r.st);
+}
+
 int ilqg_forward(ilqg_solver* s) {
   if (!s || !s->initialized) return fail(ILQG_ERR_ARG, "solver not initialised");
-  const ilqg_model* m = s->model;
-  TrajDev nom = s->tview(s->traj), di = s->tview(s->dinit);
-  const bool multi = s->A > 1;
-  TrajDev outv = multi ? s->tview(s->cand) : nom;
-  HIPCHK(s->timed(0, [&] {
-    if (coop_ok(m))
-      return launch_rollout_coop(m->dm, m->Lc, m->C, m->X, s->S, s->A, s->P, nom, outv, multi ? 1 : 0,
-                                 s->K.as<double>(), s->k.as<double>(), s->alphas.as<double>(), di,
-                                 s->qfrc_applied.as<double>(), s->xfrc_applied.as<double>(), 0, s->cview(),
-                                 s->cost_cand.as<double>(), s->stream);
-    return launch_rollout(m->dm, m->L, s->ws(), s->S, s->A, s->P, nom, outv, multi ? 1 : 0, s->K.as<double>(),
-                          s->k.as<double>(), s->alphas.as<double>(), di, s->qfrc_applied.as<double>(),
-                          s->xfrc_applied.as<double>(), 0, s->cview(), s->cost_cand.as<double>(), s->stream);
-  }));
-  HIPCHK(s->timed(1, [&] {
-    return launch_select(m->dm, s->S, s->A, s->P, s->opts.select_mode, multi ? 1 : 0, s->cost_cand.as<double>(),
-                         s->sel.as<int>(), s->cost_sel.as<double>(), outv, nom, di, s->stream);
-  }));
+  if (!s->groups.empty()) HIPCHK(s->sync_all());  // a lone forward pass: every group's state settled
+  HIPCHK(forward_range(s, whole(s), nullptr));
   return ILQG_OK;
 }
 
-// the fused sweep's launch: its hand-off words zeroed on the stream first
-static hipError_t fused_launch(ilqg_solver* s, bool with_backward) {
+// the fused sweep over a seed range: its hand-off words zeroed on the stream first
+// mode: 0 the sweep alone, 1 the sweep with the backward roles streamed behind it
+static hipError_t fused_launch(ilqg_solver* s, const SeedRange& r, int mode) {
   const ilqg_model* m = s->model;
-  hipError_t e = hipMemsetAsync(s->sync.p, 0, s->sync.n, s->stream);
+  const HostModel& h = m->host;
+  const size_t s0 = r.s0, P = s->P, nx = s->nx;
+  hipError_t e = hipMemsetAsync(r.sync, 0, sync_bytes((size_t)r.ns * P), r.st);
   if (e != hipSuccess) return e;
   FdFused a{};
-  a.tr = s->tview(s->traj);
-  a.S = s->S;
+  a.tr = toff(s->tview(s->traj), s0 * P, h);
+  a.S = r.ns;
   a.P = s->P;
-  a.nB = with_backward ? s->S : 0;
+  a.nB = mode ? r.ns : 0;
   a.lag = s->lag;
   a.nvt = s->nvt;
+  a.nut = s->nut;
   a.cv = s->cv;
   a.Dp = s->Dp;
   a.WCp = s->WCp;
-  a.qfrc_applied = s->qfrc_applied.as<double>();
-  a.xfrc_applied = s->xfrc_applied.as<double>();
+  a.qfrc_applied = s->qfrc_applied.as<double>() + s0 * h.nv;
+  a.xfrc_applied = s->xfrc_applied.as<double>() + s0 * 6 * h.nbody;
   a.cost = s->cview();
-  a.cw = s->cw.as<double>();
-  a.deriv = s->deriv.as<double>();
-  a.sync = s->sync.as<unsigned>();
+  a.cw = s->cw.as<double>() + s0 * P * s->WCp;
+  a.deriv = s->deriv.as<double>() + s0 * P * s->Dp;
+  a.sync = r.sync;
   a.fault = s->fault.as<unsigned>();
   a.mu = s->opts.mu;
-  a.K = s->K.as<double>();
-  a.k = s->k.as<double>();
-  a.V = s->V.as<double>();
-  a.v = s->v.as<double>();
-  return launch_fd_fused_coop(m->dm, m->Lc, m->C, m->X, a, s->stream);
+  a.K = s->K.as<double>() + s0 * P * h.nu * nx;
+  a.k = s->k.as<double>() + s0 * P * h.nu;
+  a.V = s->V.as<double>() + s0 * nx * nx;
+  a.v = s->v.as<double>() + s0 * nx;
+  return launch_fd_fused_coop(m->dm, m->Lc, m->C, m->X, a, r.st);
 }
 
 int ilqg_fd_sweep(ilqg_solver* s) {
@@ -832,7 +913,8 @@ int ilqg_fd_sweep(ilqg_solver* s) {
   TrajDev nom = s->tview(s->traj);
   const int npts = s->S * s->P;
   if (s->fused) {
-    HIPCHK(s->timed(3, [&] { return fused_launch(s, false); }));
+    if (!s->groups.empty()) HIPCHK(s->sync_all());
+    HIPCHK(s->timed(3, [&] { return fused_launch(s, whole(s), 0); }));
     return ILQG_OK;
   }
   HIPCHK(s->timed(2, [&] {
@@ -859,6 +941,7 @@ int ilqg_fd_sweep(ilqg_solver* s) {
 int ilqg_backward(ilqg_solver* s) {
   if (!s || !s->initialized) return fail(ILQG_ERR_ARG, "solver not initialised");
   const ilqg_model* m = s->model;
+  if (!s->groups.empty()) HIPCHK(s->sync_all());
   HIPCHK(s->timed(4, [&] {
     return launch_backward(m->dm, s->S, s->P, s->opts.mu, s->deriv.as<double>(), s->Dp, s->tview(s->traj),
                            s->K.as<double>(), s->k.as<double>(), s->V.as<double>(), s->v.as<double>(), s->stream);
@@ -866,12 +949,38 @@ int ilqg_backward(ilqg_solver* s) {
   return ILQG_OK;
 }
 
+// seed groups: per group g on its own stream, rollout + selection (the selection
+// after the solver stream's start-of-iteration point, where the previous
+// iteration's costs may still be read), then the fused sweep (after group g-1's
+// sweep of this iteration when the token is on).  The solver stream waits for
+// every group's selection only: per-seed costs of this iteration are ordered
+// there, while the sweeps run on behind it.
+static int iterate_groups(ilqg_solver* s) {
+  if (!s->ev_start) HIPCHK(hipEventCreateWithFlags(&s->ev_start, hipEventDisableTiming));
+  HIPCHK(hipEventRecord(s->ev_start, s->stream));
+  for (auto& gr : s->groups) {
+    // the rollout reads the gains and overwrites the trajectory the group's
+    // previous sweep read: after that sweep
+    HIPCHK(hipStreamWaitEvent(gr.rs, gr.fd, 0));
+    HIPCHK(forward_range(s, SeedRange{gr.s0, gr.ns, gr.rs, gr.sync}, s->ev_start));
+    HIPCHK(hipEventRecord(gr.costs, gr.rs));
+    HIPCHK(hipStreamWaitEvent(gr.fs, gr.costs, 0));
+    SeedRange r{gr.s0, gr.ns, gr.fs, gr.sync};
+    HIPCHK(s->timed(5, [&] { return fused_launch(s, r, 1); }, gr.fs));
+    HIPCHK(hipEventRecord(gr.fd, gr.fs));
+  }
+  for (auto& gr : s->groups) HIPCHK(hipStreamWaitEvent(s->stream, gr.costs, 0));
+  return ILQG_OK;
+}
+
 int ilqg_iterate(ilqg_solver* s) {
+  if (!s || !s->initialized) return fail(ILQG_ERR_ARG, "solver not initialised");
+  if (!s->groups.empty()) return iterate_groups(s);
   int rc = ilqg_forward(s);
   if (rc) return rc;
   if (s->fused) {
     // FD sweep with the Riccati recursion of every seed streamed behind it (one launch)
-    HIPCHK(s->timed(5, [&] { return fused_launch(s, true); }));
+    HIPCHK(s->timed(5, [&] { return fused_launch(s, whole(s), 1); }));
     return ILQG_OK;
   }
   rc = ilqg_fd_sweep(s);
@@ -881,7 +990,7 @@ int ilqg_iterate(ilqg_solver* s) {
 
 int ilqg_synchronize(ilqg_solver* s) {
   if (!s) return fail(ILQG_ERR_ARG, "null solver");
-  HIPCHK(hipStreamSynchronize(s->stream));
+  HIPCHK(s->sync_all());
   unsigned flt = 0;
   HIPCHK(hipMemcpy(&flt, s->fault.p, 4, hipMemcpyDeviceToHost));
   if (flt) return fail(ILQG_ERR_HIP, "fused FD sweep: a hand-off wait timed out");
@@ -892,7 +1001,7 @@ void* ilqg_solver_stream(ilqg_solver* s) { return s ? (void*)s->stream : nullptr
 
 int ilqg_solver_set_stream(ilqg_solver* s, void* stream) {
   if (!s) return fail(ILQG_ERR_ARG, "null solver");
-  HIPCHK(hipStreamSynchronize(s->stream));
+  HIPCHK(s->sync_all());
   s->stream = stream ? (hipStream_t)stream : s->own_stream;
   return ILQG_OK;
 }
@@ -905,7 +1014,7 @@ int ilqg_solver_set_timing(ilqg_solver* s, int enable) {
 
 int ilqg_solver_get_timing(ilqg_solver* s, double* ms, int* launches) {
   if (!s) return fail(ILQG_ERR_ARG, "null solver");
-  HIPCHK(hipStreamSynchronize(s->stream));
+  HIPCHK(s->sync_all());
   for (int k = 0; k < ILQG_NKERNEL; k++) {
     double tot = 0;
     for (auto& p : s->ev[k]) {
@@ -919,6 +1028,70 @@ int ilqg_solver_get_timing(ilqg_solver* s, double* ms, int* launches) {
     if (launches) launches[k] = (int)s->ev[k].size();
     s->ev[k].clear();
   }
+  return ILQG_OK;
+}
+
+int ilqg_solver_set_groups(ilqg_solver* s, int ngroups) {
+  if (!s || ngroups < 1) return fail(ILQG_ERR_ARG, "bad argument");
+  HIPCHK(s->sync_all());
+  s->free_groups();
+  ngroups = std::min(ngroups, s->S);
+  if (ngroups == 1) return ILQG_OK;
+  if (!s->fused) return fail(ILQG_ERR_UNSUPPORTED, "seed groups need the fused FD sweep (cooperative model kernels)");
+  const bool token = getenv_int("ILQG_GROUP_TOKEN", 1) != 0;
+  const int roll_cus = getenv_int("ILQG_ROLL_CUS", 0);
+  // CU masks: the rollout streams get roll_cus CUs spread evenly over the chip
+  // (every k-th CU), the sweep streams the rest
+  int ncu = 0;
+  HIPCHK(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, s->opts.device));
+  std::vector<uint32_t> rmask((ncu + 31) / 32, 0), fmask(rmask);
+  const bool masked = roll_cus > 0 && roll_cus < ncu;
+  if (masked) {
+    for (int c = 0, j = 0; c < ncu; c++) {
+      const bool r = j < roll_cus && (long)c * roll_cus / ncu >= j;
+      if (r) j++;
+      (r ? rmask : fmask)[c / 32] |= 1u << (c % 32);
+    }
+  }
+  auto mkstream = [&](hipStream_t* st, std::vector<uint32_t>& mask) {
+    return masked ? hipExtStreamCreateWithCUMask(st, (uint32_t)mask.size(), mask.data())
+                  : hipStreamCreateWithFlags(st, hipStreamNonBlocking);
+  };
+  if (token) {
+    hipError_t e = mkstream(&s->fstream, fmask);
+    if (e != hipSuccess) return hip_fail(e, "seed group sweep stream");
+  }
+  s->groups.resize(ngroups);
+  const size_t P = s->P;
+  size_t off = 0;  // u32 words into the sync block, 16-byte aligned per group
+  for (int g = 0; g < ngroups; g++) {
+    auto& gr = s->groups[g];
+    gr.s0 = (int)((long)s->S * g / ngroups);
+    gr.ns = (int)((long)s->S * (g + 1) / ngroups) - gr.s0;
+    gr.sync = s->sync.as<unsigned>() + off;
+    off += sync_bytes((size_t)gr.ns * P) / 4;
+    hipError_t e = mkstream(&gr.rs, rmask);
+    if (e == hipSuccess) {
+      if (token) gr.fs = s->fstream;
+      else e = mkstream(&gr.fs, fmask);
+    }
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&gr.costs, hipEventDisableTiming);
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&gr.fd, hipEventDisableTiming);
+    if (e != hipSuccess) {
+      s->free_groups();
+      return hip_fail(e, "seed group streams");
+    }
+  }
+  if (off * 4 > s->sync.n) {
+    s->free_groups();
+    return fail(ILQG_ERR_ARG, "seed groups: hand-off block too small");
+  }
+  return ILQG_OK;
+}
+
+int ilqg_solver_get_groups(ilqg_solver* s, int* ngroups) {
+  if (!s || !ngroups) return fail(ILQG_ERR_ARG, "bad argument");
+  *ngroups = s->groups.empty() ? 1 : (int)s->groups.size();  // 1 either way for one group
   return ILQG_OK;
 }
 

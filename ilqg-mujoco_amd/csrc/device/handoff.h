@@ -23,6 +23,13 @@ typedef __attribute__((address_space(1))) unsigned long long gu64;
 // broken producer can never hang the GPU
 constexpr unsigned HANDOFF_SPIN_LIMIT = 1u << 22;
 
+#ifdef ILQG_STAMPS
+// diagnostic build: fused-sweep timeline (s_memtime ticks) -- [0] backward role 0
+// cycles, [1] of which waiting for records, [2] waits that polled more than
+// once, [3] role-0 start, [4] latest FD team end, [5] role-0 end, [8 + s] role s cycles
+__device__ unsigned long long g_fused_diag[24];
+#endif
+
 __device__ __forceinline__ double ld_sc1(const double* p) {
   return __longlong_as_double(
       (long long)__hip_atomic_load((gu64*)(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
@@ -54,6 +61,33 @@ __device__ inline bool bw_wait_geq(const unsigned* w, unsigned target, unsigned*
   // keep the payload's loads below the poll
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
   return true;
+}
+
+// wave-uniform: the first record of a window is awaited, and the window's
+// later records are checked in the same poll (lane l reads flag p + l), so a
+// consumer running behind its producer polls once per run of published records
+// instead of once per record (an agent-scope load takes microseconds while a
+// sweep loads the memory system).  Returns the last index q >= p with flags
+// p..q all >= target (p on a timed-out wait, after setting *fault).
+__device__ inline int bw_wait_window(const unsigned* flags, int p, int n, unsigned target, unsigned* fault) {
+  const int lane = threadIdx.x & 63;
+  for (unsigned spins = 0;; spins++) {
+    if ((spins & 255) == 255 && fault &&
+        __builtin_amdgcn_readfirstlane(__hip_atomic_load((gu32*)(fault), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)))
+      return p;
+    const int q = p + lane;
+    const bool ok = q < n && __hip_atomic_load((gu32*)(flags + q), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= target;
+    const unsigned long long mask = __ballot(ok);
+    if (mask & 1ull) {
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      return ~mask ? p + (int)__builtin_ctzll(~mask) - 1 : p + 63;
+    }
+    if (spins > HANDOFF_SPIN_LIMIT) {
+      if (fault && lane == 0) __hip_atomic_fetch_or((gu32*)(fault), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      return p;
+    }
+    __builtin_amdgcn_s_sleep(4);
+  }
 }
 
 // one lane signals for the (single-wave) team after drain_stores()

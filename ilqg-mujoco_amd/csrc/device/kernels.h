@@ -64,6 +64,7 @@ struct FdFused {
   int nB;        // backward roles (S, or 0 for the sweep alone)
   int lag;       // points between a centre team and its column teams
   int nvt, cv;   // qvel teams per point, columns per qvel team
+  int nut;       // ctrl teams per point (one per ctrl column), or 0: the centre team runs them
   int Dp, WCp;   // padded record strides (doubles, multiples of 16 = 128 B)
   const double* qfrc_applied;
   const double* xfrc_applied;

@@ -23,6 +23,9 @@ constexpr int TEAM = TEAM_SIZE;
 // FD teams: at least 2 waves per SIMD (<= 256 VGPRs), so LDS (6 teams per CU
 // for the hopper) and not registers bounds the sweep's occupancy
 constexpr int FD_WAVES_PER_EU = 2;
+#ifndef ILQG_BW_PRIO
+#define ILQG_BW_PRIO 1
+#endif
 
 // LDS: [workspace doubles][coop doubles][model image][workspace ints][coop ints]
 __device__ inline Team make_team(const auto& L, const auto& C) {
@@ -272,17 +275,21 @@ __global__ __launch_bounds__(TEAM, FD_WAVES_PER_EU) void k_fd_cols_s(DevModel mg
 // teams in point-major order, terminal point first -- the order the Riccati
 // recursion consumes them (inc/ilqr.h:144):
 //   C(s,p): cpMjData + mj_forward + 2 forwardSkip(VEL) (mjderivative.cpp:61-75),
-//           publishes the centre warm start and cost, then the ctrl columns
-//           (:78-111) on its own position/velocity stages (the reference's
-//           forwardSkip(mjSTAGE_VEL));
+//           publishes the centre warm start and cost (then, when nut = 0, the
+//           ctrl columns (:78-111) on its own position/velocity stages, the
+//           reference's forwardSkip(mjSTAGE_VEL));
+//   U(s,p,i): ctrl column i (:78-111) on a position/velocity stage of its own
+//           (nut > 0: the centre's 3 + 2 nu evaluations in a row were the
+//           longest chain of the sweep; a Newton solve runs up to 30 iterations
+//           at tolerance 0, :241-242);
 //   V(s,p,k): qvel columns k*cv .. (:114-142) on one position stage
 //           (forwardSkip(mjSTAGE_POS));
 //   Q(s,p,i): qpos column i (:145-206).
-// V and Q teams run their first position/velocity stages before they wait for
-// C's warm start (those stages never read it); the V/Q teams of point p are
+// U, V and Q teams run their first position/velocity stages before they wait for
+// C's warm start (those stages never read it); the U/V/Q teams of point p are
 // issued `lag` points after C(p).  A team stores its deriv entries
 // write-through and announces them on done[s,p] (handoff.h); the backward role
-// reads record p once all 1 + nvt + nv teams have announced.  Every evaluation
+// reads record p once all 1 + nut + nvt + nv teams have announced.  Every evaluation
 // reads exactly the inputs the two-kernel sweep gives it, so the records are
 // bit-identical.  Deadlock-free: a team waits only on work holding a smaller
 // ticket (already running, never waiting), the backward roles only on FD teams
@@ -294,7 +301,7 @@ __device__ inline unsigned take_ticket(unsigned* sync) {
   return __builtin_amdgcn_readfirstlane(t);
 }
 
-// FD item u -> role (0 = C, 1 = V, 2 = Q), seed, point, index; ntm = nvt + nv
+// FD item u -> role (0 = C, 1 = V, 2 = Q, 3 = U), seed, point, index; ntm = nut + nvt + nv
 __device__ inline void fd_decode(const FdFused& a, unsigned ntm, unsigned u, int& role, int& s, int& p, int& idx) {
   const unsigned nC = a.S, nW = a.S * ntm, lag = a.lag, P = a.P;
   idx = 0;
@@ -321,8 +328,9 @@ __device__ inline void fd_decode(const FdFused& a, unsigned ntm, unsigned u, int
   p = g - lag;
   s = o / ntm;
   const int w = o % ntm;
-  if (w < a.nvt) { role = 1; idx = w; }
-  else { role = 2; idx = w - a.nvt; }
+  if (w < a.nut) { role = 3; idx = w; }
+  else if (w < a.nut + a.nvt) { role = 1; idx = w - a.nut; }
+  else { role = 2; idx = w - a.nut - a.nvt; }
 }
 
 __device__ inline void fd_fused_body(const auto& m, const auto& L, const auto& C, const auto& X, const Team& T,
@@ -331,7 +339,7 @@ __device__ inline void fd_fused_body(const auto& m, const auto& L, const auto& C
   const int nv = m.nv, nu = m.nu, nq = m.nq;
   const int nctrl = nu < nv ? nu : nv;  // mjderivative.cpp:78-82 (assumes nv >= nu)
   int role, s, p, idx;
-  fd_decode(a, a.nvt + nv, u, role, s, p, idx);
+  fd_decode(a, a.nut + a.nvt + nv, u, role, s, p, idx);
   const int pt = s * a.P + p;
   double* dr = a.deriv + (size_t)pt * a.Dp;
   double* cwp = a.cw + (size_t)pt * a.WCp;
@@ -366,7 +374,7 @@ __device__ inline void fd_fused_body(const auto& m, const auto& L, const auto& C
     drain_stores();
     TSYNC();
     if (tid == 0) signal_set(cflag, 1u);
-    for (int i = 0; i < nctrl; i++) {
+    for (int i = 0; i < (a.nut ? 0 : nctrl); i++) {
       const double u0 = ctrl[i];
       TSYNC();
       if (tid == 0) {
@@ -383,6 +391,25 @@ __device__ inline void fd_fused_body(const auto& m, const auto& L, const auto& C
       if (tid == 0) ctrl[i] = u0;
       TSYNC();
     }
+  } else if (role == 3) {
+    // ctrl column idx on its own position/velocity stages (ctrl enters only the
+    // acceleration stage, so they equal the centre's)
+    const int i = idx;
+    forward_posvel(m, L, C, X, T, STAGE_NONE);
+    get_centre();
+    const double u0 = ctrl[i];
+    TSYNC();
+    if (tid == 0) {
+      ctrl[i] = u0 + FD_EPS;
+      st_sc1(dr + G + 2 * nv + i, (step_cost(m, a.cost, qpos, qvel, ctrl) - costCenter) / FD_EPS);
+    }
+    set_warm();
+    forward_acc(m, L, C, X, T, FD_NITER, 0.0);
+    const double qp = tid < nv ? qacc[tid] : 0.0;
+    if (tid == 0) ctrl[i] = u0 - FD_EPS;
+    set_warm();
+    forward_skip(m, L, C, X, T, STAGE_VEL, FD_NITER, 0.0);
+    if (tid < nv) st_sc1(dr + 2 * nv * nv + i + tid * nu, (qp - qacc[tid]) / (2 * FD_EPS));
   } else if (role == 1) {
     const int i0 = idx * a.cv, i1 = i0 + a.cv < nv ? i0 + a.cv : nv;
     for (int i = i0; i < i1; i++) {
@@ -444,15 +471,34 @@ __device__ inline void fd_fused_body(const auto& m, const auto& L, const auto& C
   drain_stores();
   TSYNC();
   if (tid == 0) signal_add(done);
+#ifdef ILQG_STAMPS
+  if (tid == 0) atomicMax(&g_fused_diag[4], __builtin_amdgcn_s_memtime());
+#endif
   STAMP_FLUSH();
 }
 
 template <int NV, int NU, class MD>
 __device__ inline void fd_backward_role(const MD& mg, const FdFused& a, int s) {
   extern __shared__ double lds[];
+  // the serial Riccati chain shares its CU with sweep teams: it takes the
+  // SIMD's issue arbitration (MI355X_MICROARCH.md "VALU issue is arbitrated
+  // ... by priority, then age")
+  if (ILQG_BW_PRIO) __builtin_amdgcn_s_setprio(3);
+#ifdef ILQG_STAMPS
+  const unsigned long long t0_ = __builtin_amdgcn_s_memtime();
+  if (s == 0 && threadIdx.x == 0) g_fused_diag[3] = t0_;
+#endif
   backward_seed<NV, NU>(mg, mg.nq, mg.nv, mg.nu, a.P, mg.opt_timestep, a.mu, a.deriv, a.Dp, a.tr, a.K, a.k, a.V,
-                        a.v, s, threadIdx.x, lds, a.sync + 4 + (size_t)a.S * a.P, (unsigned)(1 + a.nvt + mg.nv),
+                        a.v, s, threadIdx.x, lds, a.sync + 4 + (size_t)a.S * a.P, (unsigned)(1 + a.nut + a.nvt + mg.nv),
                         a.fault);
+#ifdef ILQG_STAMPS
+  if (s < 16 && threadIdx.x == 0) g_fused_diag[8 + s] = __builtin_amdgcn_s_memtime() - t0_;
+  if (s == 0 && threadIdx.x == 0) {
+    const unsigned long long t1_ = __builtin_amdgcn_s_memtime();
+    g_fused_diag[0] += t1_ - t0_;
+    g_fused_diag[5] = t1_;
+  }
+#endif
 }
 
 __global__ __launch_bounds__(TEAM, FD_WAVES_PER_EU) void k_fd_fused_coop(DevModel mg, WsLayout L, CoopLayout C, CoopAux Xg, FdFused a) {
@@ -723,7 +769,7 @@ hipError_t launch_fd_cols_coop(const DevModel& m, const WsLayout& L, const CoopL
 
 hipError_t launch_fd_fused_coop(const DevModel& m, const WsLayout& L, const CoopLayout& C, const CoopAux& X,
                                 const FdFused& a, hipStream_t st) {
-  const long items = (long)a.S * a.P * (1 + a.nvt + m.nv);
+  const long items = (long)a.S * a.P * (1 + a.nut + a.nvt + m.nv);
   const long blocks = items + a.nB;
   if (items <= 0) return hipSuccess;
   size_t lds = coop_lds_bytes(L, C);
@@ -810,6 +856,14 @@ hipError_t launch_rollout_coop(const DevModel& m, const WsLayout& L, const CoopL
 }  // namespace ilqg
 
 #ifdef ILQG_STAMPS
+extern "C" int ilqg_debug_fused(unsigned long long* d, int reset) {
+  if (hipMemcpyFromSymbol(d, HIP_SYMBOL(ilqg::g_fused_diag), sizeof(unsigned long long) * 24) != hipSuccess) return 3;
+  if (reset) {
+    unsigned long long z[24] = {0};
+    (void)hipMemcpyToSymbol(HIP_SYMBOL(ilqg::g_fused_diag), z, sizeof(z));
+  }
+  return 0;
+}
 extern "C" int ilqg_debug_stamps(unsigned long long* acc, unsigned long long* cnt, int reset) {
   if (hipMemcpyFromSymbol(acc, HIP_SYMBOL(ilqg::coop::g_stamp_acc), sizeof(unsigned long long) * 48) != hipSuccess)
     return 3;

@@ -105,8 +105,21 @@ __device__ inline void backward_seed(const MD& m, int nq, int nv_rt, int nu_rt, 
   const bool pref = D <= BW_PF * BW_THREADS;
   // streaming (done != nullptr): record p is read only once its FD teams have
   // all published it (done[s P + p] >= target), with sc1 loads
+  // (the flags of records up to ready_upto were seen published by an earlier poll)
+  int ready_upto = -1;
   auto ready = [&](int p) {
-    if (done) bw_wait_geq(done + (size_t)s * P + p, target, fault);
+    if (!done || p <= ready_upto) return;
+#ifdef ILQG_STAMPS
+    const unsigned long long t0_ = __builtin_amdgcn_s_memtime();
+#endif
+    ready_upto = bw_wait_window(done + (size_t)s * P, p, P, target, fault);
+#ifdef ILQG_STAMPS
+    if (s == 0 && tid == 0) {
+      g_fused_diag[1] += __builtin_amdgcn_s_memtime() - t0_;
+      g_fused_diag[2]++;
+    }
+    if (s < 8 && tid == 0) g_fused_diag[16 + s] += __builtin_amdgcn_s_memtime() - t0_;
+#endif
   };
   auto ld = [&](const double* a) -> double { return done ? ld_sc1(a) : *a; };
   // buffers are reused once dead: V holds V_new (V is read only by stage 1),

@@ -61,7 +61,7 @@ EXPORTS = [
     "ilqg_solver_get_deriv", "ilqg_solver_set_deriv", "ilqg_solver_get_value", "ilqg_solver_get_costs",
     "ilqg_forward", "ilqg_fd_sweep", "ilqg_backward", "ilqg_iterate", "ilqg_synchronize",
     "ilqg_solver_stream", "ilqg_solver_device_costs", "ilqg_solver_set_stream", "ilqg_solver_set_timing",
-    "ilqg_solver_get_timing",
+    "ilqg_solver_get_timing", "ilqg_solver_set_groups", "ilqg_solver_get_groups",
 ]
 KERNELS = ("rollout", "select", "fd_centre", "fd_cols", "backward", "fd_backward")
 
@@ -378,6 +378,16 @@ class ILQR:
     def set_stream(self, stream: Optional[int]):
         """enqueue on an external hipStream_t (e.g. torch.cuda.current_stream().cuda_stream)"""
         _check(lib().ilqg_solver_set_stream(self._h, ctypes.c_void_p(stream) if stream else None), "set_stream")
+
+    def set_groups(self, ngroups: int):
+        """pipeline the seeds as `ngroups` groups on their own streams (ilqg_solver_set_groups)"""
+        _check(lib().ilqg_solver_set_groups(self._h, int(ngroups)), "set_groups")
+
+    @property
+    def groups(self) -> int:
+        n = ctypes.c_int()
+        _check(lib().ilqg_solver_get_groups(self._h, ctypes.byref(n)), "get_groups")
+        return n.value
 
     def set_timing(self, enable: bool):
         _check(lib().ilqg_solver_set_timing(self._h, int(enable)), "set_timing")

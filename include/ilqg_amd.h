@@ -150,6 +150,16 @@ int ilqg_solver_get_timing(ilqg_solver* s, double* ms, int* launches);
 /* device pointer to the per-seed selected-candidate cost (nseed doubles), for
    an in-stream collective (RCCL all-gather) without a host round trip */
 int ilqg_solver_device_costs(ilqg_solver* s, double** dptr);
+/* seed groups (an MI355X extension; no reference counterpart): split the
+   nseed seeds into ngroups contiguous ranges, each iterated on its own stream,
+   so one group's latency-bound rollout overlaps another group's FD sweep.
+   ilqg_iterate then orders on the solver stream only the completion of every
+   group's rollout + selection (the per-seed costs, ilqg_solver_device_costs);
+   every other entry point synchronises all groups first.  Results are
+   bit-identical to ngroups = 1 (seeds are independent).  Needs the fused FD
+   sweep (cooperative model kernels): ILQG_ERR_UNSUPPORTED otherwise. */
+int ilqg_solver_set_groups(ilqg_solver* s, int ngroups);
+int ilqg_solver_get_groups(ilqg_solver* s, int* ngroups);
 
 #ifdef __cplusplus
 }

@@ -309,10 +309,12 @@ def test_humanoid_iterate_tangent_space(ia, ora):
 
 
 @pytest.mark.parametrize("env", [{"ILQG_FUSED": "0"}, {"ILQG_FD_LAG": "0"}, {"ILQG_FD_LAG": "1"},
-                                 {"ILQG_FD_LAG": "7", "ILQG_FD_CV": "1"}, {"ILQG_FD_CV": "6"}])
+                                 {"ILQG_FD_LAG": "7", "ILQG_FD_CV": "1"}, {"ILQG_FD_CV": "6"},
+                                 {"ILQG_FD_USPLIT": "0"}, {"ILQG_FD_USPLIT": "0", "ILQG_FD_LAG": "3"}])
 def test_fused_sweep_schedules(ia, ora, env, monkeypatch):
     """The fused FD sweep + streamed backward pass (k_fd_fused_s): every hand-off
-    schedule (centre lag, qvel columns per team) and the two-kernel sweep give the
+    schedule (centre lag, qvel columns per team, ctrl columns on their own teams
+    or the centre's) and the two-kernel sweep give the
     oracle's iterate bit for bit (seeds x points x columns vary the ticket order)"""
     import workloads
     for k, v in env.items():
@@ -340,3 +342,30 @@ def test_fused_sweep_schedules(ia, ora, env, monkeypatch):
     g.fd_sweep()
     g.synchronize()
     exact(g.deriv(), D, "fd_sweep alone vs iterate's fused records")
+
+
+@pytest.mark.parametrize("G,env", [(1, {}), (2, {}), (3, {"ILQG_ROLL_CUS": "64"}),
+                                   (2, {"ILQG_ROLL_CUS": "32", "ILQG_GROUP_TOKEN": "0"}),
+                                   (5, {"ILQG_GROUP_TOKEN": "0"})])
+def test_seed_groups_identical(ia, G, env, monkeypatch):
+    """ilqg_solver_set_groups: seeds iterated as G groups on their own streams
+    (uneven ranges; with and without CU masks and the sweep token) give exactly the single-stream results, and the solver stream
+    sees every group's selected costs"""
+    import workloads
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
+    m = ia.Model.load(model_path("hopper"))
+    S, H = 5, 50
+    dmain = workloads.hopper_dmain(m, S, sigma=0.01)
+    out = []
+    for g_ in (None, G):
+        g = ia.ILQR(m, dmain, H, ia.HOPPER_COST, alphas=workloads.LINESEARCH_ALPHAS[:4], select="min_cost")
+        if g_ is not None:
+            g.set_groups(g_)
+            assert g.groups == g_
+        for _ in range(3):
+            g.iterate()
+        g.synchronize()
+        out.append((g.traj().qpos, *g.gains(), g.deriv(), *g.value(), *g.costs()))
+    for a, b, what in zip(out[0], out[1], ("qpos", "K", "k", "deriv", "V", "v", "cost", "sel")):
+        exact(b, a, f"groups={G} {what}")
