@@ -78,6 +78,9 @@ __shared__ unsigned long long s_stamp_acc[STAMP_N], s_stamp_cnt[STAMP_N], s_stam
 #endif
 #define FOR_T(v, n) for (int v = T.tid; v < (n); v += T.nt)
 
+#ifndef KIN_SPLIT
+#define KIN_SPLIT 1
+#endif
 // below this many dofs the small factorizations run on lane 0 (fewer LDS round trips)
 constexpr int SERIAL_NV = 12;
 
@@ -184,6 +187,164 @@ __device__ inline void kin_chain_static(const M& m, const double* qpos, const do
   xquat[1] = xquat[2] = xquat[3] = 0;
 }
 
+// The same chain as kin_chain_static, split by dependency (compile-time models):
+//   1. lane 0 walks the quaternion chain alone (body quat products, joint
+//      rotations, normalisation) -- it never reads a position -- and parks
+//      every quaternion a rotation below needs;
+//   2. every vector rotation of the walk (body offsets, joint anchors, axes and
+//      post-rotation anchors) runs on a lane of its own;
+//   3. lane 0 walks the position chain: additions only.
+// Each output is produced by the same operations in the same order as in
+// kin_chain_static (and the oracle), only on another lane or earlier.
+template <class M>
+struct KinPlan {
+  // rotation r: vector kind (0 body_pos, 1 jnt_pos, 2 jnt_axis) and index, quaternion
+  // source (>= 0: parked slot, < 0: final quaternion of body -1 - src), role
+  // (0 body offset, 1 anchor, 2 axis, 3 post-rotation anchor) and its joint
+  static constexpr int MAXR = 64;
+  int nrot = 0, nslot = 0;
+  int vkind[MAXR] = {}, vidx[MAXR] = {}, qsrc[MAXR] = {}, role[MAXR] = {}, jnt[MAXR] = {};
+  int body_rot[M::nbody > 0 ? M::nbody : 1] = {};            // rotation of body i's offset
+  int anc_rot[M::njnt > 0 ? M::njnt : 1] = {}, ax_rot[M::njnt > 0 ? M::njnt : 1] = {},
+      tmp_rot[M::njnt > 0 ? M::njnt : 1] = {};
+  int qb_slot[M::nbody > 0 ? M::nbody : 1] = {};             // quat after the body quat (-1: not parked)
+  int qj_slot[M::njnt > 0 ? M::njnt : 1] = {};               // quat after joint j's rotation (-1)
+  bool ok = true;
+  constexpr KinPlan() {
+    auto add = [&](int kind, int idx, int q, int rl, int j) {
+      if (nrot >= MAXR) { ok = false; return 0; }
+      vkind[nrot] = kind; vidx[nrot] = idx; qsrc[nrot] = q; role[nrot] = rl; jnt[nrot] = j;
+      return nrot++;
+    };
+    for (int i = 0; i < M::nbody; i++) qb_slot[i] = -1;
+    for (int j = 0; j < M::njnt; j++) qj_slot[j] = anc_rot[j] = ax_rot[j] = tmp_rot[j] = -1;
+    for (int i = 1; i < M::nbody; i++) {
+      body_rot[i] = add(0, i, -1 - M::body_parentid[i], 0, -1);
+      int cur = -2;  // quaternion the next joint starts from: -2 = q_b (not parked yet)
+      for (int jj = 0; jj < M::body_jntnum[i]; jj++) {
+        const int j = M::body_jntadr[i] + jj, type = M::jnt_type[j];
+        if (type == JNT_FREE) { cur = -3; continue; }  // no rotations; later joints unsupported
+        if (cur == -3) { ok = false; continue; }
+        if (cur == -2) { qb_slot[i] = nslot++; cur = qb_slot[i]; }
+        anc_rot[j] = add(1, j, cur, 1, j);
+        ax_rot[j] = add(2, j, cur, 2, j);
+        if (type != JNT_SLIDE) {
+          qj_slot[j] = nslot++;
+          cur = qj_slot[j];
+          tmp_rot[j] = add(1, j, cur, 3, j);
+        }
+      }
+    }
+  }
+};
+
+template <class M>
+__device__ inline void kin_chain_par(const M& m, const Team& T, const double* qpos, const double* qloc, double* xpos,
+                                     double* xquat, double* xanchor, double* xaxis, double* scratch) {
+  static constexpr KinPlan<M> P{};
+  constexpr int NB = M::nbody;
+  double* QS = scratch;                 // parked quaternions, 4 per slot
+  double* RS = scratch + 4 * P.nslot;   // rotation results, 3 per rotation
+  // 1. quaternion chain (lane 0)
+  if (T.tid == 0) {
+    double xq[NB][4];
+    xq[0][0] = 1;
+    xq[0][1] = xq[0][2] = xq[0][3] = 0;
+    sfor<1, NB>(SLAM(ii) {
+      constexpr int i = SK(ii);
+      constexpr int pid = M::body_parentid[i];
+      double bquat[4];
+      ldm<4>(bquat, m.body_quat + 4 * i);
+      quat_mul(xq[i], xq[pid], bquat);
+      if constexpr (P.qb_slot[i] >= 0)
+        for (int k = 0; k < 4; k++) QS[4 * P.qb_slot[i] + k] = xq[i][k];
+      sfor<0, M::body_jntnum[i]>(SLAM(jj) {
+        constexpr int jid = M::body_jntadr[i] + SK(jj);
+        constexpr int type = M::jnt_type[jid], qadr = M::jnt_qposadr[jid];
+        if constexpr (type == JNT_FREE) {
+          for (int k = 0; k < 4; k++) xq[i][k] = qpos[qadr + 3 + k];
+          normalize4_sel(xq[i]);
+        } else if constexpr (type != JNT_SLIDE) {
+          double ql[4];
+          ldm<4>(ql, qloc + 4 * jid);
+          quat_mul(xq[i], xq[i], ql);
+          for (int k = 0; k < 4; k++) QS[4 * P.qj_slot[jid] + k] = xq[i][k];
+        }
+      });
+      normalize4_sel(xq[i]);
+      for (int k = 0; k < 4; k++) xquat[4 * i + k] = xq[i][k];
+    });
+    xquat[0] = 1;
+    xquat[1] = xquat[2] = xquat[3] = 0;
+  }
+  team_sync();
+  STAMP(22);
+  // 2. every rotation on a lane of its own
+  if (T.tid < P.nrot) {
+    int kind = 0, idx = 0, q = 0, rl = 0, j = 0;
+    sfor<0, P.nrot>(SLAM(rr) {  // lane -> plan entry as selects (no divergent branches)
+      constexpr int r = SK(rr);
+      const bool me = T.tid == r;
+      kind = me ? P.vkind[r] : kind;
+      idx = me ? P.vidx[r] : idx;
+      q = me ? P.qsrc[r] : q;
+      rl = me ? P.role[r] : rl;
+      j = me ? P.jnt[r] : j;
+    });
+    const double* v = kind == 0 ? m.body_pos + 3 * idx : (kind == 1 ? m.jnt_pos + 3 * idx : m.jnt_axis + 3 * idx);
+    const double* qq = q >= 0 ? QS + 4 * q : xquat + 4 * (-1 - q);
+    double vv[3], q4[4], r3[3];
+    ldm<3>(vv, v);
+    ldm<4>(q4, qq);
+    rot_vec_quat_sel(r3, vv, q4);
+    for (int k = 0; k < 3; k++) RS[3 * T.tid + k] = r3[k];
+    if (rl == 2)
+      for (int k = 0; k < 3; k++) xaxis[3 * j + k] = r3[k];
+  }
+  team_sync();
+  STAMP(23);
+  // 3. position chain (lane 0): the additions of kin_chain_static in its order
+  if (T.tid == 0) {
+    double xp[NB][3];
+    xp[0][0] = xp[0][1] = xp[0][2] = 0;
+    sfor<1, NB>(SLAM(ii) {
+      constexpr int i = SK(ii);
+      constexpr int pid = M::body_parentid[i];
+      const double* tmp = RS + 3 * P.body_rot[i];
+      xp[i][0] = xp[pid][0] + tmp[0];
+      xp[i][1] = xp[pid][1] + tmp[1];
+      xp[i][2] = xp[pid][2] + tmp[2];
+      sfor<0, M::body_jntnum[i]>(SLAM(jj) {
+        constexpr int jid = M::body_jntadr[i] + SK(jj);
+        constexpr int type = M::jnt_type[jid], qadr = M::jnt_qposadr[jid];
+        if constexpr (type == JNT_FREE) {
+          double jaxis[3];
+          ldm<3>(jaxis, m.jnt_axis + 3 * jid);
+          for (int k = 0; k < 3; k++) xp[i][k] = qpos[qadr + k];
+          for (int k = 0; k < 3; k++) { xanchor[3 * jid + k] = xp[i][k]; xaxis[3 * jid + k] = jaxis[k]; }
+        } else {
+          const double* ra = RS + 3 * P.anc_rot[jid];
+          double anc[3];
+          anc[0] = ra[0] + xp[i][0]; anc[1] = ra[1] + xp[i][1]; anc[2] = ra[2] + xp[i][2];
+          if constexpr (type == JNT_SLIDE) {
+            const double* ax = RS + 3 * P.ax_rot[jid];
+            const double dq = qpos[qadr] - m.qpos0[qadr];
+            xp[i][0] += ax[0] * dq; xp[i][1] += ax[1] * dq; xp[i][2] += ax[2] * dq;
+          } else {
+            const double* tmp2 = RS + 3 * P.tmp_rot[jid];
+            xp[i][0] = anc[0] - tmp2[0];
+            xp[i][1] = anc[1] - tmp2[1];
+            xp[i][2] = anc[2] - tmp2[2];
+          }
+          for (int k = 0; k < 3; k++) xanchor[3 * jid + k] = anc[k];
+        }
+      });
+      for (int k = 0; k < 3; k++) xpos[3 * i + k] = xp[i][k];
+    });
+    xpos[0] = xpos[1] = xpos[2] = 0;
+  }
+}
+
 __device__ inline void kinematics(const auto& m, const auto& L, const auto& C, const Team& T) {
   double* qpos = T.w + L.qpos;
   double* xpos = T.w + L.xpos;
@@ -213,7 +374,12 @@ __device__ inline void kinematics(const auto& m, const auto& L, const auto& C, c
   // the kinematic chain: lane 0
   using MT = std::remove_cvref_t<decltype(m)>;
   if constexpr (StaticModel<MT>) {
-    if (T.tid == 0) kin_chain_static(m, qpos, qloc, xpos, xquat, xanchor, xaxis);
+    static constexpr KinPlan<MT> plan{};
+    // the split chain needs its scratch in the union (dead until collision) and a lane per rotation
+    if constexpr (plan.ok && 4 * plan.nslot + 3 * plan.nrot <= 12 * MT::nbody + 10 * MT::nv && KIN_SPLIT)
+      kin_chain_par(m, T, qpos, qloc, xpos, xquat, xanchor, xaxis, T.w + L.con);
+    else if (T.tid == 0)
+      kin_chain_static(m, qpos, qloc, xpos, xquat, xanchor, xaxis);
   } else if (T.tid == 0) {
     xpos[0] = xpos[1] = xpos[2] = 0;
     xquat[0] = 1; xquat[1] = xquat[2] = xquat[3] = 0;
@@ -1754,8 +1920,6 @@ __device__ inline void step_dual(const auto& m, const auto& L, const auto& C, co
     transmission(m, L, T);
     crb(m, L, C, X, T);
     STAMP(2);
-    factor_ld(m, X, T, T.w + L.qM, T.w + L.qLD, T.w + L.qLDinv, T.c + C.ftmp);
-    STAMP(3);
   } else {
     make_constraint(m, L, C, X, T);
     STAMPB(35);
@@ -1763,23 +1927,36 @@ __device__ inline void step_dual(const auto& m, const auto& L, const auto& C, co
   __syncthreads();
   STAMP(26);
   STAMPB(36);
+  // the L'DL factor of M runs on the helper beside the com velocities and RNE
+  // (nothing on the primary reads it before the acceleration stage)
   if (A) {
     fwd_velocity(m, L, C, T, 1);
     STAMP(6);
   } else {
     fwd_velocity(m, L, C, T, 2);
     STAMPB(37);
-    if (eul) euler_prefactor(m, L, C, X, T);
-    STAMPB(38);
+    factor_ld(m, X, T, T.w + L.qM, T.w + L.qLD, T.w + L.qLDinv, T.c + C.ftmp);
+    STAMPB(42);
   }
   __syncthreads();
   STAMP(27);
   STAMPB(39);
+  // the Euler factor of M + h D on the helper beside the constraint solve
   if (A) {
     fwd_acceleration(m, L, X, T);
     STAMP(7);
     fwd_constraint(m, L, C, X, T, m.opt_iterations, m.opt_tolerance);
     STAMP(8);
+  } else if (eul) {
+    euler_prefactor(m, L, C, X, T);
+    STAMPB(38);
+  }
+  __syncthreads();
+  STAMP(29);
+  STAMPB(43);
+  if (A) {
+    // (after the barrier: a reset recomputes the forward pass on this wave
+    // alone, and its factorisations share scratch with the helper's)
     bool reset = false;
     if (any_bad(T, C, T.w + L.qacc, m.nv)) {
       reset = true;

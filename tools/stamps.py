@@ -7,13 +7,14 @@ sys.path.insert(0, os.path.join(ROOT, "ilqg-mujoco_amd"))
 import ilqg_amd as ia, workloads
 NAMES = {0: "kinematics", 1: "com_pos", 2: "trn+crb", 3: "factor_ld(M)", 4: "collision", 5: "make_constraint",
          6: "fwd_velocity", 7: "fwd_acceleration", 8: "fwd_constraint(newton)", 9: "integrator",
-         11: " kin: joint quats", 12: " kin: lane-0 chain", 13: " kin: body frames", 14: " nt: chol solve",
+         11: " kin: joint quats", 12: " kin: lane-0 chain / position chain", 13: " kin: body frames", 14: " nt: chol solve",
          15: " nt: Mv,Jv", 16: " nt: linesearch", 17: " nt: update", 18: " nt: cost+grad", 19: " nt: hessian",
-         20: "empty sync", 21: "empty sync 2",
+         20: "empty sync", 21: "empty sync 2", 22: " kin: quat chain (lane 0)", 23: " kin: rotations (lanes)",
          24: "A: barrier 1 (wait for B)", 25: "A: barrier 2", 26: "A: barrier 3", 27: "A: barrier 4", 28: "A: barrier 5",
          32: "B: barrier 1 (wait for A kinematics)", 33: "B: collision", 34: "B: barrier 2", 35: "B: make_constraint",
-         36: "B: barrier 3", 37: "B: passive+aref", 38: "B: euler prefactor", 39: "B: barrier 4 (A accel..euler)",
-         40: "B: barrier 5", 41: "B: control law + record"}
+         36: "B: barrier 3", 37: "B: passive+aref", 38: "B: euler prefactor", 39: "B: barrier 4 (A com vel + RNE)",
+         40: "B: barrier 6 (end of step)", 41: "B: control law + record", 42: "B: factor_ld(M)", 43: "B: barrier 5",
+         29: "A: barrier 5b (Euler factor)"}
 L = ia.lib()
 acc = (ctypes.c_ulonglong * 48)(); cnt = (ctypes.c_ulonglong * 48)()
 m = ia.Model.load(workloads.model_file(sys.argv[1] if len(sys.argv) > 1 else "hopper"))
@@ -27,7 +28,7 @@ for what, fn in (("rollout (1 seed)", g.forward_pass), ("fd sweep", g.fd_sweep))
     fn(); g.synchronize()
     tm = g.timing()
     L.ilqg_debug_stamps(acc, cnt, 1)
-    tot = sum(acc[i] for i in list(range(10)) + list(range(24, 29)))
+    tot = sum(acc[i] for i in list(range(10)) + list(range(24, 30)))
     ms = sum(v[0] for v in tm.values())
     print(f"== {what}: block 0, lane 0, total {tot} ticks (wave-0 stages + barriers); kernel time {ms:.3f} ms "
           f"-> {tot / (ms * 1e3):.0f} ticks/us if the stages were all of it")
