@@ -124,6 +124,18 @@ __device__ __forceinline__ void normalize4_sel(double* q) {
   q[3] = tiny ? 0.0 : (scale ? s3 : q[3]);
 }
 
+// normalize4_sel when the squared norm already decides that q stays as it is:
+// |fl(sqrt(s)) - 1| <= MINVAL exactly for s in [S_LO, S_HI] (sqrt correctly
+// rounded and monotone; the bounds are the ends of that run of doubles,
+// tests/test_oracle_physics.py::test_normalize4_window).  Unit quaternion
+// products land there almost always, so the chain skips the sqrt and divide.
+constexpr double NORM4_S_LO = 0x1.fffffffffffeep-1, NORM4_S_HI = 0x1.0000000000009p+0;
+__device__ __forceinline__ void normalize4_fast(double* q) {
+  const double s = q[0] * q[0] + q[1] * q[1] + q[2] * q[2] + q[3] * q[3];
+  if (s >= NORM4_S_LO && s <= NORM4_S_HI) return;
+  normalize4_sel(q);
+}
+
 // The kinematic chain of a compile-time model on lane 0 with every body frame
 // in registers (no store->load round trip through LDS between a body and its
 // children): the tree walk is unrolled with compile-time parent indices and
@@ -210,6 +222,18 @@ struct KinPlan {
   int qb_slot[M::nbody > 0 ? M::nbody : 1] = {};             // quat after the body quat (-1: not parked)
   int qj_slot[M::njnt > 0 ? M::njnt : 1] = {};               // quat after joint j's rotation (-1)
   bool ok = true;
+  struct Packed {
+    unsigned long long w[MAXR / 4];
+    __host__ __device__ constexpr unsigned long long operator[](int i) const { return w[i]; }
+  };
+  constexpr Packed packed() const {
+    Packed p{};
+    for (int r = 0; r < nrot; r++) {
+      const unsigned long long d = (unsigned long long)(vkind[r] | (vidx[r] << 2) | ((qsrc[r] + 64) << 9));
+      p.w[r / 4] |= d << (16 * (r % 4));
+    }
+    return p;
+  }
   constexpr KinPlan() {
     auto add = [&](int kind, int idx, int q, int rl, int j) {
       if (nrot >= MAXR) { ok = false; return 0; }
@@ -229,6 +253,7 @@ struct KinPlan {
         anc_rot[j] = add(1, j, cur, 1, j);
         ax_rot[j] = add(2, j, cur, 2, j);
         if (type != JNT_SLIDE) {
+          if (nslot >= 63 || j >= 127 || i >= 64) ok = false;
           qj_slot[j] = nslot++;
           cur = qj_slot[j];
           tmp_rot[j] = add(1, j, cur, 3, j);
@@ -263,7 +288,7 @@ __device__ inline void kin_chain_par(const M& m, const Team& T, const double* qp
         constexpr int type = M::jnt_type[jid], qadr = M::jnt_qposadr[jid];
         if constexpr (type == JNT_FREE) {
           for (int k = 0; k < 4; k++) xq[i][k] = qpos[qadr + 3 + k];
-          normalize4_sel(xq[i]);
+          normalize4_fast(xq[i]);
         } else if constexpr (type != JNT_SLIDE) {
           double ql[4];
           ldm<4>(ql, qloc + 4 * jid);
@@ -271,7 +296,7 @@ __device__ inline void kin_chain_par(const M& m, const Team& T, const double* qp
           for (int k = 0; k < 4; k++) QS[4 * P.qj_slot[jid] + k] = xq[i][k];
         }
       });
-      normalize4_sel(xq[i]);
+      normalize4_fast(xq[i]);
       for (int k = 0; k < 4; k++) xquat[4 * i + k] = xq[i][k];
     });
     xquat[0] = 1;
@@ -281,16 +306,15 @@ __device__ inline void kin_chain_par(const M& m, const Team& T, const double* qp
   STAMP(22);
   // 2. every rotation on a lane of its own
   if (T.tid < P.nrot) {
-    int kind = 0, idx = 0, q = 0, rl = 0, j = 0;
-    sfor<0, P.nrot>(SLAM(rr) {  // lane -> plan entry as selects (no divergent branches)
-      constexpr int r = SK(rr);
-      const bool me = T.tid == r;
-      kind = me ? P.vkind[r] : kind;
-      idx = me ? P.vidx[r] : idx;
-      q = me ? P.qsrc[r] : q;
-      rl = me ? P.role[r] : rl;
-      j = me ? P.jnt[r] : j;
-    });
+    // lane -> plan entry: 16-bit descriptors packed 4 per 64-bit immediate
+    // (kind 2 bits | vector index 7 bits | quaternion source + 64 7 bits)
+    static constexpr auto D = P.packed();
+    const int l = T.tid;
+    unsigned long long w = D[0];
+    sfor<1, (P.nrot + 3) / 4>(SLAM(kk) { w = (l >> 2) == SK(kk) ? D[SK(kk)] : w; });
+    const unsigned d = (unsigned)(w >> (16 * (l & 3))) & 0xffffu;
+    const int kind = d & 3, idx = (d >> 2) & 127, q = (int)(d >> 9) - 64, j = idx;
+    const int rl = kind == 2 ? 2 : 0;
     const double* v = kind == 0 ? m.body_pos + 3 * idx : (kind == 1 ? m.jnt_pos + 3 * idx : m.jnt_axis + 3 * idx);
     const double* qq = q >= 0 ? QS + 4 * q : xquat + 4 * (-1 - q);
     double vv[3], q4[4], r3[3];

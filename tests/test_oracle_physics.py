@@ -170,3 +170,28 @@ def test_iterate_counts_cout_sink(ia, ora):
     il.set_dinit(d)
     il.iterate()
     assert il.arrays()["cout_lines"] == 40
+
+
+def test_normalize4_window():
+    """dcoop.h normalize4_fast: for the squared norm s, the window
+    [0x1.fffffffffffeep-1, 0x1.0000000000009p+0] is exactly the set where
+    mju_normalize4 leaves q unchanged (not tiny, |sqrt(s) - 1| <= mjMINVAL)"""
+    import numpy as np
+    lo, hi = float.fromhex("0x1.fffffffffffeep-1"), float.fromhex("0x1.0000000000009p+0")
+    minval = 1e-15
+
+    def unchanged(s):
+        n = np.sqrt(np.float64(s))
+        return not (n < minval) and not (abs(n - 1.0) > minval)
+
+    for edge in (lo, hi, 1.0):
+        x = np.float64(edge)
+        for _ in range(64):
+            x = np.nextafter(x, 0.0)
+        for _ in range(128):
+            assert unchanged(x) == (lo <= x <= hi), float(x).hex()
+            x = np.nextafter(x, 2.0)
+    # elsewhere the window is only required to be sound (outside it the full
+    # normalisation runs, which leaves e.g. a NaN quaternion as it is)
+    for s in (0.0, 1e-40, 0.25, 4.0, float("nan"), float("inf")):
+        assert not (lo <= s <= hi) or unchanged(s)
