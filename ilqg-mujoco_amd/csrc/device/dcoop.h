@@ -272,15 +272,20 @@ __device__ inline void kin_chain_par(const M& m, const Team& T, const double* qp
   double* RS = scratch + 4 * P.nslot;   // rotation results, 3 per rotation
   // 1. quaternion chain (lane 0)
   if (T.tid == 0) {
+    // every LDS operand of the walk is loaded up front: one wait, none inside the walk
+    double bq[NB][4], ql[M::njnt > 0 ? M::njnt : 1][4];
+    sfor<1, NB>(SLAM(ii) { ldm<4>(bq[SK(ii)], m.body_quat + 4 * SK(ii)); });
+    sfor<0, M::njnt>(SLAM(jj) {
+      constexpr int j = SK(jj);
+      if constexpr (M::jnt_type[j] != JNT_FREE && M::jnt_type[j] != JNT_SLIDE) ldm<4>(ql[j], qloc + 4 * j);
+    });
     double xq[NB][4];
     xq[0][0] = 1;
     xq[0][1] = xq[0][2] = xq[0][3] = 0;
     sfor<1, NB>(SLAM(ii) {
       constexpr int i = SK(ii);
       constexpr int pid = M::body_parentid[i];
-      double bquat[4];
-      ldm<4>(bquat, m.body_quat + 4 * i);
-      quat_mul(xq[i], xq[pid], bquat);
+      quat_mul(xq[i], xq[pid], bq[i]);
       if constexpr (P.qb_slot[i] >= 0)
         for (int k = 0; k < 4; k++) QS[4 * P.qb_slot[i] + k] = xq[i][k];
       sfor<0, M::body_jntnum[i]>(SLAM(jj) {
@@ -290,9 +295,7 @@ __device__ inline void kin_chain_par(const M& m, const Team& T, const double* qp
           for (int k = 0; k < 4; k++) xq[i][k] = qpos[qadr + 3 + k];
           normalize4_fast(xq[i]);
         } else if constexpr (type != JNT_SLIDE) {
-          double ql[4];
-          ldm<4>(ql, qloc + 4 * jid);
-          quat_mul(xq[i], xq[i], ql);
+          quat_mul(xq[i], xq[i], ql[jid]);
           for (int k = 0; k < 4; k++) QS[4 * P.qj_slot[jid] + k] = xq[i][k];
         }
       });
@@ -315,8 +318,12 @@ __device__ inline void kin_chain_par(const M& m, const Team& T, const double* qp
     const unsigned d = (unsigned)(w >> (16 * (l & 3))) & 0xffffu;
     const int kind = d & 3, idx = (d >> 2) & 127, q = (int)(d >> 9) - 64, j = idx;
     const int rl = kind == 2 ? 2 : 0;
-    const double* v = kind == 0 ? m.body_pos + 3 * idx : (kind == 1 ? m.jnt_pos + 3 * idx : m.jnt_axis + 3 * idx);
-    const double* qq = q >= 0 ? QS + 4 * q : xquat + 4 * (-1 - q);
+    // integer offsets from one base each (a select between pointers becomes a
+    // lookup table in scratch and a flat load)
+    const int d1 = (int)(m.jnt_pos - m.body_pos), d2 = (int)(m.jnt_axis - m.body_pos);
+    const double* v = m.body_pos + (3 * idx + (kind == 1 ? d1 : 0) + (kind == 2 ? d2 : 0));
+    const int dq = (int)(xquat - QS);
+    const double* qq = QS + (q >= 0 ? 4 * q : dq + 4 * (-1 - q));
     double vv[3], q4[4], r3[3];
     ldm<3>(vv, v);
     ldm<4>(q4, qq);
@@ -329,12 +336,14 @@ __device__ inline void kin_chain_par(const M& m, const Team& T, const double* qp
   STAMP(23);
   // 3. position chain (lane 0): the additions of kin_chain_static in its order
   if (T.tid == 0) {
+    double R[P.nrot][3];
+    sfor<0, P.nrot>(SLAM(rr) { ldm<3>(R[SK(rr)], RS + 3 * SK(rr)); });
     double xp[NB][3];
     xp[0][0] = xp[0][1] = xp[0][2] = 0;
     sfor<1, NB>(SLAM(ii) {
       constexpr int i = SK(ii);
       constexpr int pid = M::body_parentid[i];
-      const double* tmp = RS + 3 * P.body_rot[i];
+      const double* tmp = R[P.body_rot[i]];
       xp[i][0] = xp[pid][0] + tmp[0];
       xp[i][1] = xp[pid][1] + tmp[1];
       xp[i][2] = xp[pid][2] + tmp[2];
@@ -347,15 +356,15 @@ __device__ inline void kin_chain_par(const M& m, const Team& T, const double* qp
           for (int k = 0; k < 3; k++) xp[i][k] = qpos[qadr + k];
           for (int k = 0; k < 3; k++) { xanchor[3 * jid + k] = xp[i][k]; xaxis[3 * jid + k] = jaxis[k]; }
         } else {
-          const double* ra = RS + 3 * P.anc_rot[jid];
+          const double* ra = R[P.anc_rot[jid]];
           double anc[3];
           anc[0] = ra[0] + xp[i][0]; anc[1] = ra[1] + xp[i][1]; anc[2] = ra[2] + xp[i][2];
           if constexpr (type == JNT_SLIDE) {
-            const double* ax = RS + 3 * P.ax_rot[jid];
+            const double* ax = R[P.ax_rot[jid]];
             const double dq = qpos[qadr] - m.qpos0[qadr];
             xp[i][0] += ax[0] * dq; xp[i][1] += ax[1] * dq; xp[i][2] += ax[2] * dq;
           } else {
-            const double* tmp2 = RS + 3 * P.tmp_rot[jid];
+            const double* tmp2 = R[P.tmp_rot[jid]];
             xp[i][0] = anc[0] - tmp2[0];
             xp[i][1] = anc[1] - tmp2[1];
             xp[i][2] = anc[2] - tmp2[2];
@@ -779,14 +788,9 @@ __device__ inline void collision(const auto& m, const auto& L, const auto& C, co
       ldm<3>(pos2, gxpos + 3 * gb);
       ldm<9>(mat2, gxmat + 9 * gb);
       ldm<3>(sz2, m.geom_size + 3 * gb);
-      RCon tmp[2];
-      n = narrow(m, m.geom_type[ga], m.geom_type[gb], pos1, mat1, sz1, pos2, mat2, sz2, margin, tmp);
-      for (int k = 0; k < n; k++) {
-        double* pc = pcon + 14 * p + 7 * k;
-        pc[0] = tmp[k].dist;
-        pc[1] = tmp[k].pos[0]; pc[2] = tmp[k].pos[1]; pc[3] = tmp[k].pos[2];
-        pc[4] = tmp[k].n[0]; pc[5] = tmp[k].n[1]; pc[6] = tmp[k].n[2];
-      }
+      // contacts straight into the pair's LDS records
+      n = narrow(m, m.geom_type[ga], m.geom_type[gb], pos1, mat1, sz1, pos2, mat2, sz2, margin,
+                 LdsConSink{pcon + 14 * p});
     }
     pcnt[p] = n;
   }

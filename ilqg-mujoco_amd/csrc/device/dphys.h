@@ -555,57 +555,75 @@ __device__ inline void jac_rot(const DevModel& m, const WsLayout& L, const Lane&
   }
 }
 
-// ---- narrow phase (register contacts: dist, pos[3], frame[0..2]) ----
+// ---- narrow phase (contacts: dist, pos[3], frame[0..2]) ----
+// Contact k goes to a sink: RConSink (a private array, lane kernels) or
+// LdsConSink (7-double records in LDS, cooperative kernels -- a runtime
+// contact index into a private array would put it in scratch memory).
 struct RCon {
   double dist, pos[3], n[3];
 };
-__device__ inline int sphere_sphere(RCon* c, double margin, const double* p1, double r1, const double* p2, double r2) {
+struct RConSink {
+  RCon* c;
+  __device__ __forceinline__ void put(int k, double d, const double* p, const double* n) const {
+    c[k].dist = d;
+    c[k].pos[0] = p[0]; c[k].pos[1] = p[1]; c[k].pos[2] = p[2];
+    c[k].n[0] = n[0]; c[k].n[1] = n[1]; c[k].n[2] = n[2];
+  }
+};
+struct LdsConSink {
+  double* rec;  // contact k at rec + 7k: dist, pos[3], n[3]
+  __device__ __forceinline__ void put(int k, double d, const double* p, const double* n) const {
+    double* r = rec + 7 * k;
+    r[0] = d;
+    r[1] = p[0]; r[2] = p[1]; r[3] = p[2];
+    r[4] = n[0]; r[5] = n[1]; r[6] = n[2];
+  }
+};
+template <class S>
+__device__ __forceinline__ int sphere_sphere(const S& out, int k, double margin, const double* p1, double r1,
+                                             const double* p2, double r2) {
   double axis[3] = {p2[0] - p1[0], p2[1] - p1[1], p2[2] - p1[2]};
   double dist = normalize3(axis) - r1 - r2;
-  double s;
   if (dist > margin) return 0;
-  c->dist = dist;
-  c->n[0] = axis[0]; c->n[1] = axis[1]; c->n[2] = axis[2];
-  s = r1 + dist / 2;
-  c->pos[0] = p1[0] + axis[0] * s;
-  c->pos[1] = p1[1] + axis[1] * s;
-  c->pos[2] = p1[2] + axis[2] * s;
+  const double s = r1 + dist / 2;
+  const double pos[3] = {p1[0] + axis[0] * s, p1[1] + axis[1] * s, p1[2] + axis[2] * s};
+  out.put(k, dist, pos, axis);
   return 1;
 }
-__device__ inline int plane_sphere(RCon* c, double margin, const double* pos1, const double* mat1, const double* p2, double r2) {
+template <class S>
+__device__ __forceinline__ int plane_sphere(const S& out, int k, double margin, const double* pos1,
+                                            const double* mat1, const double* p2, double r2) {
   double n[3] = {mat1[2], mat1[5], mat1[8]};
   double tmp[3] = {p2[0] - pos1[0], p2[1] - pos1[1], p2[2] - pos1[2]};
-  double cdist = dot3(tmp, n), s;
+  double cdist = dot3(tmp, n);
   if (cdist > margin + r2) return 0;
-  c->dist = cdist - r2;
-  c->n[0] = n[0]; c->n[1] = n[1]; c->n[2] = n[2];
-  s = -c->dist / 2 - r2;
-  c->pos[0] = p2[0] + n[0] * s;
-  c->pos[1] = p2[1] + n[1] * s;
-  c->pos[2] = p2[2] + n[2] * s;
+  const double dist = cdist - r2;
+  const double s = -dist / 2 - r2;
+  const double pos[3] = {p2[0] + n[0] * s, p2[1] + n[1] * s, p2[2] + n[2] * s};
+  out.put(k, dist, pos, n);
   return 1;
 }
-template <class M>
-__device__ inline int narrow(const M& m, int t1, int t2, const double* pos1, const double* mat1,
-                             const double* sz1, const double* pos2, const double* mat2, const double* sz2,
-                             double margin, RCon* con) {
-  if (t1 == GEOM_PLANE && t2 == GEOM_SPHERE) return plane_sphere(con, margin, pos1, mat1, pos2, sz2[0]);
+template <class M, class S>
+__device__ __forceinline__ int narrow(const M& m, int t1, int t2, const double* pos1, const double* mat1,
+                                      const double* sz1, const double* pos2, const double* mat2, const double* sz2,
+                                      double margin, const S& out) {
+  if (t1 == GEOM_PLANE && t2 == GEOM_SPHERE) return plane_sphere(out, 0, margin, pos1, mat1, pos2, sz2[0]);
   if (t1 == GEOM_PLANE && t2 == GEOM_CAPSULE) {
     double seg[3] = {mat2[2] * sz2[1], mat2[5] * sz2[1], mat2[8] * sz2[1]}, p[3];
     int n1, n2;
     p[0] = pos2[0] + seg[0]; p[1] = pos2[1] + seg[1]; p[2] = pos2[2] + seg[2];
-    n1 = plane_sphere(con, margin, pos1, mat1, p, sz2[0]);
+    n1 = plane_sphere(out, 0, margin, pos1, mat1, p, sz2[0]);
     p[0] = pos2[0] - seg[0]; p[1] = pos2[1] - seg[1]; p[2] = pos2[2] - seg[2];
-    n2 = plane_sphere(con + n1, margin, pos1, mat1, p, sz2[0]);
+    n2 = plane_sphere(out, n1, margin, pos1, mat1, p, sz2[0]);
     return n1 + n2;
   }
-  if (t1 == GEOM_SPHERE && t2 == GEOM_SPHERE) return sphere_sphere(con, margin, pos1, sz1[0], pos2, sz2[0]);
+  if (t1 == GEOM_SPHERE && t2 == GEOM_SPHERE) return sphere_sphere(out, 0, margin, pos1, sz1[0], pos2, sz2[0]);
   if (t1 == GEOM_SPHERE && t2 == GEOM_CAPSULE) {
     double ax[3] = {mat2[2], mat2[5], mat2[8]}, dif[3], p[3], x;
     dif[0] = pos1[0] - pos2[0]; dif[1] = pos1[1] - pos2[1]; dif[2] = pos1[2] - pos2[2];
     x = clipd(dot3(ax, dif), -sz2[1], sz2[1]);
     p[0] = pos2[0] + ax[0] * x; p[1] = pos2[1] + ax[1] * x; p[2] = pos2[2] + ax[2] * x;
-    return sphere_sphere(con, margin, pos1, sz1[0], p, sz2[0]);
+    return sphere_sphere(out, 0, margin, pos1, sz1[0], p, sz2[0]);
   }
   if (t1 == GEOM_CAPSULE && t2 == GEOM_CAPSULE) {
     double a1[3] = {mat1[2] * sz1[1], mat1[5] * sz1[1], mat1[8] * sz1[1]};
@@ -624,17 +642,17 @@ __device__ inline int narrow(const M& m, int t1, int t2, const double* pos1, con
       else if (x2 < -1) { x2 = -1; x1 = clipd((u + mb) / ma, -1, 1); }
       v1[0] = pos1[0] + a1[0] * x1; v1[1] = pos1[1] + a1[1] * x1; v1[2] = pos1[2] + a1[2] * x1;
       v2[0] = pos2[0] + a2[0] * x2; v2[1] = pos2[1] + a2[1] * x2; v2[2] = pos2[2] + a2[2] * x2;
-      return sphere_sphere(con, margin, v1, sz1[0], v2, sz2[0]);
+      return sphere_sphere(out, 0, margin, v1, sz1[0], v2, sz2[0]);
     } else {
       int n1, n2;
       v1[0] = pos1[0] + a1[0]; v1[1] = pos1[1] + a1[1]; v1[2] = pos1[2] + a1[2];
       x2 = clipd((v - mb) / mc, -1, 1);
       v2[0] = pos2[0] + a2[0] * x2; v2[1] = pos2[1] + a2[1] * x2; v2[2] = pos2[2] + a2[2] * x2;
-      n1 = sphere_sphere(con, margin, v1, sz1[0], v2, sz2[0]);
+      n1 = sphere_sphere(out, 0, margin, v1, sz1[0], v2, sz2[0]);
       v1[0] = pos1[0] - a1[0]; v1[1] = pos1[1] - a1[1]; v1[2] = pos1[2] - a1[2];
       x2 = clipd((v + mb) / mc, -1, 1);
       v2[0] = pos2[0] + a2[0] * x2; v2[1] = pos2[1] + a2[1] * x2; v2[2] = pos2[2] + a2[2] * x2;
-      n2 = sphere_sphere(con + n1, margin, v1, sz1[0], v2, sz2[0]);
+      n2 = sphere_sphere(out, n1, margin, v1, sz1[0], v2, sz2[0]);
       return n1 + n2;
     }
   }
@@ -673,7 +691,7 @@ __device__ inline void collision(const DevModel& m, const WsLayout& L, const Lan
       ld<9>(mat2, gxmat + 9 * gb);
       ldm<3>(sz2, m.geom_size + 3 * gb);
       RCon tmp[2];
-      int n = narrow(m, m.geom_type[ga], m.geom_type[gb], pos1, mat1, sz1, pos2, mat2, sz2, margin, tmp);
+      int n = narrow(m, m.geom_type[ga], m.geom_type[gb], pos1, mat1, sz1, pos2, mat2, sz2, margin, RConSink{tmp});
       if (!n) continue;
       double gap = maxd(m.geom_gap[ga], m.geom_gap[gb]);
       double s1 = m.geom_solmix[ga], s2 = m.geom_solmix[gb], mix;
