@@ -1457,6 +1457,12 @@ __device__ __forceinline__ double lane_sum(double s0, double v, int n) {
   for (int i = 0; i < n; i++) s0 += bcast(v, i);
   return s0;
 }
+// the same ordered sum over the lanes of a (wave-uniform) mask only: lanes
+// outside it hold -0.0, and x + (-0.0) == x for every x, so skipping them is exact
+__device__ __forceinline__ double lane_sum_mask(double s0, double v, unsigned long long mask) {
+  for (unsigned long long mm = mask; mm; mm &= mm - 1) s0 += bcast(v, __builtin_ctzll(mm));
+  return s0;
+}
 
 // constraint_update for row registers: returns the cost (uniform) and the
 // active-row mask; with `full` also force/state and qfrc_constraint = J' force
@@ -1476,16 +1482,22 @@ __device__ inline double cu_fast(const auto& m, const auto& L, const Team& T, do
     TSYNC();
     double* J = T.w + L.efc_J;
     double* qc = T.w + L.qfrc_con;
+    // rows with zero force add J * 0 = +-0 to a sum that is never -0 (it starts
+    // at +0): skipping them is exact
+    const unsigned long long am = __ballot(act);
     FOR_T(j, nv) {
       double s = 0;
-      for (int i = 0; i < ne; i++) s += J[i * nv + j] * force[i];
+      for (unsigned long long mm = am; mm; mm &= mm - 1) {
+        const int i = __builtin_ctzll(mm);
+        s += J[i * nv + j] * force[i];
+      }
       qc[j] = s;
     }
     TSYNC();
   }
   mask = __ballot(act);
   const double tv = act ? 0.5 * Di * jr * jr : -0.0;
-  return lane_sum(0.0, tv, ne);
+  return lane_sum_mask(0.0, tv, mask);
 }
 
 // 0.5 * sum_j (Ma_j - qfs_j)(qacc_j - qas_j), every lane (uniform)
@@ -1578,17 +1590,24 @@ __device__ inline void fwd_constraint_fast(const auto& m, const auto& L, const a
         double g1 = 0, g2 = 0, d1, d2, lo = 0, hi = -1;
         for (int j = 0; j < nv; j++) g1 += search[j] * (Ma[j] - qfs[j]);
         for (int j = 0; j < nv; j++) g2 += search[j] * Mv[j];
+        // active rows only (the others add -0.0); d2 depends on the active set
+        // alone, so it is summed again only when the set changes
+        unsigned long long pmask = 0;
+        bool have = false;
+        double d2c = 0;
+        const double c2 = Di * jv * jv;
         auto eval = [&](double a) {
           const double x = jr + a * jv;
           const bool on = row && x < 0;
-          const double c1 = on ? Di * x * jv : -0.0;
-          const double c2 = on ? Di * jv * jv : -0.0;
-          d1 = g1 + g2 * a;
-          d2 = g2;
-          for (int i = 0; i < ne; i++) {
-            d1 += bcast(c1, i);
-            d2 += bcast(c2, i);
+          const double c1 = Di * x * jv;
+          const unsigned long long am = __ballot(on);
+          d1 = lane_sum_mask(g1 + g2 * a, c1, am);
+          if (!have || am != pmask) {
+            d2c = lane_sum_mask(g2, c2, am);
+            pmask = am;
+            have = true;
           }
+          d2 = d2c;
         };
         eval(0.0);
         if (!(d1 >= 0)) {
