@@ -1507,18 +1507,21 @@ __device__ inline double gauss_u(int nv, const double* Ma, const double* qfs, co
   return 0.5 * g;
 }
 
-__device__ inline void hessian_build_fast(const auto& m, const auto& L, const Team& T, double* H) {
-  const int nv = m.nv, ne = T.iw[L.nefc];
+// amask: the active rows (efc_state != 0) as a ballot, walked in ascending order
+__device__ inline void hessian_build_fast(const auto& m, const auto& L, const Team& T, double* H,
+                                          unsigned long long amask) {
+  const int nv = m.nv;
   double* J = T.w + L.efc_J;
   double* D = T.w + L.efc_D;
   double* qM = T.w + L.qM;
-  int* state = T.iw + L.efc_state;
   FOR_T(e, nv * nv) {
     int r = e / nv, c = e % nv;
     if (c <= r) {
       double h = 0;
-      for (int i = 0; i < ne; i++)
-        if (state[i]) h += J[i * nv + r] * D[i] * J[i * nv + c];
+      for (unsigned long long mm = amask; mm; mm &= mm - 1) {
+        const int i = __builtin_ctzll(mm);
+        h += J[i * nv + r] * D[i] * J[i * nv + c];
+      }
       H[e] = qM[e] + h;
     }
   }
@@ -1568,7 +1571,7 @@ __device__ inline void fwd_constraint_fast(const auto& m, const auto& L, const a
   }
   double cost = gauss_u(nv, Ma, qfs, qacc, qas) + cu_fast(m, L, T, jr, Di, true, mask);
   FOR_T(j, nv) grad[j] = (Ma[j] - qfs[j]) - qc[j];
-  hessian_build_fast(m, L, T, H);
+  hessian_build_fast(m, L, T, H, mask);
   cholesky_rows(nv, T.tid, H);
   hmask = mask;
   int iter = 0;
@@ -1645,7 +1648,7 @@ __device__ inline void fwd_constraint_fast(const auto& m, const auto& L, const a
     STAMP(18);
     if (improvement < tol || gradient < tol) break;
     if (mask != hmask) {
-      hessian_build_fast(m, L, T, H);
+      hessian_build_fast(m, L, T, H, mask);
       cholesky_rows(nv, T.tid, H);
       hmask = mask;
     }
