@@ -11,7 +11,8 @@ import collections, csv, json, re, sys
 # kernel-name alternatives per group (model-specific *_s, two-wave *2*, generic *_coop)
 GROUPS = {"rollout": (("k_rollout2_s", "k_rollout_s", "k_rollout2_coop", "k_rollout_coop"),),
           "fd_sweep": (("k_fd_centre_s", "k_fd_centre_coop"), ("k_fd_cols_s", "k_fd_cols_coop")),
-          "backward": (("k_backward",),), "select": (("k_select",),)}
+          "backward": (("k_backward",),), "select": (("k_select",),),
+          "fd_backward": (("k_fd_fused_s", "k_fd_fused_coop"),)}
 
 
 def per_kernel(path, counter):
