@@ -898,8 +898,49 @@ __device__ inline void make_constraint(const auto& m, const auto& L, const auto&
                                  cc[CON_FRAME + 3 * r + 2] * b[2];
   }
   TSYNC();
-  // row allocation in the oracle's order (limits, then contacts), lane 0
-  if (T.tid == 0) {
+  // row allocation in the oracle's order (limits, then contacts).  When every
+  // row fits (no njmax truncation) the offsets are prefix counts over ballots,
+  // one lane per joint / contact; otherwise the oracle's loop on lane 0.
+  bool par = m.njnt <= TEAM_SIZE && ncon <= TEAM_SIZE;
+  if (par) {
+    const int t = T.tid;
+    const int jm = t < m.njnt ? jcnt[t] : 0;
+    const unsigned long long blo = __ballot(jm & 1), bhi = __ballot(jm & 2);
+    const int nlim = __popcll(blo) + __popcll(bhi);
+    const int dim = t < ncon ? coni[CON_NI * t + CONI_DIM] : 0;
+    const int nrow = t < ncon ? (dim == 1 ? 1 : 2 * (dim - 1)) : 0;
+    int before = 0, total = 0;  // contact rows of lanes below t, of all lanes
+    for (int b = 0; b < 5; b++) {
+      const unsigned long long bb = __ballot((nrow >> b) & 1);
+      before += (int)__builtin_amdgcn_mbcnt_hi((unsigned)(bb >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)bb, 0u)) << b;
+      total += __popcll(bb) << b;
+    }
+    par = nrow < 32 && __ballot(nrow >= 32) == 0ull && nlim + total <= njmax;
+    if (par) {
+      if (t < m.njnt && jm) {
+        const unsigned long long below = (1ull << t) - 1;
+        int r = __popcll(blo & below) + __popcll(bhi & below);
+        for (int side = -1; side <= 1; side += 2) {
+          if (!(jm & (side < 0 ? 1 : 2))) continue;
+          efc_type[r] = C_LIMIT;
+          efc_id[r] = t;
+          rsub[r] = side;
+          r++;
+        }
+      }
+      if (t < ncon) {
+        const int r0 = nlim + before;
+        coni[CON_NI * t + CONI_EFCADR] = r0;
+        for (int r = 0; r < nrow; r++) {
+          efc_type[r0 + r] = dim == 1 ? C_FRICTIONLESS : C_PYRAMIDAL;
+          efc_id[r0 + r] = t;
+          rsub[r0 + r] = r;
+        }
+      }
+      if (t == 0) T.iw[L.nefc] = nlim + total;
+    }
+  }
+  if (!par && T.tid == 0) {
     int nefc = 0;
     for (int j = 0; j < m.njnt; j++) {
       int mask = jcnt[j];
@@ -1467,7 +1508,7 @@ __device__ __forceinline__ double lane_sum_mask(double s0, double v, unsigned lo
 // constraint_update for row registers: returns the cost (uniform) and the
 // active-row mask; with `full` also force/state and qfrc_constraint = J' force
 __device__ inline double cu_fast(const auto& m, const auto& L, const Team& T, double jr, double Di, bool full,
-                                 unsigned long long& mask) {
+                                 unsigned long long& mask, bool want_cost = true) {
   const int nv = m.nv, ne = T.iw[L.nefc];
   const int r = T.tid;
   const bool row = r < ne;
@@ -1496,6 +1537,7 @@ __device__ inline double cu_fast(const auto& m, const auto& L, const Team& T, do
     TSYNC();
   }
   mask = __ballot(act);
+  if (!want_cost) return 0.0;
   const double tv = act ? 0.5 * Di * jr * jr : -0.0;
   return lane_sum_mask(0.0, tv, mask);
 }
@@ -1569,7 +1611,15 @@ __device__ inline void fwd_constraint_fast(const auto& m, const auto& L, const a
     FOR_T(i, nv) Ma[i] = tdot(qM + i * nv, qacc, nv);
     TSYNC();
   }
-  double cost = gauss_u(nv, Ma, qfs, qacc, qas) + cu_fast(m, L, T, jr, Di, true, mask);
+  // from the warm start the full update's cost is cost_warm's expression on the
+  // same values: only its side effects (force, state, qfrc_constraint) are new
+  double cost;
+  if (use_smooth) {
+    cost = gauss_u(nv, Ma, qfs, qacc, qas) + cu_fast(m, L, T, jr, Di, true, mask);
+  } else {
+    (void)cu_fast(m, L, T, jr, Di, true, mask, false);
+    cost = cost_warm;
+  }
   FOR_T(j, nv) grad[j] = (Ma[j] - qfs[j]) - qc[j];
   hessian_build_fast(m, L, T, H, mask);
   cholesky_rows(nv, T.tid, H);
