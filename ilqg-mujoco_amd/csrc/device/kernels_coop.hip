@@ -530,6 +530,27 @@ __global__ __launch_bounds__(TEAM, FD_WAVES_PER_EU) void k_fd_fused_s(DevModel m
   fd_fused_body(m, L, C, X, T, a, t - a.nB);
 }
 
+// the same with the model read from its global image (L1/L2 cached) instead of
+// an LDS copy: the team's LDS drops by the image, so more teams fit a CU
+template <class SM, class SX>
+__global__ __launch_bounds__(TEAM, FD_WAVES_PER_EU) void k_fd_fused_g(DevModel mg, FdFused a) {
+  const unsigned t = take_ticket(a.sync);
+  if (t < (unsigned)a.nB) {
+    fd_backward_role<SM::nv, SM::nu>(mg, a, (int)t);
+    return;
+  }
+  static constexpr WsLayout L = make_layout(SM{}, SX::npair);
+  static constexpr CoopLayout C = make_coop_layout(SM{}, SX::npair);
+  static constexpr SX X{};
+  extern __shared__ double lds[];
+  Team T = make_team(L, C);
+  T.iw = reinterpret_cast<int*>(lds + L.nd + C.nd);  // no image region
+  T.ci = T.iw + L.ni;
+  SM m;
+  m.bind(mg.img, mg);
+  fd_fused_body(m, L, C, X, T, a, t - a.nB);
+}
+
 __device__ inline void rollout_body(const auto& m, const auto& L, const auto& C, const auto& X, const Team& T,
                                 int S, int A, int P, TrajDev nom, TrajDev out, int out_is_cand, const double* K, const double* k, const double* alphas, TrajDev dinit, const double* qfrc_applied, const double* xfrc_applied, int passive, CostDev cost, double* cost_cand, int wave) {
   // wave < 0: one-wave team; 0/1: primary/helper wave of a two-wave team (step_dual)
@@ -767,6 +788,11 @@ hipError_t launch_fd_cols_coop(const DevModel& m, const WsLayout& L, const CoopL
   return hipGetLastError();
 }
 
+static bool fd_global_image() {
+  const char* e = getenv("ILQG_FD_GIMG");
+  return !(e && *e == '0');  // default on (ILQG_FD_GIMG=0: LDS copy)
+}
+
 hipError_t launch_fd_fused_coop(const DevModel& m, const WsLayout& L, const CoopLayout& C, const CoopAux& X,
                                 const FdFused& a, hipStream_t st) {
   const long items = (long)a.S * a.P * (1 + a.nut + a.nvt + m.nv);
@@ -775,8 +801,18 @@ hipError_t launch_fd_fused_coop(const DevModel& m, const WsLayout& L, const Coop
   size_t lds = coop_lds_bytes(L, C);
   if (a.nB > 0) lds = std::max(lds, backward_lds_bytes(m.nv, m.nu));
   hipError_t e;
+  const bool gimg = fd_global_image();
+  const size_t lds_g = std::max((size_t)(L.nd + C.nd) * sizeof(double) + (size_t)(L.ni + C.ni) * sizeof(int),
+                                a.nB > 0 ? backward_lds_bytes(m.nv, m.nu) : (size_t)0);
 #define ILQG_CASE(id, SMT, SXT)                                                                                 \
   case id:                                                                                                      \
+    if (gimg) {                                                                                                 \
+      e = allow_lds(k_fd_fused_g<stat::SMT, stat::SXT>, lds_g);                                                 \
+      if (e != hipSuccess) return e;                                                                            \
+      hipLaunchKernelGGL((k_fd_fused_g<stat::SMT, stat::SXT>), dim3((unsigned)blocks), dim3(TEAM), lds_g, st, m, \
+                         a);                                                                                    \
+      return hipGetLastError();                                                                                 \
+    }                                                                                                           \
     e = allow_lds(k_fd_fused_s<stat::SMT, stat::SXT>, lds);                                                     \
     if (e != hipSuccess) return e;                                                                              \
     hipLaunchKernelGGL((k_fd_fused_s<stat::SMT, stat::SXT>), dim3((unsigned)blocks), dim3(TEAM), lds, st, m, a); \

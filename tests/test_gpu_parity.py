@@ -310,7 +310,8 @@ def test_humanoid_iterate_tangent_space(ia, ora):
 
 @pytest.mark.parametrize("env", [{"ILQG_FUSED": "0"}, {"ILQG_FD_LAG": "0"}, {"ILQG_FD_LAG": "1"},
                                  {"ILQG_FD_LAG": "7", "ILQG_FD_CV": "1"}, {"ILQG_FD_CV": "6"},
-                                 {"ILQG_FD_USPLIT": "0"}, {"ILQG_FD_USPLIT": "0", "ILQG_FD_LAG": "3"}])
+                                 {"ILQG_FD_USPLIT": "0"}, {"ILQG_FD_USPLIT": "0", "ILQG_FD_LAG": "3"},
+                                 {"ILQG_FD_GIMG": "1"}, {"ILQG_FD_GIMG": "0"}])
 def test_fused_sweep_schedules(ia, ora, env, monkeypatch):
     """The fused FD sweep + streamed backward pass (k_fd_fused_s): every hand-off
     schedule (centre lag, qvel columns per team, ctrl columns on their own teams
