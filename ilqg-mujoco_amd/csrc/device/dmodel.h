@@ -80,10 +80,13 @@ constexpr WsLayout make_layout(const M& m, int npair = -1) {
   L.kstr = coop ? 3 : 4;
   if (!coop) L.con = take(CON_ND * nc);
   L.efc_J = take(ne * nv); L.efc_pos = take(ne); L.efc_margin = take(ne); L.efc_D = take(ne);
-  L.efc_KBIP = take(L.kstr * ne); L.efc_aref = take(ne);
-  if (!coop) L.efc_vel = take(ne);
-  L.efc_force = take(ne);
-  if (!coop) L.efc_b = take(ne);
+  L.efc_KBIP = take(L.kstr * ne);
+  if (!coop) {
+    L.efc_aref = take(ne);
+    L.efc_vel = take(ne);
+    L.efc_force = take(ne);
+    L.efc_b = take(ne);
+  }
   L.cvel = take(6 * nb); L.cdof_dot = take(6 * nv); L.qfrc_passive = take(nv); L.qfrc_bias = take(nv);
   L.afrc = take(nu); L.qfrc_act = take(nv); L.qfrc_smooth = take(nv); L.qacc_smooth = take(nv);
   L.qfrc_con = take(nv);
@@ -99,8 +102,11 @@ constexpr WsLayout make_layout(const M& m, int npair = -1) {
     const int u = o;
     int a = u;  // position-stage view
     L.con = a; a += CON_ND * nc;
-    L.pcon = a; a += 14 * (npair > 0 ? npair : 1);
-    L.jc = a; a += 3 * nv * nc;
+    // per-pair candidates (dead once collision has compacted them into con)
+    // and contact-frame jacobians (first written by make_constraint) share storage
+    L.pcon = a;
+    L.jc = a;
+    a += 14 * (npair > 0 ? npair : 1) > 3 * nv * nc ? 14 * (npair > 0 ? npair : 1) : 3 * nv * nc;
     int b = u;  // velocity / constraint / integration view
     L.s_rne = b; b += 12 * nb;
     L.s_con = b; b += 10 * nv;
@@ -108,6 +114,10 @@ constexpr WsLayout make_layout(const M& m, int npair = -1) {
     L.s_euler = b; b += 2 * nv + 2 * nv * nv;
     L.efc_b = b; b += ne;
     L.efc_vel = b; b += ne;
+    // reference accelerations (velocity stage) and forces (constraint solve):
+    // first written after make_constraint, like the rest of this view
+    L.efc_aref = b; b += ne;
+    L.efc_force = b; b += ne;
     o = a > b ? a : b;
   }
   L.nd = o;
