@@ -796,9 +796,24 @@ __device__ inline void collision(const auto& m, const auto& L, const auto& C, co
   }
   TSYNC();
   // ordered compaction with the oracle's truncation at nconmax
-  if (T.tid == 0) {
+  const int lim = m.nconmax < m.maxcon ? m.nconmax : m.maxcon;
+  // offsets as ballot prefix counts when nothing is truncated (n <= 2 per pair),
+  // else the oracle's loop on lane 0
+  bool par = X.npair <= TEAM_SIZE;
+  if (par) {
+    const int t = T.tid;
+    const int n = t < X.npair ? pcnt[t] : 0;
+    const unsigned long long b0 = __ballot(n & 1), b1 = __ballot(n & 2);
+    const int total = __popcll(b0) + 2 * __popcll(b1);
+    par = total <= lim && __ballot(n > 3) == 0ull;
+    if (par) {
+      const unsigned long long below = t < 64 ? (1ull << t) - 1 : ~0ull;
+      if (t < X.npair) pcnt[t] = ((__popcll(b0 & below) + 2 * __popcll(b1 & below)) << 8) | n;
+      if (t == 0) T.iw[L.ncon] = total;
+    }
+  }
+  if (!par && T.tid == 0) {
     int ncon = 0;
-    const int lim = m.nconmax < m.maxcon ? m.nconmax : m.maxcon;
     for (int p = 0; p < X.npair; p++) {
       int n = pcnt[p];
       int take = 0;
