@@ -1585,8 +1585,44 @@ __device__ inline void hessian_build_fast(const auto& m, const auto& L, const Te
   TSYNC();
 }
 
+// The helper wave of a two-wave rollout team, beside the primary's
+// acceleration stage: everything of the Newton start that depends only on the
+// warm start -- jar and M*warm, its constraint cost, the full constraint update
+// (forces, states, qfrc_constraint) and the Hessian factor of its active set.
+// The primary then needs only the smooth start's cost to choose; from the warm
+// start (the common case) it goes straight to the first iteration.  Same
+// expressions as fwd_constraint_fast, on the other wave.
+__device__ inline void newton_warm_prep(const auto& m, const auto& L, const auto& C, const Team& T) {
+  const int nv = m.nv, ne = T.iw[L.nefc];
+  double* s = T.w + L.s_newton;
+  double *Ma = s, *H = s + 4 * nv;
+  double* jar = s + 4 * nv + nv * nv;
+  double* qM = T.w + L.qM;
+  double* warm = T.w + L.warm;
+  double* J = T.w + L.efc_J;
+  double* aref = T.w + L.efc_aref;
+  const int r = T.tid;
+  const bool row = r < ne;
+  const double Di = row ? T.w[L.efc_D + r] : 0.0;
+  const double jw = row ? tdot(J + r * nv, warm, nv) - aref[r] : 0.0;
+  if (row) jar[r] = jw;
+  FOR_T(i, nv) Ma[i] = tdot(qM + i * nv, warm, nv);
+  TSYNC();
+  unsigned long long mw;
+  const double cu_w = cu_fast(m, L, T, jw, Di, true, mw);
+  hessian_build_fast(m, L, T, H, mw);
+  cholesky_rows(nv, T.tid, H);
+  if (T.tid == 0) {
+    T.c[C.bc + 4] = cu_w;
+    T.c[C.bc + 5] = __longlong_as_double((long long)mw);
+  }
+  TSYNC();
+}
+
+// dual: the primary wave of a two-wave team whose helper runs newton_warm_prep
+// concurrently; exactly one __syncthreads (after the smooth start's cost)
 __device__ inline void fwd_constraint_fast(const auto& m, const auto& L, const auto& C, const auto& X,
-                                           const Team& T, int maxiter, double tol) {
+                                           const Team& T, int maxiter, double tol, bool dual = false) {
   const int nv = m.nv, ne = T.iw[L.nefc];
   const double scale = 1 / (m.stat_meaninertia * (nv > 1 ? nv : 1));
   double* s = T.w + L.s_newton;
@@ -1607,16 +1643,29 @@ __device__ inline void fwd_constraint_fast(const auto& m, const auto& L, const a
   const double Di = row ? T.w[L.efc_D + r] : 0.0;
   unsigned long long mask, hmask;
   // warm-start selection (oracle fwd_constraint): smooth vs warmstart cost
-  double jb = 0, jw = 0;
-  if (row) {
-    jb = tdot(J + r * nv, qas, nv) - aref[r];
-    jw = tdot(J + r * nv, warm, nv) - aref[r];
-    b[r] = jb;
+  double jb = 0, jw = 0, cost_warm, cost_smooth;
+  unsigned long long mask_w = 0;
+  if (dual) {
+    if (row) {
+      jb = tdot(J + r * nv, qas, nv) - aref[r];
+      b[r] = jb;
+    }
+    cost_smooth = cu_fast(m, L, T, jb, Di, false, mask);
+    __syncthreads();  // the helper's warm-start part (newton_warm_prep) is in LDS
+    if (row) jw = jar[r];
+    mask_w = (unsigned long long)__double_as_longlong(T.c[C.bc + 5]);
+    cost_warm = gauss_u(nv, Ma, qfs, warm, qas) + T.c[C.bc + 4];
+  } else {
+    if (row) {
+      jb = tdot(J + r * nv, qas, nv) - aref[r];
+      jw = tdot(J + r * nv, warm, nv) - aref[r];
+      b[r] = jb;
+    }
+    FOR_T(i, nv) Ma[i] = tdot(qM + i * nv, warm, nv);
+    TSYNC();
+    cost_smooth = cu_fast(m, L, T, jb, Di, false, mask);
+    cost_warm = gauss_u(nv, Ma, qfs, warm, qas) + cu_fast(m, L, T, jw, Di, false, mask);
   }
-  FOR_T(i, nv) Ma[i] = tdot(qM + i * nv, warm, nv);
-  TSYNC();
-  const double cost_smooth = cu_fast(m, L, T, jb, Di, false, mask);
-  const double cost_warm = gauss_u(nv, Ma, qfs, warm, qas) + cu_fast(m, L, T, jw, Di, false, mask);
   const bool use_smooth = cost_warm > cost_smooth;
   // solver start (oracle solver_newton): Ma, jar at qacc, full constraint update
   double jr = use_smooth ? jb : jw;
@@ -1631,13 +1680,20 @@ __device__ inline void fwd_constraint_fast(const auto& m, const auto& L, const a
   double cost;
   if (use_smooth) {
     cost = gauss_u(nv, Ma, qfs, qacc, qas) + cu_fast(m, L, T, jr, Di, true, mask);
+  } else if (dual) {
+    mask = mask_w;  // forces, states, qfrc_constraint and the factor: the helper's
+    cost = cost_warm;
   } else {
     (void)cu_fast(m, L, T, jr, Di, true, mask, false);
     cost = cost_warm;
   }
   FOR_T(j, nv) grad[j] = (Ma[j] - qfs[j]) - qc[j];
-  hessian_build_fast(m, L, T, H, mask);
-  cholesky_rows(nv, T.tid, H);
+  if (use_smooth || !dual) {
+    hessian_build_fast(m, L, T, H, mask);
+    cholesky_rows(nv, T.tid, H);
+  } else {
+    TSYNC();
+  }
   hmask = mask;
   int iter = 0;
 #ifdef ILQG_STAMPS
@@ -2057,13 +2113,25 @@ __device__ inline void step_dual(const auto& m, const auto& L, const auto& C, co
   STAMP(27);
   STAMPB(39);
   // the Euler factor of M + h D on the helper beside the constraint solve
+  // ... and the warm-start half of the Newton start before it (one extra
+  // barrier inside the phase, on both waves)
+  const int ne5 = T.iw[L.nefc];
+  const bool spec = ne5 > 0 && ne5 <= TEAM_SIZE && m.nv <= RMAX;
   if (A) {
     fwd_acceleration(m, L, X, T);
     STAMP(7);
-    fwd_constraint(m, L, C, X, T, m.opt_iterations, m.opt_tolerance);
+    if (spec) {
+      fwd_constraint_fast(m, L, C, X, T, m.opt_iterations, m.opt_tolerance, true);
+    } else {
+      __syncthreads();
+      fwd_constraint(m, L, C, X, T, m.opt_iterations, m.opt_tolerance);
+    }
     STAMP(8);
-  } else if (eul) {
-    euler_prefactor(m, L, C, X, T);
+  } else {
+    if (spec) newton_warm_prep(m, L, C, T);
+    STAMPB(30);
+    __syncthreads();
+    if (eul) euler_prefactor(m, L, C, X, T);
     STAMPB(38);
   }
   __syncthreads();

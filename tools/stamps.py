@@ -14,7 +14,7 @@ NAMES = {0: "kinematics", 1: "com_pos", 2: "trn+crb", 3: "factor_ld(M)", 4: "col
          32: "B: barrier 1 (wait for A kinematics)", 33: "B: collision", 34: "B: barrier 2", 35: "B: make_constraint",
          36: "B: barrier 3", 37: "B: passive+aref", 38: "B: euler prefactor", 39: "B: barrier 4 (A com vel + RNE)",
          40: "B: barrier 6 (end of step)", 41: "B: control law + record", 42: "B: factor_ld(M)", 43: "B: barrier 5",
-         29: "A: barrier 5b (Euler factor)"}
+         29: "A: barrier 5b (Euler factor)", 30: "B: Newton warm-start prep"}
 L = ia.lib()
 acc = (ctypes.c_ulonglong * 48)(); cnt = (ctypes.c_ulonglong * 48)()
 m = ia.Model.load(workloads.model_file(sys.argv[1] if len(sys.argv) > 1 else "hopper"))
