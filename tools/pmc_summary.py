@@ -12,7 +12,7 @@ import collections, csv, json, re, sys
 GROUPS = {"rollout": (("k_rollout2_s", "k_rollout_s", "k_rollout2_coop", "k_rollout_coop"),),
           "fd_sweep": (("k_fd_centre_s", "k_fd_centre_coop"), ("k_fd_cols_s", "k_fd_cols_coop")),
           "backward": (("k_backward",),), "select": (("k_select",),),
-          "fd_backward": (("k_fd_fused_s", "k_fd_fused_coop"),)}
+          "fd_backward": (("k_fd_fused_g", "k_fd_fused_s", "k_fd_fused_coop"),)}
 
 
 def per_kernel(path, counter):
