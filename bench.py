@@ -153,13 +153,18 @@ def main():
     m = ia.Model.load(workloads.model_file("hopper"))
     dmain = workloads.hopper_dmain(m, S, sigma=0.01, seed_offset=seed_offset(rank, S))
     solver = ia.ILQR(m, dmain, H, ia.HOPPER_COST, alphas=alphas, select="min_cost", device=local_rank)
-    stream = torch.cuda.current_stream()
+    # one explicit stream for the solver's launches and the cost exchange: the
+    # all-gather (RCCL waits on torch's current stream) is then ordered after
+    # the iteration that produced the costs (torch's default stream is the
+    # legacy null stream, which does not order against the solver's own)
+    stream = torch.cuda.Stream()
     solver.set_stream(stream.cuda_stream)
     exchange = CostExchange(device_view(solver.device_costs_ptr(), S), world)
 
     def one_step():
-        solver.iterate()
-        return exchange()
+        with torch.cuda.stream(stream):
+            solver.iterate()
+            return exchange()
 
     for _ in range(args.warmup):
         one_step()

@@ -170,8 +170,22 @@ __device__ inline void backward_seed(const MD& m, int nq, int nv_rt, int nu_rt, 
     __syncthreads();
   }
   BSTAMP(-1);
+  // the nominal states for c = x*_{n-1} - x*_n: one lane per component, in
+  // registers, each point loaded one step ahead (nq == nv; quaternion models
+  // take the tangent-space difference from memory below)
+  const bool xreg = nq == nv && nx <= BW_THREADS;
+  auto xload = [&](size_t pt) -> double {
+    return tid < nv ? tr.qpos[pt * nq + tid] : (tid < nx ? tr.qvel[pt * nv + tid - nv] : 0.0);
+  };
+  double xa = 0, xb = 0;
+  if (xreg) {
+    xa = xload((size_t)s * P);
+    if (P > 1) xb = xload((size_t)s * P + 1);
+  }
   for (int n = 1; n < P; n++) {
     const size_t pc = (size_t)s * P + n, pp = pc - 1;
+    double xn = 0;
+    if (xreg && n + 1 < P) xn = xload(pc + 1);
     // prefetch the next step's FD record; consumed at the end of this step
     double pf[BW_PF];
     if (pref && n + 1 < P) {
@@ -202,7 +216,9 @@ __device__ inline void backward_seed(const MD& m, int nq, int nv_rt, int nu_rt, 
     for (int i = tid; i < nx; i += BW_THREADS) {
       q[i] = dn[2 * nv * nv + nv * nu + i];
       // c = x*_{n-1} (-) x*_n (inc/ilqr.h:154-157; tangent space for quaternion joints)
-      if (i < nv && nq != nv) {
+      if (xreg) {
+        c[i] = xa - xb;  // i == tid
+      } else if (i < nv && nq != nv) {
         c[i] = dev::state_diff_dof(m, i, tr.qpos + pp * nq, tr.qpos + pc * nq);
       } else {
         double xp = i < nv ? tr.qpos[pp * nq + i] : tr.qvel[pp * nv + i - nv];
@@ -364,6 +380,8 @@ __device__ inline void backward_seed(const MD& m, int nq, int nv_rt, int nu_rt, 
       }
     }
     __syncthreads();
+    xa = xb;
+    xb = xn;
     BSTAMP(8);
   }
   if (Vg)
