@@ -881,6 +881,9 @@ static hipError_t fused_launch(ilqg_solver* s, const SeedRange& r, int mode) {
   const size_t s0 = r.s0, P = s->P, nx = s->nx;
   hipError_t e = hipMemsetAsync(r.sync, 0, sync_bytes((size_t)r.ns * P), r.st);
   if (e != hipSuccess) return e;
+  // the launch's own fault word (handoff.h); the report word survives until read
+  e = hipMemsetAsync(s->fault.as<unsigned>() + 1, 0, sizeof(unsigned), r.st);
+  if (e != hipSuccess) return e;
   FdFused a{};
   a.tr = toff(s->tview(s->traj), s0 * P, h);
   a.S = r.ns;
@@ -993,7 +996,24 @@ int ilqg_synchronize(ilqg_solver* s) {
   HIPCHK(s->sync_all());
   unsigned flt = 0;
   HIPCHK(hipMemcpy(&flt, s->fault.p, 4, hipMemcpyDeviceToHost));
-  if (flt) return fail(ILQG_ERR_HIP, "fused FD sweep: a hand-off wait timed out");
+  if (flt) {
+    // reported once: cleared by the read (the next launch waits normally)
+    HIPCHK(hipMemset(s->fault.p, 0, 4));
+    return fail(ILQG_ERR_HIP, "fused FD sweep: a hand-off wait timed out");
+  }
+  return ILQG_OK;
+}
+
+int ilqg_solver_device_traj(ilqg_solver* s, int field, double** dptr) {
+  if (!s || !dptr || field < 0 || field > 4) return fail(ILQG_ERR_ARG, "bad argument");
+  *dptr = s->traj[field].as<double>();
+  return ILQG_OK;
+}
+
+int ilqg_solver_debug_set_fault(ilqg_solver* s, unsigned value) {
+  if (!s) return fail(ILQG_ERR_ARG, "null solver");
+  HIPCHK(s->sync_all());
+  HIPCHK(hipMemcpy(s->fault.p, &value, 4, hipMemcpyHostToDevice));
   return ILQG_OK;
 }
 

@@ -19,8 +19,19 @@ typedef __attribute__((address_space(1))) unsigned gu32;
 typedef __attribute__((address_space(1))) unsigned long long gu64;
 
 // ~2^22 polls of >= 256 cycles: seconds, far beyond any legitimate wait; a
-// timed-out wait sets *fault (reported by ilqg_synchronize) and gives up, so a
-// broken producer can never hang the GPU
+// timed-out wait gives up, so a broken producer can never hang the GPU.  The
+// fault block is two words: fault[0] is the report (read and cleared by
+// ilqg_synchronize), fault[1] the launch's own word (zeroed before every
+// launch): a timed-out wait sets both, and every later wait of the same launch
+// sees fault[1] and gives up at once, while the next launch waits normally.
+__device__ __forceinline__ void raise_fault(unsigned* fault) {
+  __hip_atomic_fetch_or((gu32*)(fault), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __hip_atomic_fetch_or((gu32*)(fault + 1), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ bool launch_faulted(const unsigned* fault) {
+  return __builtin_amdgcn_readfirstlane(
+             __hip_atomic_load((gu32*)(fault + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) != 0u;
+}
 constexpr unsigned HANDOFF_SPIN_LIMIT = 1u << 22;
 
 #ifdef ILQG_STAMPS
@@ -45,15 +56,12 @@ __device__ __forceinline__ void drain_stores() { asm volatile("s_waitcnt vmcnt(0
 __device__ inline bool bw_wait_geq(const unsigned* w, unsigned target, unsigned* fault) {
   for (unsigned spins = 0;; spins++) {
     // after one timed-out wait every later one gives up at once
-    if ((spins & 255) == 255 && fault &&
-        __builtin_amdgcn_readfirstlane(__hip_atomic_load((gu32*)(fault), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)))
-      return false;
+    if ((spins & 255) == 255 && fault && launch_faulted(fault)) return false;
     const unsigned v = __builtin_amdgcn_readfirstlane(
         __hip_atomic_load((gu32*)(w), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
     if (v >= target) break;
     if (spins > HANDOFF_SPIN_LIMIT) {
-      if (fault && (threadIdx.x & 63) == 0) __hip_atomic_fetch_or((gu32*)(fault), 1u, __ATOMIC_RELAXED,
-                                                                 __HIP_MEMORY_SCOPE_AGENT);
+      if (fault && (threadIdx.x & 63) == 0) raise_fault(fault);
       return false;
     }
     __builtin_amdgcn_s_sleep(4);
@@ -72,9 +80,7 @@ __device__ inline bool bw_wait_geq(const unsigned* w, unsigned target, unsigned*
 __device__ inline int bw_wait_window(const unsigned* flags, int p, int n, unsigned target, unsigned* fault) {
   const int lane = threadIdx.x & 63;
   for (unsigned spins = 0;; spins++) {
-    if ((spins & 255) == 255 && fault &&
-        __builtin_amdgcn_readfirstlane(__hip_atomic_load((gu32*)(fault), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)))
-      return p;
+    if ((spins & 255) == 255 && fault && launch_faulted(fault)) return p;
     const int q = p + lane;
     const bool ok = q < n && __hip_atomic_load((gu32*)(flags + q), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= target;
     const unsigned long long mask = __ballot(ok);
@@ -83,7 +89,7 @@ __device__ inline int bw_wait_window(const unsigned* flags, int p, int n, unsign
       return ~mask ? p + (int)__builtin_ctzll(~mask) - 1 : p + 63;
     }
     if (spins > HANDOFF_SPIN_LIMIT) {
-      if (fault && lane == 0) __hip_atomic_fetch_or((gu32*)(fault), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (fault && lane == 0) raise_fault(fault);
       return p;
     }
     __builtin_amdgcn_s_sleep(4);

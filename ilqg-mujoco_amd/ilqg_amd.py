@@ -62,6 +62,7 @@ EXPORTS = [
     "ilqg_forward", "ilqg_fd_sweep", "ilqg_backward", "ilqg_iterate", "ilqg_synchronize",
     "ilqg_solver_stream", "ilqg_solver_device_costs", "ilqg_solver_set_stream", "ilqg_solver_set_timing",
     "ilqg_solver_get_timing", "ilqg_solver_set_groups", "ilqg_solver_get_groups",
+    "ilqg_solver_debug_set_fault", "ilqg_solver_device_traj",
 ]
 KERNELS = ("rollout", "select", "fd_centre", "fd_cols", "backward", "fd_backward")
 
@@ -398,6 +399,17 @@ class ILQR:
         n = (ctypes.c_int * len(KERNELS))()
         _check(lib().ilqg_solver_get_timing(self._h, ms, n), "get_timing")
         return {k: (ms[i], n[i]) for i, k in enumerate(KERNELS)}
+
+    def _debug_set_fault(self, value: int):
+        """test hook: preset the hand-off fault report word (ilqg_solver_debug_set_fault)"""
+        _check(lib().ilqg_solver_debug_set_fault(self._h, ctypes.c_uint(value)), "debug_set_fault")
+
+    def device_traj_ptr(self, field: str) -> int:
+        """device pointer to the resident nominal trajectory field (seed-major [S][P][...])"""
+        idx = ("time", "qpos", "qvel", "warm", "ctrl").index(field)
+        p = ctypes.POINTER(ctypes.c_double)()
+        _check(lib().ilqg_solver_device_traj(self._h, idx, ctypes.byref(p)), "device_traj")
+        return ctypes.cast(p, ctypes.c_void_p).value
 
     def device_costs_ptr(self) -> int:
         p = ctypes.POINTER(ctypes.c_double)()

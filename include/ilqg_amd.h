@@ -134,7 +134,11 @@ int ilqg_forward(ilqg_solver* s);   /* forwardPass over all candidates + selecti
 int ilqg_fd_sweep(ilqg_solver* s);  /* calcMJDerivatives at every point of every seed */
 int ilqg_backward(ilqg_solver* s);  /* initV + Riccati n = 1..N (inc/ilqr.h:100-107,133-176) */
 int ilqg_iterate(ilqg_solver* s);   /* forwardPass; setDInit(dArray[N]); backwardPass (inc/ilqr.h:179-186) */
+/* waits for every launch; returns ILQG_ERR_HIP once if a fused sweep's
+   hand-off wait timed out since the last call (the report is cleared by it) */
 int ilqg_synchronize(ilqg_solver* s);
+/* test hook: preset the fault report word that ilqg_synchronize reads */
+int ilqg_solver_debug_set_fault(ilqg_solver* s, unsigned value);
 void* ilqg_solver_stream(ilqg_solver* s); /* hipStream_t */
 /* enqueue subsequent hot-path launches on an external stream (hipStream_t,
    e.g. torch's current stream) instead of the solver's own; NULL restores it */
@@ -150,6 +154,11 @@ int ilqg_solver_get_timing(ilqg_solver* s, double* ms, int* launches);
 /* device pointer to the per-seed selected-candidate cost (nseed doubles), for
    an in-stream collective (RCCL all-gather) without a host round trip */
 int ilqg_solver_device_costs(ilqg_solver* s, double** dptr);
+/* device pointer to the resident nominal trajectory (field 0 time, 1 qpos,
+   2 qvel, 3 warm, 4 ctrl; seed-major [nseed][N+1][...], point N = the first
+   applied control): the multi-GPU MPC broadcast of the winning seed's first
+   control reads it in place */
+int ilqg_solver_device_traj(ilqg_solver* s, int field, double** dptr);
 /* seed groups (an MI355X extension; no reference counterpart): split the
    nseed seeds into ngroups contiguous ranges, each iterated on its own stream,
    so one group's latency-bound rollout overlaps another group's FD sweep.

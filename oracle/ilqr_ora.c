@@ -543,6 +543,88 @@ void ora_ilqr_iterate(ora_ilqr* s) {
   ora_ilqr_backwardPass(s);
 }
 
+/* ---- line-search extension (no reference counterpart,
+   quirk Q22): forwardPass (ilqr.h:116-130) rolled out once per candidate with
+   the feed-forward scaled, u = K (x - x*) + alpha k + u*, each candidate
+   recording its own trajectory and its trajectory cost sum_n cost(d_n) over
+   the recorded states (terms in n = N..0 order).  alpha = 1 is exactly the
+   reference's forwardPass.  select_mode 0 keeps candidate 0 (reference
+   semantics), 1 the lowest cost (first minimum; a NaN cost loses to any
+   number).  The selected candidate becomes dArray; the caller's setDInit
+   (ilqr.h:183) follows. ---- */
+void ora_ilqr_forward_candidates(ora_ilqr* s, int A, const mjtNum* alphas, int select_mode, mjtNum* costs,
+                                 int* selected) {
+  const mjModel* m = s->m;
+  int nq = m->nq, nv = m->nv, nu = s->nu, nx = s->nx, N = s->N, P = N + 1;
+  /* per candidate and point: time, qpos, qvel, qacc, warm, ctrl */
+  int rec = 1 + nq + 3 * nv + nu;
+  mjtNum* tr = (mjtNum*)malloc(sizeof(mjtNum) * (size_t)A * P * rec);
+  mjData* d = mj_makeData(s->m);
+  mjtNum dx[256];
+  for (int a = 0; a < A; a++) {
+    mjtNum alpha = alphas ? alphas[a] : 1.0, c = 0;
+    ora_cpMjData(m, d, s->d);
+    for (int n = N; n >= 0; n--) {
+      const mjtNum* xs = s->dArray[n]->qpos;
+      const mjtNum* us = s->dArray[n]->ctrl;
+      const mjtNum* K = s->K + (size_t)n * nu * nx;
+      const mjtNum* k = s->k + (size_t)n * nu;
+      ora_state_diff(m, d->qpos, d->qvel, xs, s->dArray[n]->qvel, dx);
+      for (int i = 0; i < nu; i++) {
+        mjtNum t = 0;
+        for (int j = 0; j < nx; j++) t += K[i + j * nu] * dx[j];
+        d->ctrl[i] = (t + alpha * k[i]) + us[i];
+      }
+      mjtNum* r = tr + ((size_t)a * P + n) * rec;
+      r[0] = d->time;
+      mju_copy(r + 1, d->qpos, nq);
+      mju_copy(r + 1 + nq, d->qvel, nv);
+      mju_copy(r + 1 + nq + nv, d->qacc, nv);
+      mju_copy(r + 1 + nq + 2 * nv, d->qacc_warmstart, nv);
+      mju_copy(r + 1 + nq + 3 * nv, d->ctrl, nu);
+      c += s->cost(d);
+      mj_step(s->m, d);
+    }
+    if (costs) costs[a] = c;
+  }
+  int best = 0;
+  if (select_mode == 1 && costs) {
+    mjtNum bc = costs[0];
+    for (int a = 1; a < A; a++)
+      if (costs[a] < bc || (bc != bc && costs[a] == costs[a])) { bc = costs[a]; best = a; }
+  }
+  if (selected) *selected = best;
+  /* the selected candidate's records become dArray (cpMjData's fields) and
+     the rollout's end state becomes d, as after the reference forwardPass */
+  for (int n = N; n >= 0; n--) {
+    mjData* dn = s->dArray[n];
+    const mjtNum* r = tr + ((size_t)best * P + n) * rec;
+    dn->time = r[0];
+    mju_copy(dn->qpos, r + 1, nq);
+    mju_copy(dn->qvel, r + 1 + nq, nv);
+    mju_copy(dn->qacc, r + 1 + nq + nv, nv);
+    mju_copy(dn->qacc_warmstart, r + 1 + nq + 2 * nv, nv);
+    mju_copy(dn->ctrl, r + 1 + nq + 3 * nv, nu);
+    mju_copy(dn->qfrc_applied, s->d->qfrc_applied, nv);
+    mju_copy(dn->xfrc_applied, s->d->xfrc_applied, 6 * m->nbody);
+  }
+  mj_deleteData(d);
+  free(tr);
+}
+
+/* iterate() with the line search: candidates, selection, setDInit(dArray[N]), backwardPass */
+void ora_ilqr_iterate_ls(ora_ilqr* s, int A, const mjtNum* alphas, int select_mode, mjtNum* costs, int* selected) {
+  ora_ilqr_forward_candidates(s, A, alphas, select_mode, costs, selected);
+  ora_ilqr_setDInit(s, s->dArray[s->N]);
+  ora_ilqr_backwardPass(s);
+}
+
+/* a rollout with fixed gains: forwardPass alone */
+void ora_ilqr_set_gains(ora_ilqr* s, const mjtNum* K, const mjtNum* k) {
+  if (K) memcpy(s->K, K, sizeof(mjtNum) * (size_t)(s->N + 1) * s->nu * s->nx);
+  if (k) memcpy(s->k, k, sizeof(mjtNum) * (size_t)(s->N + 1) * s->nu);
+}
+
 /* trajectory export: per point time, qpos, qvel, qacc_warmstart, ctrl */
 void ora_ilqr_get_traj(const ora_ilqr* s, mjtNum* time, mjtNum* qpos, mjtNum* qvel, mjtNum* warm,
                        mjtNum* ctrl) {

@@ -62,6 +62,10 @@ void ora_ilqr_forwardPass(ora_ilqr* s);
 void ora_ilqr_fd_point(ora_ilqr* s, int n);
 void ora_ilqr_backwardPass(ora_ilqr* s);
 void ora_ilqr_iterate(ora_ilqr* s);
+void ora_ilqr_forward_candidates(ora_ilqr* s, int A, const mjtNum* alphas, int select_mode, mjtNum* costs,
+                                 int* selected);
+void ora_ilqr_iterate_ls(ora_ilqr* s, int A, const mjtNum* alphas, int select_mode, mjtNum* costs, int* selected);
+void ora_ilqr_set_gains(ora_ilqr* s, const mjtNum* K, const mjtNum* k);
 void ora_ilqr_get_traj(const ora_ilqr* s, mjtNum* time, mjtNum* qpos, mjtNum* qvel, mjtNum* warm,
                        mjtNum* ctrl);
 

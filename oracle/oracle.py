@@ -79,6 +79,10 @@ class Lib:
         L.ora_ilqr_setDInit.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
         L.ora_ilqr_fd_point.argtypes = [ctypes.c_void_p, ctypes.c_int]
         L.ora_ilqr_get_traj.argtypes = [ctypes.c_void_p] + [_dp] * 5
+        _ip = ctypes.POINTER(ctypes.c_int)
+        for f in ("ora_ilqr_forward_candidates", "ora_ilqr_iterate_ls"):
+            getattr(L, f).argtypes = [ctypes.c_void_p, ctypes.c_int, _dp, ctypes.c_int, _dp, _ip]
+        L.ora_ilqr_set_gains.argtypes = [ctypes.c_void_p, _dp, _dp]
         L.ora_riccati_step.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_double, ctypes.c_double,
                                        _dp, _dp, _dp, _dp, _dp, _dp, _dp]
         if hasattr(L, "ref_calcMJDerivatives"):
@@ -235,6 +239,28 @@ class OILQR:
 
     def iterate(self):
         self.lib.L.ora_ilqr_iterate(self.s)
+
+    def iterate_ls(self, alphas, select="min_cost"):
+        """iterate() with the line-search extension (every candidate rolled out,
+        selection, setDInit, backwardPass); returns (costs[A], selected)."""
+        return self._candidates(alphas, select, "ora_ilqr_iterate_ls")
+
+    def forward_candidates(self, alphas, select="min_cost"):
+        return self._candidates(alphas, select, "ora_ilqr_forward_candidates")
+
+    def _candidates(self, alphas, select, fn):
+        a = np.ascontiguousarray(alphas, dtype=np.float64)
+        costs = np.zeros(len(a))
+        sel = ctypes.c_int(-1)
+        mode = {"reference": 0, "min_cost": 1}[select]
+        getattr(self.lib.L, fn)(self.s, len(a), a.ctypes.data_as(_dp), mode, costs.ctypes.data_as(_dp),
+                                ctypes.byref(sel))
+        return costs, sel.value
+
+    def set_gains(self, K, k):
+        K = np.ascontiguousarray(K, dtype=np.float64)
+        k = np.ascontiguousarray(k, dtype=np.float64)
+        self.lib.L.ora_ilqr_set_gains(self.s, K.ctypes.data_as(_dp), k.ctypes.data_as(_dp))
 
     def traj(self):
         m, P = self.model, self.N + 1

@@ -370,3 +370,68 @@ def test_seed_groups_identical(ia, G, env, monkeypatch):
         out.append((g.traj().qpos, *g.gains(), g.deriv(), *g.value(), *g.costs()))
     for a, b, what in zip(out[0], out[1], ("qpos", "K", "k", "deriv", "V", "v", "cost", "sel")):
         exact(b, a, f"groups={G} {what}")
+
+
+def test_bench_workload_bitexact(ia, ora):
+    """The exact timed workload of bench.py (cfg 4's per-GPU share: hopper H=500,
+    8 seeds x 8 line-search candidates alpha = 2^-i, select='min_cost'), three
+    iterations, against the oracle's line-search restatement
+    (ora_ilqr_iterate_ls: u = K dx + alpha k + u*, inc/ilqr.h:126 with alpha
+    scaling the feed-forward).  Iteration 2 selects a candidate other than
+    alpha = 1, so iteration 3's rollout and every backward pass after it run
+    from a non-reference nominal.  Compared bit for bit: every seed's
+    trajectory, FD records, K, k, V, v, the cost matrix and the selection."""
+    import workloads
+    m, om = setup(ia, ora, "hopper", ia.HOPPER_COST)
+    om.lib.L.ora_set_nthread(1)
+    S, H, iters = 8, 500, 3
+    alphas = workloads.LINESEARCH_ALPHAS
+    dmain = workloads.hopper_dmain(m, S, sigma=0.01)
+    g = ia.ILQR(m, dmain, H, ia.HOPPER_COST, alphas=alphas, select="min_cost")
+    for _ in range(iters):
+        g.iterate()
+    g.synchronize()
+    gt, (K, k), D = g.traj(), g.gains(), g.deriv()
+    V, v = g.value()
+    gc, gsel = g.costs()
+    P = H + 1
+    picked = set()
+    for s in range(S):
+        d = om.make_data()
+        d.set_state(**_state_dict(dmain, s))
+        il = ora.OILQR(om, d, H, cost_fn="ora_cost_desc_fn")
+        il.set_dinit(d)
+        for _ in range(iters):
+            oc, osel = il.iterate_ls(alphas, "min_cost")
+        picked.add(osel)
+        ot, oa = il.traj(), il.arrays()
+        for f in ("time", "qpos", "qvel", "warm", "ctrl"):
+            exact(getattr(gt, f)[s * P:(s + 1) * P].reshape(ot[f].shape), ot[f], f"seed {s} traj.{f}")
+        exact(D[s], oa["deriv"], f"seed {s} deriv")
+        exact(K[s], oa["K"], f"seed {s} K")
+        exact(k[s], oa["k"], f"seed {s} k")
+        exact(V[s], oa["V"], f"seed {s} V")
+        exact(v[s], oa["v"], f"seed {s} v")
+        exact(gc[s], oc, f"seed {s} candidate costs")
+        assert int(gsel[s]) == osel, (s, int(gsel[s]), osel)
+    assert picked != {0}, "the workload must exercise a non-alpha=1 selection"
+
+
+def test_fault_word_reported_once_then_cleared(ia, ora):
+    """A tripped hand-off (preset fault word) is reported by synchronize()
+    exactly once; the next iterate() runs every wait again and is bit-exact."""
+    import workloads
+    m, om = setup(ia, ora, "inverted_pendulum")
+    dmain = workloads.pendulum_dmain(m)
+    g = ia.ILQR(m, dmain, 20, ia.PENDULUM_COST)
+    g.iterate()
+    g.synchronize()
+    g._debug_set_fault(1)
+    with pytest.raises(ia.IlqgError):
+        g.synchronize()
+    g.synchronize()  # reported once: cleared by the read
+    il = _oracle_ilqr(ora, om, _state_dict(dmain, 0), 20, "ora_cost_pendulum", 2)
+    g.iterate()
+    g.synchronize()
+    exact(g.gains()[0][0], il.arrays()["K"], "K after a cleared fault")
+    exact(g.traj().qpos, il.traj()["qpos"], "qpos after a cleared fault")
