@@ -34,10 +34,11 @@ struct Team {
 // stamp would itself wait on memory) and flushed once at kernel end
 #ifdef ILQG_STAMPS
 #define STAMP_N 44
-__device__ unsigned long long g_stamp_acc[48];
-__device__ unsigned long long g_stamp_cnt[48];
-__device__ unsigned long long g_newton_iters;  // all workgroups: Newton iterations
-__device__ unsigned long long g_newton_calls;  // all workgroups: solver calls
+// (per translation unit: the rollout and the FD kernels each read their own copy)
+static __device__ unsigned long long g_stamp_acc[48];
+static __device__ unsigned long long g_stamp_cnt[48];
+static __device__ unsigned long long g_newton_iters;  // all workgroups: Newton iterations
+static __device__ unsigned long long g_newton_calls;  // all workgroups: solver calls
 __shared__ unsigned long long s_stamp_acc[STAMP_N], s_stamp_cnt[STAMP_N], s_stamp_prev, s_stamp_prevb;
 #define STAMP_AT(lane, prev, id)                                             \
   do {                                                                       \

@@ -1,135 +1,14 @@
-// Cooperative hot-path kernels: one 64-lane workgroup (one wavefront) per
+// Cooperative FD-sweep kernels: one 64-lane workgroup (one wavefront) per
 // physics evaluation, workspace in LDS (dcoop.h).
 //   k_fd_centre_coop  src/mjderivative.cpp:61-75   one workgroup per trajectory point
 //   k_fd_cols_coop    src/mjderivative.cpp:78-206  one workgroup per (point, column)
-//   k_rollout_coop    inc/ilqr.h:116-130           one workgroup per (seed, alpha)
-#include <algorithm>
-
-#include "dcoop.h"
-#include "handoff.h"
-#include "kernels.h"
+//   k_fd_fused_*      the sweep with the Riccati recursion (inc/ilqr.h:133-176)
+//                     streamed behind it, one ticketed launch
+#include "coop_common.h"
 #include "riccati.h"
-#include "static_models.h"
 
 namespace ilqg {
 namespace {
-
-using namespace coop;
-
-constexpr double FD_EPS = 1e-6;  // mjderivative.cpp:39
-constexpr int FD_NITER = 30;     // mjderivative.cpp:37
-constexpr int FD_NWARMUP = 3;    // mjderivative.cpp:38
-constexpr int TEAM = TEAM_SIZE;
-// FD teams: at least 2 waves per SIMD (<= 256 VGPRs), so LDS (6 teams per CU
-// for the hopper) and not registers bounds the sweep's occupancy
-constexpr int FD_WAVES_PER_EU = 2;
-#ifndef ILQG_BW_PRIO
-#define ILQG_BW_PRIO 1
-#endif
-
-// LDS: [workspace doubles][coop doubles][model image][workspace ints][coop ints]
-__device__ inline Team make_team(const auto& L, const auto& C) {
-  extern __shared__ double lds[];
-  Team T;
-  T.w = lds;
-  T.c = lds + L.nd;
-  T.iw = reinterpret_cast<int*>(lds + L.nd + C.nd + C.imgd);
-  T.ci = T.iw + L.ni;
-  T.tid = threadIdx.x & (TEAM - 1);  // lane within this wave (two-wave teams: one Team per wave)
-  T.nt = TEAM;  // every cooperative kernel is launched with one 64-lane wavefront
-  return T;
-}
-
-// Stage the read-only model image into LDS (one coalesced copy) and return a
-// DevModel / CoopAux whose array pointers address the LDS copy: every model
-// read on the serial paths then costs an LDS round trip instead of an L2 one.
-__device__ inline void stage_model(const DevModel& g, const CoopAux& Xg, const WsLayout& L, const CoopLayout& C,
-                                   const Team& T, DevModel& m, CoopAux& X) {
-  extern __shared__ double lds[];
-  double* dst = lds + L.nd + C.nd;
-  const double* src = reinterpret_cast<const double*>(g.img);
-  FOR_T(w, C.imgd) dst[w] = src[w];
-  const unsigned char* base = reinterpret_cast<const unsigned char*>(dst);
-  m = g;
-#define ILQG_RB(nm, cnt) \
-  m.nm = reinterpret_cast<decltype(m.nm)>(base + (reinterpret_cast<const unsigned char*>(g.nm) - g.img));
-  ILQG_MODEL_F64_ARRAYS(ILQG_RB)
-  ILQG_MODEL_I32_ARRAYS(ILQG_RB)
-#undef ILQG_RB
-  X.isanc = reinterpret_cast<const int*>(base + (reinterpret_cast<const unsigned char*>(Xg.isanc) - g.img));
-  X.pair = reinterpret_cast<const int*>(base + (reinterpret_cast<const unsigned char*>(Xg.pair) - g.img));
-  X.npair = Xg.npair;
-  X.pmask = Xg.pmask ? reinterpret_cast<const unsigned long long*>(
-                           base + (reinterpret_cast<const unsigned char*>(Xg.pmask) - g.img))
-                     : nullptr;
-  TSYNC();
-}
-
-// model-specific variant: same image copy; sizes/tables are compile-time
-// (static_models.h), float arrays bound at compile-time LDS offsets
-template <class SM>
-__device__ inline void stage_model_s(const DevModel& g, const auto& L, const auto& C, const Team& T, SM& m) {
-  extern __shared__ double lds[];
-  double* dst = lds + L.nd + C.nd;
-  const double* src = reinterpret_cast<const double*>(g.img);
-  FOR_T(w, C.imgd) dst[w] = src[w];
-  m.bind(reinterpret_cast<const unsigned char*>(dst), g);
-  TSYNC();
-}
-
-__device__ inline double cost_terms(double c, const double* x, const double* w, const double* t, const double* l,
-                                    int n) {
-  for (int i = 0; i < n; i++) {
-    double xi = x[i];
-    if (w[i] != 0) {
-      double dx = xi - t[i];
-      c += w[i] * dx * dx;
-    }
-    if (l[i] != 0) c += l[i] * xi;
-  }
-  return c;
-}
-__device__ inline double step_cost(const auto& m, const CostDev& c, const double* qpos, const double* qvel,
-                                   const double* ctrl) {
-  double s = 0;
-  s = cost_terms(s, qpos, c.wq, c.tq, c.lq, m.nq);
-  s = cost_terms(s, qvel, c.wv, c.tv, c.lv, m.nv);
-  s = cost_terms(s, ctrl, c.wu, c.tu, c.lu, m.nu);
-  return s;
-}
-
-// copy the cost descriptor into LDS (C.cdesc): the per-step cost loop on lane 0
-// then reads LDS instead of global memory
-__device__ inline CostDev stage_cost(const auto& m, const auto& C, const Team& T, const CostDev& g) {
-  double* d = T.c + C.cdesc;
-  const int nq = m.nq, nv = m.nv, nu = m.nu;
-  const double* src[9] = {g.wq, g.tq, g.lq, g.wv, g.tv, g.lv, g.wu, g.tu, g.lu};
-  const int off[9] = {0, nq, 2 * nq, 3 * nq, 3 * nq + nv, 3 * nq + 2 * nv, 3 * (nq + nv), 3 * (nq + nv) + nu,
-                      3 * (nq + nv) + 2 * nu};
-  const int len[9] = {nq, nq, nq, nv, nv, nv, nu, nu, nu};
-  for (int a = 0; a < 9; a++) FOR_T(i, len[a]) d[off[a] + i] = src[a][i];
-  TSYNC();
-  CostDev l;
-  l.wq = d + off[0]; l.tq = d + off[1]; l.lq = d + off[2];
-  l.wv = d + off[3]; l.tv = d + off[4]; l.lv = d + off[5];
-  l.wu = d + off[6]; l.tu = d + off[7]; l.lu = d + off[8];
-  return l;
-}
-
-// cpMjData(d, src) from a trajectory record (src/util.cpp:4-14)
-__device__ inline void load_state(const auto& m, const auto& L, const Team& T, const TrajDev& tr, int pt,
-                                  int seed, const double* qfrc_applied, const double* xfrc_applied) {
-  FOR_T(i, m.nq) T.w[L.qpos + i] = tr.qpos[(size_t)pt * m.nq + i];
-  FOR_T(i, m.nv) {
-    T.w[L.qvel + i] = tr.qvel[(size_t)pt * m.nv + i];
-    T.w[L.warm + i] = tr.warm[(size_t)pt * m.nv + i];
-    T.w[L.qfrc_applied + i] = qfrc_applied ? qfrc_applied[(size_t)seed * m.nv + i] : 0.0;
-  }
-  FOR_T(i, m.nu) T.w[L.ctrl + i] = tr.ctrl[(size_t)pt * m.nu + i];
-  FOR_T(i, 6 * m.nbody) T.w[L.xfrc_applied + i] = xfrc_applied ? xfrc_applied[(size_t)seed * 6 * m.nbody + i] : 0.0;
-  if (T.tid == 0) T.w[L.time] = tr.time[pt];
-  TSYNC();
-}
 
 __device__ inline void fd_centre_body(const auto& m, const auto& L, const auto& C, const auto& X, const Team& T,
                                 TrajDev tr, int P, const double* qfrc_applied, const double* xfrc_applied, CostDev cost, double* warm_c, double* cost_c) {
@@ -551,188 +430,11 @@ __global__ __launch_bounds__(TEAM, FD_WAVES_PER_EU) void k_fd_fused_g(DevModel m
   fd_fused_body(m, L, C, X, T, a, t - a.nB);
 }
 
-__device__ inline void rollout_body(const auto& m, const auto& L, const auto& C, const auto& X, const Team& T,
-                                int S, int A, int P, TrajDev nom, TrajDev out, int out_is_cand, const double* K, const double* k, const double* alphas, TrajDev dinit, const double* qfrc_applied, const double* xfrc_applied, int passive, CostDev cost, double* cost_cand, int wave) {
-  // wave < 0: one-wave team; 0/1: primary/helper wave of a two-wave team (step_dual)
-  const bool prim = wave <= 0;
-  STAMP_INIT();
-#ifdef ILQG_STAMPS
-  unsigned long long rt0 = __builtin_amdgcn_s_memrealtime(), mt0 = __builtin_amdgcn_s_memtime();
-#endif
-  const int lane = blockIdx.x;
-  const int s = lane / A, a = lane % A;
-  const int nq = m.nq, nv = m.nv, nu = m.nu, nx = 2 * nv;
-  load_state(m, L, T, dinit, s, s, qfrc_applied, xfrc_applied);
-  const CostDev cl = stage_cost(m, C, T, cost);
-  double* qpos = T.w + L.qpos;
-  double* qvel = T.w + L.qvel;
-  double* ctrl = T.w + L.ctrl;
-  double* warm = T.w + L.warm;
-  double* dx = T.w + L.s_fd;
-  // per-point record of the nominal trajectory and gains, [x*_q | x*_v | u* | K | k],
-  // prefetched one point ahead into registers and parked in LDS (C.rec)
-  double* rec = T.c + C.rec;
-  const int R = nq + nv + nu + nu * nx + nu;
-  const double* rq = rec;
-  const double* rv = rec + nq;
-  const double* ru = rec + nq + nv;
-  const double* rK = ru + nu;
-  const double* rk = rK + nu * nx;
-  auto fetch = [&](size_t pn, int t) -> double {
-    if (t < nq) return nom.qpos[pn * nq + t];
-    t -= nq;
-    if (t < nv) return nom.qvel[pn * nv + t];
-    t -= nv;
-    if (t < nu) return nom.ctrl[pn * nu + t];
-    t -= nu;
-    if (t < nu * nx) return K[pn * nu * nx + t];
-    return k[pn * nu + t - nu * nx];
-  };
-  constexpr int PFR = 4;  // registers per lane: R <= 4 * 64
-  double pf[PFR];
-  if (!passive) {
-    FOR_T(t, R) rec[t] = fetch((size_t)s * P + (P - 1), t);
-    TSYNC();
-  }
-  const double alpha = alphas ? alphas[a] : 1.0;
-  const int ob = out_is_cand ? lane : s;
-  // the wave that runs the control law and writes the record: the helper wave
-  // of a two-wave team (beside the primary's kinematics), else the only wave
-  const bool ctl = wave != 0;
-  double c = 0;
-  // control law u = u* + alpha k + K (x - x*) for point n, its record and cost
-  // (ilqr.h:116-133); the next point's nominal record is prefetched first
-  auto pre_step = [&](int n) {
-    const bool pre = !passive && n > 0;
-    if (pre) {
-      const size_t pn1 = (size_t)s * P + (n - 1);
-#pragma unroll
-      for (int q = 0; q < PFR; q++) {
-        const int t = T.tid + q * TEAM_SIZE;
-        pf[q] = t < R ? fetch(pn1, t) : 0.0;
-      }
-    }
-    if (!passive) {
-      FOR_T(j, nx) dx[j] = j < nv ? state_diff_dof(m, j, qpos, rq) : qvel[j - nv] - rv[j - nv];
-      TSYNC();
-      FOR_T(i, nu) {
-        double t = 0;
-        for (int j = 0; j < nx; j++) t += rK[i + j * nu] * dx[j];
-        ctrl[i] = (t + alpha * rk[i]) + ru[i];
-      }
-      TSYNC();
-    }
-    const size_t po = (size_t)ob * P + n;
-    FOR_T(i, nq) out.qpos[po * nq + i] = qpos[i];
-    FOR_T(i, nv) {
-      out.qvel[po * nv + i] = qvel[i];
-      out.warm[po * nv + i] = warm[i];
-    }
-    FOR_T(i, nu) out.ctrl[po * nu + i] = ctrl[i];
-    if (T.tid == 0) {
-      out.time[po] = T.w[L.time];
-      c += step_cost(m, cl, qpos, qvel, ctrl);
-    }
-    TSYNC();
-  };
-  // the prefetched record replaces the current one once the step no longer reads it
-  auto park = [&](int n) {
-    if (!passive && n > 0) {
-#pragma unroll
-      for (int q = 0; q < PFR; q++) {
-        const int t = T.tid + q * TEAM_SIZE;
-        if (t < R) rec[t] = pf[q];
-      }
-      TSYNC();
-    }
-  };
-  if (wave >= 0) __syncthreads();
-  for (int n = P - 1; n >= 0; n--) {
-    if (wave < 0) {
-      pre_step(n);
-      step(m, L, C, X, T);
-      park(n);
-    } else {
-      step_dual(m, L, C, X, T, wave, [&]() {
-        pre_step(n);
-        park(n);
-      });
-    }
-  }
-  if (ctl && T.tid == 0 && cost_cand) cost_cand[lane] = c;
-#ifdef ILQG_STAMPS
-  if (prim && T.tid == 0 && blockIdx.x == 0) {
-    g_stamp_acc[46] += __builtin_amdgcn_s_memrealtime() - rt0;
-    g_stamp_acc[47] += __builtin_amdgcn_s_memtime() - mt0;
-  }
-#endif
-  STAMP_FLUSH();
-}
-
-__global__ __launch_bounds__(TEAM) void k_rollout_coop(DevModel mg, WsLayout L, CoopLayout C, CoopAux Xg, int S, int A, int P, TrajDev nom, TrajDev out, int out_is_cand, const double* K, const double* k, const double* alphas, TrajDev dinit, const double* qfrc_applied, const double* xfrc_applied, int passive, CostDev cost, double* cost_cand) {
-  Team T = make_team(L, C);
-  DevModel m;
-  CoopAux X;
-  stage_model(mg, Xg, L, C, T, m, X);
-  rollout_body(m, L, C, X, T, S, A, P, nom, out, out_is_cand, K, k, alphas, dinit, qfrc_applied, xfrc_applied, passive, cost, cost_cand, -1);
-}
-
-// model-specific instance (static_models.h): compile-time sizes, tables and LDS layout
-template <class SM, class SX>
-__global__ __launch_bounds__(TEAM) void k_rollout_s(DevModel mg, int S, int A, int P, TrajDev nom, TrajDev out, int out_is_cand, const double* K, const double* k, const double* alphas, TrajDev dinit, const double* qfrc_applied, const double* xfrc_applied, int passive, CostDev cost, double* cost_cand) {
-  static constexpr WsLayout L = make_layout(SM{}, SX::npair);
-  static constexpr CoopLayout C = make_coop_layout(SM{}, SX::npair);
-  static constexpr SX X{};
-  Team T = make_team(L, C);
-  SM m;
-  stage_model_s(mg, L, C, T, m);
-  rollout_body(m, L, C, X, T, S, A, P, nom, out, out_is_cand, K, k, alphas, dinit, qfrc_applied, xfrc_applied, passive, cost, cost_cand, -1);
-}
-
-// two-wave teams (step_dual): 128 threads per (seed, candidate)
-__global__ __launch_bounds__(2 * TEAM) void k_rollout2_coop(DevModel mg, WsLayout L, CoopLayout C, CoopAux Xg, int S, int A, int P, TrajDev nom, TrajDev out, int out_is_cand, const double* K, const double* k, const double* alphas, TrajDev dinit, const double* qfrc_applied, const double* xfrc_applied, int passive, CostDev cost, double* cost_cand) {
-  Team T = make_team(L, C);
-  DevModel m;
-  CoopAux X;
-  stage_model(mg, Xg, L, C, T, m, X);
-  rollout_body(m, L, C, X, T, S, A, P, nom, out, out_is_cand, K, k, alphas, dinit, qfrc_applied, xfrc_applied,
-               passive, cost, cost_cand, (int)(threadIdx.x / TEAM));
-}
-template <class SM, class SX>
-__global__ __launch_bounds__(2 * TEAM) void k_rollout2_s(DevModel mg, int S, int A, int P, TrajDev nom, TrajDev out, int out_is_cand, const double* K, const double* k, const double* alphas, TrajDev dinit, const double* qfrc_applied, const double* xfrc_applied, int passive, CostDev cost, double* cost_cand) {
-  static constexpr WsLayout L = make_layout(SM{}, SX::npair);
-  static constexpr CoopLayout C = make_coop_layout(SM{}, SX::npair);
-  static constexpr SX X{};
-  Team T = make_team(L, C);
-  SM m;
-  stage_model_s(mg, L, C, T, m);
-  rollout_body(m, L, C, X, T, S, A, P, nom, out, out_is_cand, K, k, alphas, dinit, qfrc_applied, xfrc_applied,
-               passive, cost, cost_cand, (int)(threadIdx.x / TEAM));
-}
-
-template <typename K>
-hipError_t allow_lds(K kern, size_t lds) {
-  if (lds <= 65536) return hipSuccess;
-  return hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
-                             (int)lds);
-}
-
 }  // namespace
-
-// rollouts on two-wave teams (step_dual); ILQG_DUAL=0 selects one-wave teams (A/B)
-static bool use_dual() {
-  static int v = -1;
-  if (v < 0) {
-    const char* e = getenv("ILQG_DUAL");
-    v = (e && e[0] == '0') ? 0 : 1;
-  }
-  return v == 1;
-}
 
 size_t coop_lds_bytes(const WsLayout& L, const CoopLayout& C) {
   return (size_t)(L.nd + C.nd + C.imgd) * sizeof(double) + (size_t)(L.ni + C.ni) * sizeof(int);
 }
-
 hipError_t launch_fd_centre_coop(const DevModel& m, const WsLayout& L, const CoopLayout& C, const CoopAux& X,
                                  TrajDev tr, int npts, int P, const double* qfrc_applied, const double* xfrc_applied,
                                  CostDev cost, double* warm_c, double* cost_c, hipStream_t st) {
@@ -829,66 +531,6 @@ hipError_t launch_fd_fused_coop(const DevModel& m, const WsLayout& L, const Coop
   return hipGetLastError();
 }
 
-// LDS a rollout workgroup reserves: its workspace, or (ILQG_ROLLOUT_LDS) more,
-// so that no FD team can share its CU
-static size_t rollout_lds(size_t need) {
-  static long pad = -1;
-  if (pad < 0) {
-    const char* e = getenv("ILQG_ROLLOUT_LDS");
-    pad = e ? atol(e) : 0;
-  }
-  return (size_t)pad > need ? (size_t)pad : need;
-}
-
-hipError_t launch_rollout_coop(const DevModel& m, const WsLayout& L, const CoopLayout& C, const CoopAux& X, int S,
-                               int A, int P, TrajDev nominal, TrajDev out, int out_is_cand, const double* K,
-                               const double* k, const double* alphas, TrajDev dinit, const double* qfrc_applied,
-                               const double* xfrc_applied, int passive, CostDev cost, double* cost_cand,
-                               hipStream_t st) {
-  const size_t lds = rollout_lds(coop_lds_bytes(L, C));
-  hipError_t e;
-  if (use_dual()) {
-#define ILQG_CASE(id, SMT, SXT)                                                                                 \
-  case id:                                                                                                      \
-    e = allow_lds(k_rollout2_s<stat::SMT, stat::SXT>, lds);                                                     \
-    if (e != hipSuccess) return e;                                                                              \
-    hipLaunchKernelGGL((k_rollout2_s<stat::SMT, stat::SXT>), dim3(S * A), dim3(2 * TEAM), lds, st, m, S, A, P,   \
-                       nominal, out, out_is_cand, K, k, alphas, dinit, qfrc_applied, xfrc_applied, passive, cost, \
-                       cost_cand);                                                                              \
-    return hipGetLastError();
-    switch (m.static_id) {
-      ILQG_STATIC_MODELS(ILQG_CASE)
-      default:
-        break;
-    }
-#undef ILQG_CASE
-    e = allow_lds(k_rollout2_coop, lds);
-    if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(k_rollout2_coop, dim3(S * A), dim3(2 * TEAM), lds, st, m, L, C, X, S, A, P, nominal, out,
-                       out_is_cand, K, k, alphas, dinit, qfrc_applied, xfrc_applied, passive, cost, cost_cand);
-    return hipGetLastError();
-  }
-#define ILQG_CASE(id, SMT, SXT)                                                                                 \
-  case id:                                                                                                      \
-    e = allow_lds(k_rollout_s<stat::SMT, stat::SXT>, lds);                                                      \
-    if (e != hipSuccess) return e;                                                                              \
-    hipLaunchKernelGGL((k_rollout_s<stat::SMT, stat::SXT>), dim3(S * A), dim3(TEAM), lds, st, m, S, A, P,        \
-                       nominal, out, out_is_cand, K, k, alphas, dinit, qfrc_applied, xfrc_applied, passive, cost, \
-                       cost_cand);                                                                              \
-    return hipGetLastError();
-  switch (m.static_id) {
-    ILQG_STATIC_MODELS(ILQG_CASE)
-    default:
-      break;
-  }
-#undef ILQG_CASE
-  e = allow_lds(k_rollout_coop, coop_lds_bytes(L, C));
-  if (e != hipSuccess) return e;
-  hipLaunchKernelGGL(k_rollout_coop, dim3(S * A), dim3(TEAM), coop_lds_bytes(L, C), st, m, L, C, X, S, A, P, nominal,
-                     out, out_is_cand, K, k, alphas, dinit, qfrc_applied, xfrc_applied, passive, cost, cost_cand);
-  return hipGetLastError();
-}
-
 }  // namespace ilqg
 
 #ifdef ILQG_STAMPS
@@ -900,7 +542,11 @@ extern "C" int ilqg_debug_fused(unsigned long long* d, int reset) {
   }
   return 0;
 }
-extern "C" int ilqg_debug_stamps(unsigned long long* acc, unsigned long long* cnt, int reset) {
+#endif
+
+#ifdef ILQG_STAMPS
+// the FD kernels' copy of the stamp counters (tools/stamps.py)
+extern "C" int ilqg_debug_stamps_fd(unsigned long long* acc, unsigned long long* cnt, int reset) {
   if (hipMemcpyFromSymbol(acc, HIP_SYMBOL(ilqg::coop::g_stamp_acc), sizeof(unsigned long long) * 48) != hipSuccess)
     return 3;
   if (hipMemcpyFromSymbol(cnt, HIP_SYMBOL(ilqg::coop::g_stamp_cnt), sizeof(unsigned long long) * 48) != hipSuccess)

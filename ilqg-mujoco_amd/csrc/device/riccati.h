@@ -21,6 +21,8 @@
   } while (0)
 #endif
 
+#include "riccati_reg.h"
+
 namespace ilqg {
 
 constexpr int BW_THREADS = 64;  // one wavefront: its barriers compile to nothing
@@ -95,6 +97,15 @@ __device__ inline void backward_seed(const MD& m, int nq, int nv_rt, int nu_rt, 
                                      const double* deriv, int Ds, TrajDev tr, double* Kg, double* kg, double* Vg,
                                      double* vg, int s, int tid, double* sh, const unsigned* done, unsigned target,
                                      unsigned* fault) {
+#ifndef ILQG_RIC_LDS
+  // bundled small models: the register/exchange formulation (riccati_reg.h)
+  if constexpr (RicReg<NV_, NU_>::ok) {
+    if (nq == NV_) {
+      backward_seed_reg<NV_, NU_>(m, P, dt, mu, deriv, Ds, tr, Kg, kg, Vg, vg, s, tid, sh, done, target, fault);
+      return;
+    }
+  }
+#endif
   const int nv = NV_ > 0 ? NV_ : nv_rt;
   const int nu = NU_ > 0 ? NU_ : nu_rt;
   const int nx = 2 * nv, D = nv * (2 * nv + nu) + 2 * nv + nu;

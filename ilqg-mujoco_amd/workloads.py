@@ -17,7 +17,7 @@ import numpy as np
 import ilqg_amd as ia
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-MODEL_DIR = os.path.join(os.path.dirname(HERE), "tests", "golden", "models")
+MODEL_DIR = os.path.join(HERE, "models")
 LINESEARCH_ALPHAS = tuple(2.0 ** -i for i in range(8))  # cfg3: {2^-i, i=0..7}
 
 

@@ -9,7 +9,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 PKG = os.path.join(ROOT, "ilqg-mujoco_amd")
 ORACLE = os.path.join(ROOT, "oracle")
 GOLDEN = os.path.join(ROOT, "tests", "golden")
-MODELS = os.path.join(GOLDEN, "models")
+MODELS = os.path.join(PKG, "models")
 for p in (PKG, ORACLE):
     if p not in sys.path:
         sys.path.insert(0, p)

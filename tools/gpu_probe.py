@@ -3,7 +3,7 @@ import sys, time, os, numpy as np
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "ilqg-mujoco_amd")); sys.path.insert(0, os.path.join(ROOT, "oracle"))
 import ilqg_amd as ia, oracle as ora
-RES = os.path.join(ROOT, "tests", "golden", "models")
+RES = os.path.join(ROOT, "ilqg-mujoco_amd", "models")
 
 def rep(name, a, b):
     a = np.asarray(a); b = np.asarray(b)

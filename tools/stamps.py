@@ -22,12 +22,13 @@ dmain = workloads.hopper_dmain(m, 1) if m.nv == 6 else workloads.pendulum_dmain(
 g = ia.ILQR(m, dmain, 500 if m.nv == 6 else 200, ia.HOPPER_COST if m.nv == 6 else ia.PENDULUM_COST)
 g.iterate(); g.synchronize()
 g.set_timing(True)
-for what, fn in (("rollout (1 seed)", g.forward_pass), ("fd sweep", g.fd_sweep)):
-    L.ilqg_debug_stamps(acc, cnt, 1)
+for what, fn, rd in (("rollout (1 seed)", g.forward_pass, L.ilqg_debug_stamps),
+                     ("fd sweep", g.fd_sweep, L.ilqg_debug_stamps_fd)):
+    rd(acc, cnt, 1)
     g.timing()
     fn(); g.synchronize()
     tm = g.timing()
-    L.ilqg_debug_stamps(acc, cnt, 1)
+    rd(acc, cnt, 1)
     tot = sum(acc[i] for i in list(range(10)) + list(range(24, 30)))
     ms = sum(v[0] for v in tm.values())
     print(f"== {what}: block 0, lane 0, total {tot} ticks (wave-0 stages + barriers); kernel time {ms:.3f} ms "
