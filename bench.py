@@ -33,6 +33,20 @@ from seed_shard import CostExchange, device_view, max_over_ranks, seed_offset  #
 
 METRIC = "iLQR iterations/sec (FD+backward+forward) for Hopper H=500 at 1/2/4/8 GPUs"
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md chip table (spec)
+# FP64 vector peak: 256 CUs x 4 SIMDs x 16 f64 FMA lanes/clk x 2 x 2.4 GHz (AMD spec
+# 78.6 TFLOP/s; half the guide's 157.3 TFLOP/s FP32 vector rate)
+FP64_PEAK_TFS = 78.6
+FLOPS_JSON = os.path.join(ROOT, "tests", "fixtures", "flops.json")
+
+
+def algorithmic_flops(S, A, P):
+    """fp64 flops per launch from the instrumented oracle's counts
+    (tests/fixtures/flops.json): the rollout = S*A*P mj_steps,
+    the fused sweep = S*P calcMJDerivatives calls + S*(P-1) Riccati steps."""
+    with open(FLOPS_JSON) as f:
+        h = json.load(f)["models"]["hopper"]
+    return {"rollout": S * A * P * h["step"]["flops"],
+            "fd_backward": S * (P * h["fd_point"]["flops"] + (P - 1) * h["riccati_step"]["flops"])}
 
 
 def algorithmic_bytes(m, S, A, P):
@@ -193,6 +207,14 @@ def main():
         with open(pmc) as f:
             traffic = json.load(f).get(dom)
 
+    # the binding roof: FP64 VALU (algorithmic flops / launch time vs the vector peak)
+    aflops = algorithmic_flops(S, A, P)
+    valu = {k: {"flops_per_launch": f, "avg_launch_ms": gtime[k] / max(1, per_kernel[k]["launches"]),
+                "achieved_tflops": f / (gtime[k] / max(1, per_kernel[k]["launches"]) * 1e-3) / 1e12
+                if per_kernel[k]["launches"] else 0.0} for k, f in aflops.items()}
+    for v in valu.values():
+        v["frac"] = v["achieved_tflops"] / FP64_PEAK_TFS
+
     out = {
         "metric": METRIC,
         "value": value,
@@ -212,7 +234,9 @@ def main():
         "roofline": {"bound": "hbm", "kernel": dom, "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                      "algorithmic_bytes_per_launch": abytes[dom], "avg_launch_ms": dom_avg_ms,
-                     "note": "latency/FP64-VALU-bound path; HBM fraction reported per contract"},
+                     "note": "latency/FP64-VALU-bound path; HBM fraction reported per contract",
+                     "valu": {"bound": "fp64-valu", "peak_tflops": FP64_PEAK_TFS, "unit": "TFLOP/s",
+                              "flops_source": "tests/fixtures/flops.json (instrumented oracle)", "kernels": valu}},
         "kernels": per_kernel,
         "best_seed": best_seed,
     }

@@ -256,27 +256,11 @@ struct ilqg_solver {
   std::vector<double> host_alphas;
   bool initialized = false;
   hipStream_t own_stream = nullptr;
-  // seed groups (ilqg_solver_set_groups): contiguous seed ranges; each group's
-  // rollout runs on its own stream (rs) so one group's latency-bound rollout
-  // overlaps another group's FD sweep; the sweeps run on fs (one stream shared
-  // by the groups -- they take turns -- unless ILQG_GROUP_TOKEN=0).  Optional
-  // CU masks (ILQG_ROLL_CUS) keep the rollout and sweep streams on disjoint CUs:
-  // without them a running sweep refills every CU slot it frees and a rollout
-  // launched behind it cannot start until the sweep has drained.
-  // (A split variant -- the Riccati recursion as a launch of its own on a third
+  // (A split variant -- the Riccati recursion as a launch of its own on a second
   // stream, streaming a concurrent sweep launch's records -- deadlocked when the
   // two streams shared a hardware queue: HIP does not guarantee that two
   // launches run concurrently, so every producer/consumer pair stays inside one
   // ticketed launch.)
-  struct Group {
-    int s0 = 0, ns = 0;
-    hipStream_t rs = nullptr, fs = nullptr;
-    hipEvent_t costs = nullptr, fd = nullptr;
-    unsigned* sync = nullptr;
-  };
-  std::vector<Group> groups;  // empty: one group, on `stream`
-  hipStream_t fstream = nullptr;  // shared sweep stream
-  hipEvent_t ev_start = nullptr;
   bool timing = false;
   std::vector<std::pair<hipEvent_t, hipEvent_t>> ev[ILQG_NKERNEL];
   std::vector<hipEvent_t> event_pool;
@@ -317,30 +301,9 @@ struct ilqg_solver {
                    c + 3 * nq + 3 * nv, c + 3 * nq + 3 * nv + nu, c + 3 * nq + 3 * nv + 2 * nu};
   }
   WsDev ws() const { return WsDev{wsd.as<double>(), wsi.as<int>(), nlanes}; }
-  void free_groups() {
-    for (auto& g : groups) {
-      if (g.rs) (void)hipStreamDestroy(g.rs);
-      if (g.fs && g.fs != fstream) (void)hipStreamDestroy(g.fs);
-      for (hipEvent_t e : {g.costs, g.fd})
-        if (e) (void)hipEventDestroy(e);
-    }
-    groups.clear();
-    if (fstream) (void)hipStreamDestroy(fstream);
-    fstream = nullptr;
-  }
-  // every stream the solver launches on
-  hipError_t sync_all() {
-    hipError_t e = hipStreamSynchronize(stream);
-    for (auto& g : groups) {
-      if (e == hipSuccess) e = hipStreamSynchronize(g.rs);
-      if (e == hipSuccess) e = hipStreamSynchronize(g.fs);
-    }
-    return e;
-  }
+  hipError_t sync_all() { return hipStreamSynchronize(stream); }
   ~ilqg_solver() {
     (void)sync_all();
-    free_groups();
-    if (ev_start) (void)hipEventDestroy(ev_start);
     for (auto& v : ev)
       for (auto& p : v) {
         (void)hipEventDestroy(p.first);
@@ -678,7 +641,7 @@ int ilqg_solver_create(const ilqg_model* mc, const ilqg_solver_opts* o, const il
   ALLOC(s->deriv, S * P * s->Dp * 8);
   if (s->fused) {
     ALLOC(s->cw, S * P * s->WCp * 8);
-    ALLOC(s->sync, sync_bytes(S * P) + S * 32);  // + per-seed-group header and padding
+    ALLOC(s->sync, sync_bytes(S * P));
   }
   ALLOC(s->fault, 16);
   ALLOC(s->warm_c, S * P * h.nv * 8);
@@ -715,7 +678,7 @@ static int upload_state(ilqg_solver* s, DevBuf* dst, size_t npts, const double* 
   const HostModel& h = s->model->host;
   const double* src[5] = {time, qpos, qvel, warm, ctrl};
   const size_t fld[5] = {1, (size_t)h.nq, (size_t)h.nv, (size_t)h.nv, (size_t)h.nu};
-  HIPCHK(s->sync_all());  // no group still reading the buffers being replaced
+  HIPCHK(s->sync_all());  // no launch still reading the buffers being replaced
   for (int f = 0; f < 5; f++)
     if (src[f]) HIPCHK(hipMemcpyAsync(dst[f].p, src[f], npts * fld[f] * 8, hipMemcpyHostToDevice, s->stream));
     else HIPCHK(hipMemsetAsync(dst[f].p, 0, npts * fld[f] * 8, s->stream));
@@ -834,9 +797,8 @@ static TrajDev toff(TrajDev t, size_t pts, const HostModel& h) {
   return TrajDev{t.time + pts, t.qpos + pts * h.nq, t.qvel + pts * h.nv, t.warm + pts * h.nv, t.ctrl + pts * h.nu};
 }
 
-// rollout of every (seed, alpha) candidate of the range, then selection + setDInit.
-// before_select: an event the selection waits on (its outputs may still be read there)
-static hipError_t forward_range(ilqg_solver* s, const SeedRange& r, hipEvent_t before_select) {
+// rollout of every (seed, alpha) candidate of the range, then selection + setDInit
+static hipError_t forward_range(ilqg_solver* s, const SeedRange& r) {
   const ilqg_model* m = s->model;
   const HostModel& h = m->host;
   const size_t s0 = r.s0, P = s->P, A = s->A, nx = s->nx;
@@ -856,10 +818,6 @@ static hipError_t forward_range(ilqg_solver* s, const SeedRange& r, hipEvent_t b
                           s->alphas.as<double>(), di, qa, xf, 0, s->cview(), cc, r.st);
   }, r.st);
   if (e != hipSuccess) return e;
-  if (before_select) {
-    e = hipStreamWaitEvent(r.st, before_select, 0);
-    if (e != hipSuccess) return e;
-  }
   return s->timed(1, [&] {
     return launch_select(m->dm, r.ns, s->A, s->P, s->opts.select_mode, multi ? 1 : 0, cc, s->sel.as<int>() + s0,
                          s->cost_sel.as<double>() + s0, outv, nom, di, r.st);
@@ -868,8 +826,7 @@ static hipError_t forward_range(ilqg_solver* s, const SeedRange& r, hipEvent_t b
 
 int ilqg_forward(ilqg_solver* s) {
   if (!s || !s->initialized) return fail(ILQG_ERR_ARG, "solver not initialised");
-  if (!s->groups.empty()) HIPCHK(s->sync_all());  // a lone forward pass: every group's state settled
-  HIPCHK(forward_range(s, whole(s), nullptr));
+  HIPCHK(forward_range(s, whole(s)));
   return ILQG_OK;
 }
 
@@ -916,7 +873,6 @@ int ilqg_fd_sweep(ilqg_solver* s) {
   TrajDev nom = s->tview(s->traj);
   const int npts = s->S * s->P;
   if (s->fused) {
-    if (!s->groups.empty()) HIPCHK(s->sync_all());
     HIPCHK(s->timed(3, [&] { return fused_launch(s, whole(s), 0); }));
     return ILQG_OK;
   }
@@ -944,7 +900,6 @@ int ilqg_fd_sweep(ilqg_solver* s) {
 int ilqg_backward(ilqg_solver* s) {
   if (!s || !s->initialized) return fail(ILQG_ERR_ARG, "solver not initialised");
   const ilqg_model* m = s->model;
-  if (!s->groups.empty()) HIPCHK(s->sync_all());
   HIPCHK(s->timed(4, [&] {
     return launch_backward(m->dm, s->S, s->P, s->opts.mu, s->deriv.as<double>(), s->Dp, s->tview(s->traj),
                            s->K.as<double>(), s->k.as<double>(), s->V.as<double>(), s->v.as<double>(), s->stream);
@@ -952,33 +907,8 @@ int ilqg_backward(ilqg_solver* s) {
   return ILQG_OK;
 }
 
-// seed groups: per group g on its own stream, rollout + selection (the selection
-// after the solver stream's start-of-iteration point, where the previous
-// iteration's costs may still be read), then the fused sweep (after group g-1's
-// sweep of this iteration when the token is on).  The solver stream waits for
-// every group's selection only: per-seed costs of this iteration are ordered
-// there, while the sweeps run on behind it.
-static int iterate_groups(ilqg_solver* s) {
-  if (!s->ev_start) HIPCHK(hipEventCreateWithFlags(&s->ev_start, hipEventDisableTiming));
-  HIPCHK(hipEventRecord(s->ev_start, s->stream));
-  for (auto& gr : s->groups) {
-    // the rollout reads the gains and overwrites the trajectory the group's
-    // previous sweep read: after that sweep
-    HIPCHK(hipStreamWaitEvent(gr.rs, gr.fd, 0));
-    HIPCHK(forward_range(s, SeedRange{gr.s0, gr.ns, gr.rs, gr.sync}, s->ev_start));
-    HIPCHK(hipEventRecord(gr.costs, gr.rs));
-    HIPCHK(hipStreamWaitEvent(gr.fs, gr.costs, 0));
-    SeedRange r{gr.s0, gr.ns, gr.fs, gr.sync};
-    HIPCHK(s->timed(5, [&] { return fused_launch(s, r, 1); }, gr.fs));
-    HIPCHK(hipEventRecord(gr.fd, gr.fs));
-  }
-  for (auto& gr : s->groups) HIPCHK(hipStreamWaitEvent(s->stream, gr.costs, 0));
-  return ILQG_OK;
-}
-
 int ilqg_iterate(ilqg_solver* s) {
   if (!s || !s->initialized) return fail(ILQG_ERR_ARG, "solver not initialised");
-  if (!s->groups.empty()) return iterate_groups(s);
   int rc = ilqg_forward(s);
   if (rc) return rc;
   if (s->fused) {
@@ -1048,70 +978,6 @@ int ilqg_solver_get_timing(ilqg_solver* s, double* ms, int* launches) {
     if (launches) launches[k] = (int)s->ev[k].size();
     s->ev[k].clear();
   }
-  return ILQG_OK;
-}
-
-int ilqg_solver_set_groups(ilqg_solver* s, int ngroups) {
-  if (!s || ngroups < 1) return fail(ILQG_ERR_ARG, "bad argument");
-  HIPCHK(s->sync_all());
-  s->free_groups();
-  ngroups = std::min(ngroups, s->S);
-  if (ngroups == 1) return ILQG_OK;
-  if (!s->fused) return fail(ILQG_ERR_UNSUPPORTED, "seed groups need the fused FD sweep (cooperative model kernels)");
-  const bool token = getenv_int("ILQG_GROUP_TOKEN", 1) != 0;
-  const int roll_cus = getenv_int("ILQG_ROLL_CUS", 0);
-  // CU masks: the rollout streams get roll_cus CUs spread evenly over the chip
-  // (every k-th CU), the sweep streams the rest
-  int ncu = 0;
-  HIPCHK(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, s->opts.device));
-  std::vector<uint32_t> rmask((ncu + 31) / 32, 0), fmask(rmask);
-  const bool masked = roll_cus > 0 && roll_cus < ncu;
-  if (masked) {
-    for (int c = 0, j = 0; c < ncu; c++) {
-      const bool r = j < roll_cus && (long)c * roll_cus / ncu >= j;
-      if (r) j++;
-      (r ? rmask : fmask)[c / 32] |= 1u << (c % 32);
-    }
-  }
-  auto mkstream = [&](hipStream_t* st, std::vector<uint32_t>& mask) {
-    return masked ? hipExtStreamCreateWithCUMask(st, (uint32_t)mask.size(), mask.data())
-                  : hipStreamCreateWithFlags(st, hipStreamNonBlocking);
-  };
-  if (token) {
-    hipError_t e = mkstream(&s->fstream, fmask);
-    if (e != hipSuccess) return hip_fail(e, "seed group sweep stream");
-  }
-  s->groups.resize(ngroups);
-  const size_t P = s->P;
-  size_t off = 0;  // u32 words into the sync block, 16-byte aligned per group
-  for (int g = 0; g < ngroups; g++) {
-    auto& gr = s->groups[g];
-    gr.s0 = (int)((long)s->S * g / ngroups);
-    gr.ns = (int)((long)s->S * (g + 1) / ngroups) - gr.s0;
-    gr.sync = s->sync.as<unsigned>() + off;
-    off += sync_bytes((size_t)gr.ns * P) / 4;
-    hipError_t e = mkstream(&gr.rs, rmask);
-    if (e == hipSuccess) {
-      if (token) gr.fs = s->fstream;
-      else e = mkstream(&gr.fs, fmask);
-    }
-    if (e == hipSuccess) e = hipEventCreateWithFlags(&gr.costs, hipEventDisableTiming);
-    if (e == hipSuccess) e = hipEventCreateWithFlags(&gr.fd, hipEventDisableTiming);
-    if (e != hipSuccess) {
-      s->free_groups();
-      return hip_fail(e, "seed group streams");
-    }
-  }
-  if (off * 4 > s->sync.n) {
-    s->free_groups();
-    return fail(ILQG_ERR_ARG, "seed groups: hand-off block too small");
-  }
-  return ILQG_OK;
-}
-
-int ilqg_solver_get_groups(ilqg_solver* s, int* ngroups) {
-  if (!s || !ngroups) return fail(ILQG_ERR_ARG, "bad argument");
-  *ngroups = s->groups.empty() ? 1 : (int)s->groups.size();  // 1 either way for one group
   return ILQG_OK;
 }
 

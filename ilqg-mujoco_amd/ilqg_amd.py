@@ -61,7 +61,7 @@ EXPORTS = [
     "ilqg_solver_get_deriv", "ilqg_solver_set_deriv", "ilqg_solver_get_value", "ilqg_solver_get_costs",
     "ilqg_forward", "ilqg_fd_sweep", "ilqg_backward", "ilqg_iterate", "ilqg_synchronize",
     "ilqg_solver_stream", "ilqg_solver_device_costs", "ilqg_solver_set_stream", "ilqg_solver_set_timing",
-    "ilqg_solver_get_timing", "ilqg_solver_set_groups", "ilqg_solver_get_groups",
+    "ilqg_solver_get_timing",
     "ilqg_solver_debug_set_fault", "ilqg_solver_device_traj",
 ]
 KERNELS = ("rollout", "select", "fd_centre", "fd_cols", "backward", "fd_backward")
@@ -366,6 +366,11 @@ class ILQR:
         _check(lib().ilqg_fd_sweep(self._h), "ilqg_fd_sweep")
         _check(lib().ilqg_backward(self._h), "ilqg_backward")
 
+    def riccati_pass(self):
+        """initV + the Riccati recursion over the resident FD records (ilqg_backward),
+        without a sweep: the records are whatever set_deriv / the last sweep left"""
+        _check(lib().ilqg_backward(self._h), "ilqg_backward")
+
     def iterate(self):
         _check(lib().ilqg_iterate(self._h), "ilqg_iterate")
 
@@ -379,16 +384,6 @@ class ILQR:
     def set_stream(self, stream: Optional[int]):
         """enqueue on an external hipStream_t (e.g. torch.cuda.current_stream().cuda_stream)"""
         _check(lib().ilqg_solver_set_stream(self._h, ctypes.c_void_p(stream) if stream else None), "set_stream")
-
-    def set_groups(self, ngroups: int):
-        """pipeline the seeds as `ngroups` groups on their own streams (ilqg_solver_set_groups)"""
-        _check(lib().ilqg_solver_set_groups(self._h, int(ngroups)), "set_groups")
-
-    @property
-    def groups(self) -> int:
-        n = ctypes.c_int()
-        _check(lib().ilqg_solver_get_groups(self._h, ctypes.byref(n)), "get_groups")
-        return n.value
 
     def set_timing(self, enable: bool):
         _check(lib().ilqg_solver_set_timing(self._h, int(enable)), "set_timing")

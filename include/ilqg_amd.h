@@ -159,17 +159,6 @@ int ilqg_solver_device_costs(ilqg_solver* s, double** dptr);
    applied control): the multi-GPU MPC broadcast of the winning seed's first
    control reads it in place */
 int ilqg_solver_device_traj(ilqg_solver* s, int field, double** dptr);
-/* seed groups (an MI355X extension; no reference counterpart): split the
-   nseed seeds into ngroups contiguous ranges, each iterated on its own stream,
-   so one group's latency-bound rollout overlaps another group's FD sweep.
-   ilqg_iterate then orders on the solver stream only the completion of every
-   group's rollout + selection (the per-seed costs, ilqg_solver_device_costs);
-   every other entry point synchronises all groups first.  Results are
-   bit-identical to ngroups = 1 (seeds are independent).  Needs the fused FD
-   sweep (cooperative model kernels): ILQG_ERR_UNSUPPORTED otherwise. */
-int ilqg_solver_set_groups(ilqg_solver* s, int ngroups);
-int ilqg_solver_get_groups(ilqg_solver* s, int* ngroups);
-
 #ifdef __cplusplus
 }
 #endif

@@ -21,7 +21,12 @@
 extern "C" {
 #endif
 
+#ifdef ORA_MJTNUM
+typedef ORA_MJTNUM mjtNum; /* instrumented flop-counting build (oracle/flops) */
+#else
 typedef double mjtNum;
+#define ORA_FLOP_TRANS() ((void)0)
+#endif
 typedef unsigned char mjtByte;
 
 #define mjPI            3.14159265358979323846

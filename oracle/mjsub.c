@@ -102,8 +102,9 @@ static int rem_pio2(double x, double* y0, double* y1) {
 mjtNum ora_sin(mjtNum x) {
   double y0, y1;
   int n;
-  if (fabs(x) < PIO4) return x == 0 ? x : k_sin(x, 0.0, 0);
-  n = rem_pio2(x, &y0, &y1);
+  ORA_FLOP_TRANS();
+  if (fabs(x) < PIO4) return x == 0 ? x : k_sin((double)x, 0.0, 0);
+  n = rem_pio2((double)x, &y0, &y1);
   switch (n & 3) {
     case 0: return k_sin(y0, y1, 1);
     case 1: return k_cos(y0, y1);
@@ -114,8 +115,9 @@ mjtNum ora_sin(mjtNum x) {
 mjtNum ora_cos(mjtNum x) {
   double y0, y1;
   int n;
-  if (fabs(x) < PIO4) return k_cos(x, 0.0);
-  n = rem_pio2(x, &y0, &y1);
+  ORA_FLOP_TRANS();
+  if (fabs(x) < PIO4) return k_cos((double)x, 0.0);
+  n = rem_pio2((double)x, &y0, &y1);
   switch (n & 3) {
     case 0: return k_cos(y0, y1);
     case 1: return -k_sin(y0, y1, 1);
@@ -876,7 +878,7 @@ static mjtNum get_impedance(const mjtNum* solimp, mjtNum pos, mjtNum margin) {
   if (x <= 0) return dmin;
   {
     /* integer powers by repeated multiplication (power 2 is the MuJoCo default) */
-    int p = (int)power;
+    int p = (int)(double)power;
     mjtNum xp = 1, mp = 1;
     if ((mjtNum)p != power || p < 1 || p > 8) mju_error("solimp power must be an integer in [1,8]");
     if (x <= mid) {

@@ -1,11 +1,14 @@
 /* ORACLE / TEST INFRASTRUCTURE ONLY: flat accessors so tests can drive the
    oracle through ctypes without mirroring struct layouts. */
 #include "ilqr_ora.h"
+#ifdef __cplusplus
+extern "C" {  /* the instrumented C++ build (flops/) keeps C names */
+#endif
 
 void ora_model_info(const mjModel* m, int* out, double* dt) {
   out[0] = m->nq; out[1] = m->nv; out[2] = m->nu; out[3] = m->nbody; out[4] = m->njnt;
   out[5] = m->ngeom; out[6] = m->nconmax; out[7] = m->njmax; out[8] = m->nstack; out[9] = m->nbuffer;
-  *dt = m->opt.timestep;
+  *dt = (double)m->opt.timestep;
 }
 mjtNum* ora_d_field(mjData* d, int which) {
   switch (which) {
@@ -42,5 +45,8 @@ void ora_set_solver(mjModel* m, int iterations, double tolerance) {
 }
 void ora_get_solver(const mjModel* m, int* iterations, double* tolerance) {
   *iterations = m->opt.iterations;
-  *tolerance = m->opt.tolerance;
+  *tolerance = (double)m->opt.tolerance;
 }
+#ifdef __cplusplus
+}
+#endif

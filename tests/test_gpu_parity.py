@@ -345,33 +345,6 @@ def test_fused_sweep_schedules(ia, ora, env, monkeypatch):
     exact(g.deriv(), D, "fd_sweep alone vs iterate's fused records")
 
 
-@pytest.mark.parametrize("G,env", [(1, {}), (2, {}), (3, {"ILQG_ROLL_CUS": "64"}),
-                                   (2, {"ILQG_ROLL_CUS": "32", "ILQG_GROUP_TOKEN": "0"}),
-                                   (5, {"ILQG_GROUP_TOKEN": "0"})])
-def test_seed_groups_identical(ia, G, env, monkeypatch):
-    """ilqg_solver_set_groups: seeds iterated as G groups on their own streams
-    (uneven ranges; with and without CU masks and the sweep token) give exactly the single-stream results, and the solver stream
-    sees every group's selected costs"""
-    import workloads
-    for k, v in env.items():
-        monkeypatch.setenv(k, v)
-    m = ia.Model.load(model_path("hopper"))
-    S, H = 5, 50
-    dmain = workloads.hopper_dmain(m, S, sigma=0.01)
-    out = []
-    for g_ in (None, G):
-        g = ia.ILQR(m, dmain, H, ia.HOPPER_COST, alphas=workloads.LINESEARCH_ALPHAS[:4], select="min_cost")
-        if g_ is not None:
-            g.set_groups(g_)
-            assert g.groups == g_
-        for _ in range(3):
-            g.iterate()
-        g.synchronize()
-        out.append((g.traj().qpos, *g.gains(), g.deriv(), *g.value(), *g.costs()))
-    for a, b, what in zip(out[0], out[1], ("qpos", "K", "k", "deriv", "V", "v", "cost", "sel")):
-        exact(b, a, f"groups={G} {what}")
-
-
 def test_bench_workload_bitexact(ia, ora):
     """The exact timed workload of bench.py (cfg 4's per-GPU share: hopper H=500,
     8 seeds x 8 line-search candidates alpha = 2^-i, select='min_cost'), three
@@ -435,3 +408,69 @@ def test_fault_word_reported_once_then_cleared(ia, ora):
     g.synchronize()
     exact(g.gains()[0][0], il.arrays()["K"], "K after a cleared fault")
     exact(g.traj().qpos, il.traj()["qpos"], "qpos after a cleared fault")
+
+
+# ---- committed known-answer fixtures (tests/golden/make_golden_ilqr.py)
+def _fixture_traj(ia, g, pre):
+    return ia.State(*(g[pre + k] for k in ("time", "qpos", "qvel", "warm", "ctrl")))
+
+
+@pytest.mark.parametrize("fixture", ["riccati_pendulum.npz", "riccati_hopper.npz"])
+def test_riccati_vs_golden(ia, fixture):
+    """initV + Riccati recursion (k_backward, inc/ilqr.h:100-107,144-175) on
+    seeded synthetic FD records and trajectory == the committed fixture"""
+    g = load_golden(fixture)
+    m = ia.Model.load(model_path(str(g["model"])))
+    P = g["deriv"].shape[0]
+    tr = _fixture_traj(ia, g, "traj_")
+    s = ia.ILQR(m, ia.State(tr.time[:1], tr.qpos[:1], tr.qvel[:1], tr.warm[:1], tr.ctrl[:1]), P - 1,
+                ia.HOPPER_COST if str(g["model"]) == "hopper" else ia.PENDULUM_COST)
+    s.set_traj(tr)
+    s.set_deriv(g["deriv"][None])
+    s.riccati_pass()
+    s.synchronize()
+    K, k = s.gains()
+    V, v = s.value()
+    exact(K[0, 1:], g["K"][1:], "K")
+    exact(k[0, 1:], g["k"][1:], "k")
+    exact(V[0], g["V"], "V")
+    exact(v[0], g["v"], "v")
+
+
+@pytest.mark.parametrize("fixture", ["iterate_pendulum_H20.npz", "iterate_pendulum_H100.npz"])
+def test_iterate_vs_golden(ia, fixture):
+    """ILQR::iterate() from the reference's initial state == the fixture written
+    with the reference's own calcMJDerivatives (oracle/_ref)"""
+    g = load_golden(fixture)
+    m = ia.Model.load(model_path("inverted_pendulum"))
+    s = ia.ILQR(m, _fixture_traj(ia, g, "dmain_"), int(g["horizon"]), ia.PENDULUM_COST)
+    for _ in range(int(g["iters"])):
+        s.iterate()
+    s.synchronize()
+    t = s.traj()
+    for k in ("time", "qpos", "qvel", "warm", "ctrl"):
+        exact(getattr(t, k).reshape(g["traj_" + k].shape), g["traj_" + k], "traj " + k)
+    K, k = s.gains()
+    V, v = s.value()
+    exact(K[0], g["K"], "K")
+    exact(k[0], g["k"], "k")
+    exact(V[0], g["V"], "V")
+    exact(v[0], g["v"], "v")
+    exact(s.deriv()[0], g["deriv"], "deriv")
+
+
+def test_fixed_gain_rollout_vs_golden(ia):
+    """forwardPass with fixed seeded gains (inc/ilqr.h:116-130), hopper H=100
+    from the cfg-3 state (contacts) == the committed fixture"""
+    g = load_golden("rollout_hopper_H100.npz")
+    m = ia.Model.load(model_path("hopper"))
+    s = ia.ILQR(m, _fixture_traj(ia, g, "dmain_"), int(g["horizon"]), ia.HOPPER_COST)
+    t = s.traj()
+    for k in ("time", "qpos", "qvel", "warm", "ctrl"):
+        exact(getattr(t, k).reshape(g["nominal_" + k].shape), g["nominal_" + k], "nominal " + k)
+    s.set_gains(g["K"][None], g["k"][None])
+    s.forward_pass()
+    s.synchronize()
+    t = s.traj()
+    for k in ("time", "qpos", "qvel", "warm", "ctrl"):
+        exact(getattr(t, k).reshape(g["traj_" + k].shape), g["traj_" + k], "traj " + k)
