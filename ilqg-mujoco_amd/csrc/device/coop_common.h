@@ -78,6 +78,19 @@ __device__ inline void stage_model_s(const DevModel& g, const auto& L, const aut
   TSYNC();
 }
 
+// model-specific variant with the image in a __shared__ object of its own
+// (not the workspace array): loads of model data provably do not alias the
+// workspace stores, so the compiler may hoist and overlap them
+template <class SM>
+__device__ inline void stage_model_sep(const DevModel& g, const Team& T, SM& m) {
+  constexpr int ND = (SM::img_bytes + 7) / 8;
+  __shared__ double img[ND];
+  const double* src = reinterpret_cast<const double*>(g.img);
+  FOR_T(w, ND) img[w] = src[w];
+  m.bind(reinterpret_cast<const unsigned char*>(img), g);
+  TSYNC();
+}
+
 __device__ inline double cost_terms(double c, const double* x, const double* w, const double* t, const double* l,
                                     int n) {
   for (int i = 0; i < n; i++) {

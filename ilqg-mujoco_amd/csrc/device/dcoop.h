@@ -868,27 +868,13 @@ __device__ inline void collision(const auto& m, const auto& L, const auto& C, co
   TSYNC();
 }
 
-__device__ inline void make_constraint(const auto& m, const auto& L, const auto& C, const auto& X,
-                                       const Team& T) {
-  const int nv = m.nv;
+// make_constraint, in pieces the two-wave rollout schedules separately
+// (step_dual_split); make_constraint() runs them in the oracle's order.
+
+// which limit sides are violated (bit 0 lower, bit 1 upper): qpos only
+__device__ inline void mc_limit_masks(const auto& m, const auto& L, const auto& C, const Team& T) {
   double* qpos = T.w + L.qpos;
-  double* con = T.w + L.con;
-  double* efcJ = T.w + L.efc_J;
-  double* efc_pos = T.w + L.efc_pos;
-  double* efc_margin = T.w + L.efc_margin;
-  double* efc_D = T.w + L.efc_D;
-  double* KBIP = T.w + L.efc_KBIP;
-  int* coni = T.iw + L.coni;
-  int* efc_type = T.iw + L.efc_type;
-  int* efc_id = T.iw + L.efc_id;
-  int* rsub = T.ci + C.rsub;
   int* jcnt = T.ci + C.jcnt;
-  double* jc = T.w + L.jc;
-  double* scom = T.w + L.scom;
-  double* cdof = T.w + L.cdof;
-  const int ncon = T.iw[L.ncon];
-  const int njmax = m.njmax < m.maxefc ? m.njmax : m.maxefc;
-  // which limit sides are violated: bit 0 lower, bit 1 upper
   FOR_T(j, m.njnt) {
     int type = m.jnt_type[j], mask = 0;
     if (m.jnt_limited[j] && (type == JNT_SLIDE || type == JNT_HINGE)) {
@@ -900,7 +886,17 @@ __device__ inline void make_constraint(const auto& m, const auto& L, const auto&
     }
     jcnt[j] = mask;
   }
-  // contact jacobians in the contact frame: one lane per (contact, dof)
+}
+
+// contact jacobians in the contact frame: one lane per (contact, dof)
+__device__ inline void mc_contact_jac(const auto& m, const auto& L, const auto& X, const Team& T) {
+  const int nv = m.nv;
+  double* con = T.w + L.con;
+  int* coni = T.iw + L.coni;
+  double* jc = T.w + L.jc;
+  double* scom = T.w + L.scom;
+  double* cdof = T.w + L.cdof;
+  const int ncon = T.iw[L.ncon];
   FOR_T(e, ncon * nv) {
     int c = e / nv, k = e % nv;
     const double* cc = con + CON_ND * c;
@@ -913,10 +909,20 @@ __device__ inline void make_constraint(const auto& m, const auto& L, const auto&
       jc[(c * 3 + r) * nv + k] = cc[CON_FRAME + 3 * r] * b[0] + cc[CON_FRAME + 3 * r + 1] * b[1] +
                                  cc[CON_FRAME + 3 * r + 2] * b[2];
   }
-  TSYNC();
-  // row allocation in the oracle's order (limits, then contacts).  When every
-  // row fits (no njmax truncation) the offsets are prefix counts over ballots,
-  // one lane per joint / contact; otherwise the oracle's loop on lane 0.
+}
+
+// row allocation in the oracle's order (limits, then contacts).  When every
+// row fits (no njmax truncation) the offsets are prefix counts over ballots,
+// one lane per joint / contact; otherwise the oracle's loop on lane 0.
+// Returns whether the parallel branch ran (wave-uniform).
+__device__ inline bool mc_alloc(const auto& m, const auto& L, const auto& C, const Team& T) {
+  int* coni = T.iw + L.coni;
+  int* efc_type = T.iw + L.efc_type;
+  int* efc_id = T.iw + L.efc_id;
+  int* rsub = T.ci + C.rsub;
+  int* jcnt = T.ci + C.jcnt;
+  const int ncon = T.iw[L.ncon];
+  const int njmax = m.njmax < m.maxefc ? m.njmax : m.maxefc;
   bool par = m.njnt <= TEAM_SIZE && ncon <= TEAM_SIZE;
   if (par) {
     const int t = T.tid;
@@ -983,9 +989,26 @@ __device__ inline void make_constraint(const auto& m, const auto& L, const auto&
     }
     T.iw[L.nefc] = nefc;
   }
-  TSYNC();
-  const int nefc = T.iw[L.nefc];
-  FOR_T(e, nefc * nv) {
+  return par;
+}
+
+// jacobian rows and row parameters (impedance, K/B, D) of rows [r0, r1)
+__device__ inline void mc_rows(const auto& m, const auto& L, const auto& C, const Team& T, int r0, int r1) {
+  const int nv = m.nv;
+  double* qpos = T.w + L.qpos;
+  double* con = T.w + L.con;
+  double* efcJ = T.w + L.efc_J;
+  double* efc_pos = T.w + L.efc_pos;
+  double* efc_margin = T.w + L.efc_margin;
+  double* efc_D = T.w + L.efc_D;
+  double* KBIP = T.w + L.efc_KBIP;
+  int* coni = T.iw + L.coni;
+  int* efc_type = T.iw + L.efc_type;
+  int* efc_id = T.iw + L.efc_id;
+  int* rsub = T.ci + C.rsub;
+  double* jc = T.w + L.jc;
+  FOR_T(e0, (r1 - r0) * nv) {
+    const int e = e0 + r0 * nv;
     int i = e / nv, k = e % nv;
     int type = efc_type[i], id = efc_id[i], sub = rsub[i];
     double v;
@@ -1001,7 +1024,8 @@ __device__ inline void make_constraint(const auto& m, const auto& L, const auto&
     }
     efcJ[i * nv + k] = v;
   }
-  FOR_T(i, nefc) {
+  FOR_T(i0, r1 - r0) {
+    const int i = i0 + r0;
     int type = efc_type[i], id = efc_id[i];
     double solref[2], solimp[5], dA, imp, tc, dr, dmax, K, B, pos, mar;
     if (type == C_LIMIT) {
@@ -1048,7 +1072,52 @@ __device__ inline void make_constraint(const auto& m, const auto& L, const auto&
     double R = maxd(MINVAL, (1 - imp) * dA / imp);
     efc_D[i] = 1 / R;
   }
+}
+
+__device__ inline void make_constraint(const auto& m, const auto& L, const auto& C, const auto& X,
+                                       const Team& T) {
+  mc_limit_masks(m, L, C, T);
+  mc_contact_jac(m, L, X, T);
   TSYNC();
+  (void)mc_alloc(m, L, C, T);
+  TSYNC();
+  mc_rows(m, L, C, T, 0, T.iw[L.nefc]);
+  TSYNC();
+}
+
+// The limit rows -- the first rows of the constraint arrays -- from qpos alone,
+// ahead of make_constraint (two-wave rollout, beside the kinematics): masks,
+// allocation and rows [0, nlim) exactly as make_constraint computes them.
+// Returns nlim (-1 when the limits alone exceed njmax: make_constraint then
+// takes its serial branch and computes every row).
+__device__ inline int limit_rows_pre(const auto& m, const auto& L, const auto& C, const Team& T) {
+  mc_limit_masks(m, L, C, T);
+  TSYNC();
+  if (m.njnt > TEAM_SIZE) return -1;
+  const int njmax = m.njmax < m.maxefc ? m.njmax : m.maxefc;
+  int* efc_type = T.iw + L.efc_type;
+  int* efc_id = T.iw + L.efc_id;
+  int* rsub = T.ci + C.rsub;
+  const int t = T.tid;
+  const int jm = t < m.njnt ? T.ci[C.jcnt + t] : 0;
+  const unsigned long long blo = __ballot(jm & 1), bhi = __ballot(jm & 2);
+  const int nlim = __popcll(blo) + __popcll(bhi);
+  if (nlim > njmax) return -1;
+  if (t < m.njnt && jm) {
+    const unsigned long long below = (1ull << t) - 1;
+    int r = __popcll(blo & below) + __popcll(bhi & below);
+    for (int side = -1; side <= 1; side += 2) {
+      if (!(jm & (side < 0 ? 1 : 2))) continue;
+      efc_type[r] = C_LIMIT;
+      efc_id[r] = t;
+      rsub[r] = side;
+      r++;
+    }
+  }
+  TSYNC();
+  mc_rows(m, L, C, T, 0, nlim);
+  TSYNC();
+  return nlim;
 }
 
 // transmission: actuator_moment (joint transmissions)
@@ -1081,6 +1150,66 @@ __device__ inline void fwd_position(const auto& m, const auto& L, const auto& C,
 // ------------------------------------------------------ velocity stage ---
 // part 0: the whole stage; 1: com velocities + RNE (primary wave of a
 // two-wave step); 2: passive forces + constraint reference (helper wave)
+// passive forces: one lane per dof (hinge/slide springs; ball/free rejected on the host)
+__device__ inline void passive_forces(const auto& m, const auto& L, const Team& T) {
+  double* qvel = T.w + L.qvel;
+  double* qpos = T.w + L.qpos;
+  double* qp = T.w + L.qfrc_passive;
+  FOR_T(i, m.nv) {
+    int j = m.dof_jntid[i];
+    double v = 0;
+    double k = m.jnt_stiffness[j];
+    if (k != 0) {
+      int pa = m.jnt_qposadr[j];
+      v = -k * (qpos[pa] - m.qpos_spring[pa]);
+    }
+    v -= m.dof_damping[i] * qvel[i];
+    qp[i] = v;
+  }
+}
+
+// constraint velocities and reference accelerations: one lane per row
+__device__ inline void constraint_ref(const auto& m, const auto& L, const Team& T) {
+  const int nv = m.nv;
+  double* qvel = T.w + L.qvel;
+  const int nefc = T.iw[L.nefc];
+  double* KBIP = T.w + L.efc_KBIP;
+  double* efc_vel = T.w + L.efc_vel;
+  double* aref = T.w + L.efc_aref;
+  double* J = T.w + L.efc_J;
+  double* pos = T.w + L.efc_pos;
+  double* mar = T.w + L.efc_margin;
+  FOR_T(i, nefc) {
+    double k0 = KBIP[L.kstr * i], k1 = KBIP[L.kstr * i + 1], k2 = KBIP[L.kstr * i + 2];
+    double v = tdot(J + i * nv, qvel, nv);
+    efc_vel[i] = v;
+    aref[i] = -k1 * v - k0 * k2 * (pos[i] - mar[i]);
+  }
+}
+
+// actuator forces and qfrc_actuator = moment' * force (the first part of the
+// acceleration stage; ctrl and the joint transmissions only)
+__device__ inline void actuator_force(const auto& m, const auto& L, const Team& T) {
+  const int nv = m.nv, nu = m.nu;
+  double* ctrl = T.w + L.ctrl;
+  double* af = T.w + L.afrc;
+  double* amom = T.w + L.amom;
+  double* qa = T.w + L.qfrc_act;
+  FOR_T(i, nu) {
+    double c = ctrl[i], f;
+    if (m.actuator_ctrllimited[i]) c = clipd(c, m.actuator_ctrlrange[2 * i], m.actuator_ctrlrange[2 * i + 1]);
+    f = m.actuator_gainprm[i] * c;
+    if (m.actuator_forcelimited[i]) f = clipd(f, m.actuator_forcerange[2 * i], m.actuator_forcerange[2 * i + 1]);
+    af[i] = f;
+  }
+  TSYNC();
+  FOR_T(j, nv) {
+    double s = 0;
+    for (int i = 0; i < nu; i++) s += amom[i * nv + j] * af[i];
+    qa[j] = s;
+  }
+}
+
 __device__ inline void fwd_velocity(const auto& m, const auto& L, const auto& C, const Team& T, int part = 0) {
   const int nv = m.nv, nb = m.nbody;
   double* cvelw = T.w + L.cvel;
@@ -1142,33 +1271,8 @@ __device__ inline void fwd_velocity(const auto& m, const auto& L, const auto& C,
   }
   }
   if (part != 1) {
-  // passive forces: one lane per dof (hinge/slide springs; ball/free rejected on the host)
-  double* qp = T.w + L.qfrc_passive;
-  FOR_T(i, nv) {
-    int j = m.dof_jntid[i];
-    double v = 0;
-    double k = m.jnt_stiffness[j];
-    if (k != 0) {
-      int pa = m.jnt_qposadr[j];
-      v = -k * (qpos[pa] - m.qpos_spring[pa]);
-    }
-    v -= m.dof_damping[i] * qvel[i];
-    qp[i] = v;
-  }
-  // constraint velocities and reference accelerations: one lane per row
-  const int nefc = T.iw[L.nefc];
-  double* KBIP = T.w + L.efc_KBIP;
-  double* efc_vel = T.w + L.efc_vel;
-  double* aref = T.w + L.efc_aref;
-  double* J = T.w + L.efc_J;
-  double* pos = T.w + L.efc_pos;
-  double* mar = T.w + L.efc_margin;
-  FOR_T(i, nefc) {
-    double k0 = KBIP[L.kstr * i], k1 = KBIP[L.kstr * i + 1], k2 = KBIP[L.kstr * i + 2];
-    double v = tdot(J + i * nv, qvel, nv);
-    efc_vel[i] = v;
-    aref[i] = -k1 * v - k0 * k2 * (pos[i] - mar[i]);
-  }
+    passive_forces(m, L, T);
+    constraint_ref(m, L, T);
   }
   TSYNC();
   if (part == 2) return;
@@ -1220,20 +1324,24 @@ __device__ inline void fwd_velocity(const auto& m, const auto& L, const auto& C,
 }
 
 // -------------------------------------------------- acceleration stage ---
-__device__ inline void fwd_acceleration(const auto& m, const auto& L, const auto& X, const Team& T) {
+// act_pre: actuator_force() already ran (two-wave rollout: on the helper wave)
+__device__ inline void fwd_acceleration(const auto& m, const auto& L, const auto& X, const Team& T,
+                                        bool act_pre = false) {
   const int nv = m.nv, nu = m.nu;
   double* ctrl = T.w + L.ctrl;
   double* af = T.w + L.afrc;
   double* amom = T.w + L.amom;
   double* qa = T.w + L.qfrc_act;
-  FOR_T(i, nu) {
-    double c = ctrl[i], f;
-    if (m.actuator_ctrllimited[i]) c = clipd(c, m.actuator_ctrlrange[2 * i], m.actuator_ctrlrange[2 * i + 1]);
-    f = m.actuator_gainprm[i] * c;
-    if (m.actuator_forcelimited[i]) f = clipd(f, m.actuator_forcerange[2 * i], m.actuator_forcerange[2 * i + 1]);
-    af[i] = f;
+  if (!act_pre) {
+    FOR_T(i, nu) {
+      double c = ctrl[i], f;
+      if (m.actuator_ctrllimited[i]) c = clipd(c, m.actuator_ctrlrange[2 * i], m.actuator_ctrlrange[2 * i + 1]);
+      f = m.actuator_gainprm[i] * c;
+      if (m.actuator_forcelimited[i]) f = clipd(f, m.actuator_forcerange[2 * i], m.actuator_forcerange[2 * i + 1]);
+      af[i] = f;
+    }
+    TSYNC();
   }
-  TSYNC();
   double* sm = T.w + L.qfrc_smooth;
   double* qp = T.w + L.qfrc_passive;
   double* qb = T.w + L.qfrc_bias;
@@ -1249,9 +1357,14 @@ __device__ inline void fwd_acceleration(const auto& m, const auto& L, const auto
   for (int i0 = 6; i0 < 6 * m.nbody; i0 += TEAM_SIZE) fmask |= __ballot(i0 + T.tid < 6 * m.nbody && xf[i0 + T.tid] != 0);
   const bool anyf = fmask != 0ull;
   FOR_T(j, nv) {
-    double s = 0;
-    for (int i = 0; i < nu; i++) s += amom[i * nv + j] * af[i];
-    qa[j] = s;
+    double s;
+    if (act_pre) {
+      s = qa[j];
+    } else {
+      s = 0;
+      for (int i = 0; i < nu; i++) s += amom[i * nv + j] * af[i];
+      qa[j] = s;
+    }
     double v = qp[j] - qb[j];
     v += qap[j];
     v += s;
@@ -2044,6 +2157,160 @@ __device__ inline void step(const auto& m, const auto& L, const auto& C, const a
   else
     euler(m, L, C, X, T);
   STAMP(9);
+}
+
+// the L'DL factor of M and, for Euler with damping, the factor of M + h D
+// (euler_prefactor's matrix) in one pass of the register-row factorization:
+// lanes 0..31 factor M, lanes 32..63 factor M + h D.  Same numbers as
+// factor_ld() followed by euler_prefactor().
+__device__ inline void factor_m_and_euler(const auto& m, const auto& L, const auto& C, const auto& X,
+                                          const Team& T, bool eul) {
+  const int nv = m.nv;
+  double* qM = T.w + L.qM;
+  if (!(eul && euler_damped(m, T))) {
+    factor_ld(m, X, T, qM, T.w + L.qLD, T.w + L.qLDinv, T.c + C.ftmp);
+    return;
+  }
+  if (!(nv <= RMAX && X.pmask)) {
+    factor_ld(m, X, T, qM, T.w + L.qLD, T.w + L.qLDinv, T.c + C.ftmp);
+    euler_prefactor(m, L, C, X, T);
+    return;
+  }
+  double* s = T.w + L.s_euler;
+  double *qH = s + nv, *qHLD = s + nv + nv * nv, *qHinv = s + nv + 2 * nv * nv;
+  FOR_T(e, nv * nv) {
+    int i = e / nv, j = e % nv;
+    double v = qM[e];
+    if (i == j) v += m.opt_timestep * m.dof_damping[i];
+    qH[e] = v;
+  }
+  TSYNC();
+  factor_ld_rows2(nv, X.pmask, T.tid, qM, T.w + L.qLD, T.w + L.qLDinv, qH, qHLD, qHinv);
+}
+
+// step_dual for the split layout (L.split: RNE / com-velocity scratch outside
+// the union) and register-row models.  Work moves to where the helper wave
+// has slack, without changing any value:
+//   phase 1 (beside the kinematics): control law + record, the limit rows of
+//     make_constraint (qpos only), passive forces, transmission and actuator
+//     forces (ctrl only);
+//   phase 3 (beside crb): contact jacobians and row allocation;
+//   phase 4 (beside com velocities + RNE): the contact rows' jacobians and
+//     parameters, constraint reference accelerations, and the factors of M
+//     and of M + h D in one register-row pass;
+//   phase 5 (beside the acceleration stage): the warm-start half of the
+//     Newton start.
+__device__ inline void step_dual_split(const auto& m, const auto& L, const auto& C, const auto& X, const Team& T,
+                                       int wave, auto&& pre) {
+  const bool A = wave == 0;
+  const bool eul = m.opt_integrator != 1;
+  STAMP(-1);
+  STAMPB(-1);
+  const bool bad = any_bad(T, C, T.w + L.qpos, m.nq) || any_bad(T, C, T.w + L.qvel, m.nv);
+  if (bad) {
+    if (!A) pre();
+    __syncthreads();
+    if (A) reset_data(m, L, T);
+    __syncthreads();  // the helper's phase-1 work reads the reset state
+  }
+  int nlim = 0;
+  if (A) {
+    kinematics(m, L, C, T);
+    STAMP(0);
+  } else {
+    if (!bad) pre();
+    STAMPB(41);
+    nlim = limit_rows_pre(m, L, C, T);
+    passive_forces(m, L, T);
+    transmission(m, L, T);
+    TSYNC();
+    actuator_force(m, L, T);
+    STAMPB(42);
+  }
+  __syncthreads();
+  STAMP(24);
+  STAMPB(32);
+  if (A) {
+    com_pos(m, L, T);
+    STAMP(1);
+  } else {
+    collision(m, L, C, X, T);
+    STAMPB(33);
+  }
+  __syncthreads();
+  STAMP(25);
+  STAMPB(34);
+  bool rows_done = false;
+  if (A) {
+    crb(m, L, C, X, T);
+    STAMP(2);
+  } else {
+    mc_contact_jac(m, L, X, T);
+    TSYNC();
+    const bool par = mc_alloc(m, L, C, T);
+    TSYNC();
+    if (!par || nlim < 0) {
+      // the serial allocation (njmax truncation): every row here, as make_constraint
+      mc_rows(m, L, C, T, 0, T.iw[L.nefc]);
+      TSYNC();
+      rows_done = true;
+    }
+    STAMPB(35);
+  }
+  __syncthreads();
+  STAMP(26);
+  STAMPB(36);
+  if (A) {
+    fwd_velocity(m, L, C, T, 1);
+    STAMP(6);
+  } else {
+    if (!rows_done) {
+      mc_rows(m, L, C, T, nlim, T.iw[L.nefc]);
+      TSYNC();
+    }
+    constraint_ref(m, L, T);
+    TSYNC();
+    STAMPB(37);
+    factor_m_and_euler(m, L, C, X, T, eul);
+    STAMPB(38);
+  }
+  __syncthreads();
+  STAMP(27);
+  STAMPB(39);
+  const int ne5 = T.iw[L.nefc];
+  const bool spec = ne5 > 0 && ne5 <= TEAM_SIZE && m.nv <= RMAX;
+  if (A) {
+    fwd_acceleration(m, L, X, T, true);
+    STAMP(7);
+    if (spec) {
+      fwd_constraint_fast(m, L, C, X, T, m.opt_iterations, m.opt_tolerance, true);
+    } else {
+      __syncthreads();
+      fwd_constraint(m, L, C, X, T, m.opt_iterations, m.opt_tolerance);
+    }
+    STAMP(8);
+  } else {
+    if (spec) newton_warm_prep(m, L, C, T);
+    STAMPB(30);
+    __syncthreads();
+  }
+  __syncthreads();
+  STAMP(29);
+  STAMPB(43);
+  if (A) {
+    bool reset = false;
+    if (any_bad(T, C, T.w + L.qacc, m.nv)) {
+      reset = true;
+      reset_data(m, L, T);
+      forward_skip(m, L, C, X, T, STAGE_NONE, m.opt_iterations, m.opt_tolerance);
+    }
+    if (!eul) rk4(m, L, C, X, T, m.opt_iterations, m.opt_tolerance);
+    else euler_finish(m, L, C, X, T, !reset);
+    STAMP(9);
+  }
+  __syncthreads();
+  STAMP(28);
+  STAMPB(40);
 }
 
 // mj_step by a two-wave team (rollout kernels): wave 0 runs the dependency

@@ -52,6 +52,7 @@ struct WsLayout {
   int s_rne, s_con, s_newton, s_euler, s_rk4, s_fd;
   int pcon, jc;  // cooperative layout only: per-pair contacts, contact-frame jacobians
   int kstr;      // stride of efc_KBIP rows (4 lane layout, 3 cooperative)
+  int split;     // two-wave rollout layout: RNE / com-velocity scratch outside the union
   int nd;
   int coni, efc_type, efc_id, efc_state, ncon, nefc;
   int ni;
@@ -62,8 +63,11 @@ struct WsLayout {
 // make_constraint (contacts, per-pair candidates, contact-frame jacobians)
 // shares storage with scratch first written afterwards (RNE, com velocities,
 // Newton, Euler, efc_b/efc_vel): less LDS per team, more teams per CU.
+// split (rollout kernels): the RNE and com-velocity scratch live outside the
+// union, so the helper wave may still read contacts and contact-frame
+// jacobians while the primary runs the velocity stage (step_dual)
 template <class M>
-constexpr WsLayout make_layout(const M& m, int npair = -1) {
+constexpr WsLayout make_layout(const M& m, int npair = -1, bool split = false) {
   WsLayout L{};
   int o = 0;
   const int nq = m.nq, nv = m.nv, nu = m.nu, nb = m.nbody, nj = m.njnt, ng = m.ngeom;
@@ -98,6 +102,11 @@ constexpr WsLayout make_layout(const M& m, int npair = -1) {
   }
   L.s_rk4 = take(2 * nv + 4 * (nq + nv) + 4 * nv);
   L.s_fd = take(2 * nv);
+  if (coop && split) {
+    L.split = 1;
+    L.s_rne = take(12 * nb);
+    L.s_con = take(10 * nv);
+  }
   if (coop) {
     const int u = o;
     int a = u;  // position-stage view
@@ -108,8 +117,10 @@ constexpr WsLayout make_layout(const M& m, int npair = -1) {
     L.jc = a;
     a += 14 * (npair > 0 ? npair : 1) > 3 * nv * nc ? 14 * (npair > 0 ? npair : 1) : 3 * nv * nc;
     int b = u;  // velocity / constraint / integration view
-    L.s_rne = b; b += 12 * nb;
-    L.s_con = b; b += 10 * nv;
+    if (!split) {
+      L.s_rne = b; b += 12 * nb;
+      L.s_con = b; b += 10 * nv;
+    }
     L.s_newton = b; b += 4 * nv + nv * nv + 2 * ne;
     L.s_euler = b; b += 2 * nv + 2 * nv * nv;
     L.efc_b = b; b += ne;

@@ -121,6 +121,72 @@ __device__ inline void factor_ld_rows(int nv, const auto& pmask, int tid, const 
   team_sync();
 }
 
+// Two tree L'DL factorizations with the same sparsity at once: lanes 0..31
+// factor mat0 (row t on lane t), lanes 32..63 factor mat1 (row t on lane
+// 32 + t); every broadcast reads the lane of the caller's own half.  Each
+// factor receives exactly the operations of factor_ld_rows.  The matrices and
+// factors are addressed as offsets from mat0 / LD0 / dinv0 (no pointer
+// selects).  nv <= RMAX <= 32.
+__device__ inline void factor_ld_rows2(int nv, const auto& pmask, int tid, const double* mat0, double* LD0,
+                                       double* diaginv0, const double* mat1, double* LD1, double* diaginv1) {
+  const bool hi = tid >= 32;
+  const int t = tid & 31;
+  const int om = hi ? (int)(mat1 - mat0) : 0, ol = hi ? (int)(LD1 - LD0) : 0,
+            od = hi ? (int)(diaginv1 - diaginv0) : 0;
+  const double* mat = mat0 + om;
+  double* LD = LD0 + ol;
+  double* diaginv = diaginv0 + od;
+  auto bc = [&](double x, int k) __attribute__((always_inline)) {
+    const double a = bcast(x, k), b = bcast(x, 32 + k);
+    return hi ? b : a;
+  };
+  double r[RMAX];
+  unsigned long long pm[RMAX];
+  const bool own = t < nv;
+  sfor<0, RMAX>(SLAM(jj) {
+    constexpr int j = SK(jj);
+    r[j] = (own && j < nv && j <= t) ? mat[t * nv + j] : 0.0;
+    pm[j] = j < nv ? pmask[j] : 0ull;
+  });
+  const unsigned long long self = own ? (pmask[t] | (1ull << t)) : 0ull;
+  team_sync();
+  sfor<0, RMAX>(SLAM(kk) {
+    constexpr int k = RMAX - 1 - SK(kk);
+    if (k >= nv) return;
+    const unsigned long long ak = pm[k];
+    double dk = bc(r[k], k);
+    if (dk < MINVAL) dk = MINVAL;
+    double rk[RMAX];
+    sfor<0, RMAX>(SLAM(jj) {
+      constexpr int j = SK(jj);
+      rk[j] = (j <= k) ? bc(r[j], k) : 0.0;
+    });
+    double tmp = 0;
+    if (own && ((ak >> t) & 1)) {
+      tmp = rsel(rk, t) / dk;
+      sfor<0, k>(SLAM(jj) {
+        constexpr int j = SK(jj);
+        if ((self >> j) & 1) r[j] -= tmp * rk[j];
+      });
+    }
+    sfor<0, k>(SLAM(ii) {
+      constexpr int i = SK(ii);
+      if ((ak >> i) & 1) {
+        const double ti = bc(tmp, i);
+        if (t == k) r[i] = ti;
+      }
+    });
+    if (t == k) r[k] = dk;
+  });
+  if (own) {
+    sfor<0, RMAX>(SLAM(jj) {
+      if (SK(jj) < nv) LD[t * nv + SK(jj)] = r[SK(jj)];
+    });
+    diaginv[t] = 1 / rsel(r, t);
+  }
+  team_sync();
+}
+
 // x <- (L'DL)^-1 x for the factor above; mirrors coop::solve_ld.
 __device__ inline void solve_ld_rows(int nv, const auto& pmask, int tid, const double* LD,
                                      const double* diaginv, double* x) {

@@ -6,7 +6,7 @@ namespace ilqg {
 namespace {
 
 __device__ inline void rollout_body(const auto& m, const auto& L, const auto& C, const auto& X, const Team& T,
-                                int S, int A, int P, TrajDev nom, TrajDev out, int out_is_cand, const double* K, const double* k, const double* alphas, TrajDev dinit, const double* qfrc_applied, const double* xfrc_applied, int passive, CostDev cost, double* cost_cand, int wave) {
+                                int S, int A, int P, TrajDev nom, TrajDev out, int out_is_cand, const double* K, const double* k, const double* alphas, TrajDev dinit, const double* qfrc_applied, const double* xfrc_applied, int passive, CostDev cost, double* cost_cand, int wave, auto split) {
   // wave < 0: one-wave team; 0/1: primary/helper wave of a two-wave team (step_dual)
   const bool prim = wave <= 0;
   STAMP_INIT();
@@ -107,10 +107,13 @@ __device__ inline void rollout_body(const auto& m, const auto& L, const auto& C,
       step(m, L, C, X, T);
       park(n);
     } else {
-      step_dual(m, L, C, X, T, wave, [&]() {
+      auto pre = [&]() {
         pre_step(n);
         park(n);
-      });
+      };
+      // split layout (compile-time models): the rebalanced two-wave schedule
+      if constexpr (decltype(split)::value) step_dual_split(m, L, C, X, T, wave, pre);
+      else step_dual(m, L, C, X, T, wave, pre);
     }
   }
   if (ctl && T.tid == 0 && cost_cand) cost_cand[lane] = c;
@@ -128,7 +131,7 @@ __global__ __launch_bounds__(TEAM) void k_rollout_coop(DevModel mg, WsLayout L, 
   DevModel m;
   CoopAux X;
   stage_model(mg, Xg, L, C, T, m, X);
-  rollout_body(m, L, C, X, T, S, A, P, nom, out, out_is_cand, K, k, alphas, dinit, qfrc_applied, xfrc_applied, passive, cost, cost_cand, -1);
+  rollout_body(m, L, C, X, T, S, A, P, nom, out, out_is_cand, K, k, alphas, dinit, qfrc_applied, xfrc_applied, passive, cost, cost_cand, -1, std::false_type{});
 }
 
 // model-specific instance (static_models.h): compile-time sizes, tables and LDS layout
@@ -139,8 +142,8 @@ __global__ __launch_bounds__(TEAM) void k_rollout_s(DevModel mg, int S, int A, i
   static constexpr SX X{};
   Team T = make_team(L, C);
   SM m;
-  stage_model_s(mg, L, C, T, m);
-  rollout_body(m, L, C, X, T, S, A, P, nom, out, out_is_cand, K, k, alphas, dinit, qfrc_applied, xfrc_applied, passive, cost, cost_cand, -1);
+  stage_model_sep(mg, T, m);
+  rollout_body(m, L, C, X, T, S, A, P, nom, out, out_is_cand, K, k, alphas, dinit, qfrc_applied, xfrc_applied, passive, cost, cost_cand, -1, std::false_type{});
 }
 
 // two-wave teams (step_dual): 128 threads per (seed, candidate)
@@ -150,18 +153,18 @@ __global__ __launch_bounds__(2 * TEAM) void k_rollout2_coop(DevModel mg, WsLayou
   CoopAux X;
   stage_model(mg, Xg, L, C, T, m, X);
   rollout_body(m, L, C, X, T, S, A, P, nom, out, out_is_cand, K, k, alphas, dinit, qfrc_applied, xfrc_applied,
-               passive, cost, cost_cand, (int)(threadIdx.x / TEAM));
+               passive, cost, cost_cand, (int)(threadIdx.x / TEAM), std::false_type{});
 }
 template <class SM, class SX>
 __global__ __launch_bounds__(2 * TEAM) void k_rollout2_s(DevModel mg, int S, int A, int P, TrajDev nom, TrajDev out, int out_is_cand, const double* K, const double* k, const double* alphas, TrajDev dinit, const double* qfrc_applied, const double* xfrc_applied, int passive, CostDev cost, double* cost_cand) {
-  static constexpr WsLayout L = make_layout(SM{}, SX::npair);
+  static constexpr WsLayout L = make_layout(SM{}, SX::npair, true);
   static constexpr CoopLayout C = make_coop_layout(SM{}, SX::npair);
   static constexpr SX X{};
   Team T = make_team(L, C);
   SM m;
-  stage_model_s(mg, L, C, T, m);
+  stage_model_sep(mg, T, m);
   rollout_body(m, L, C, X, T, S, A, P, nom, out, out_is_cand, K, k, alphas, dinit, qfrc_applied, xfrc_applied,
-               passive, cost, cost_cand, (int)(threadIdx.x / TEAM));
+               passive, cost, cost_cand, (int)(threadIdx.x / TEAM), std::bool_constant<SM::nv <= RMAX>{});
 }
 
 }  // namespace
@@ -194,13 +197,15 @@ hipError_t launch_rollout_coop(const DevModel& m, const WsLayout& L, const CoopL
   hipError_t e;
   if (use_dual()) {
 #define ILQG_CASE(id, SMT, SXT)                                                                                 \
-  case id:                                                                                                      \
-    e = allow_lds(k_rollout2_s<stat::SMT, stat::SXT>, lds);                                                     \
+  case id: {                                                                                                    \
+    const size_t lds2 = rollout_lds(coop_lds_bytes(make_layout(stat::SMT{}, stat::SXT::npair, true), C));       \
+    e = allow_lds(k_rollout2_s<stat::SMT, stat::SXT>, lds2);                                                    \
     if (e != hipSuccess) return e;                                                                              \
-    hipLaunchKernelGGL((k_rollout2_s<stat::SMT, stat::SXT>), dim3(S * A), dim3(2 * TEAM), lds, st, m, S, A, P,   \
+    hipLaunchKernelGGL((k_rollout2_s<stat::SMT, stat::SXT>), dim3(S * A), dim3(2 * TEAM), lds2, st, m, S, A, P,  \
                        nominal, out, out_is_cand, K, k, alphas, dinit, qfrc_applied, xfrc_applied, passive, cost, \
                        cost_cand);                                                                              \
-    return hipGetLastError();
+    return hipGetLastError();                                                                                   \
+  }
     switch (m.static_id) {
       ILQG_STATIC_MODELS(ILQG_CASE)
       default:

@@ -62,7 +62,7 @@ EXPORTS = [
     "ilqg_forward", "ilqg_fd_sweep", "ilqg_backward", "ilqg_iterate", "ilqg_synchronize",
     "ilqg_solver_stream", "ilqg_solver_device_costs", "ilqg_solver_set_stream", "ilqg_solver_set_timing",
     "ilqg_solver_get_timing",
-    "ilqg_solver_debug_set_fault", "ilqg_solver_device_traj",
+    "ilqg_solver_debug_set_fault", "ilqg_solver_device_traj", "ilqg_solver_set_groups", "ilqg_solver_get_groups",
 ]
 KERNELS = ("rollout", "select", "fd_centre", "fd_cols", "backward", "fd_backward")
 
@@ -384,6 +384,18 @@ class ILQR:
     def set_stream(self, stream: Optional[int]):
         """enqueue on an external hipStream_t (e.g. torch.cuda.current_stream().cuda_stream)"""
         _check(lib().ilqg_solver_set_stream(self._h, ctypes.c_void_p(stream) if stream else None), "set_stream")
+
+    def set_groups(self, ngroups: int, roll_cus: int = 0):
+        """pipelined seed groups (ilqg_solver_set_groups): ngroups seed ranges whose
+        rollouts overlap each other's FD sweeps; roll_cus > 0 puts the rollouts on
+        that many CUs and the sweeps on the rest.  Bit-identical to ngroups = 1."""
+        _check(lib().ilqg_solver_set_groups(self._h, int(ngroups), int(roll_cus)), "set_groups")
+
+    def groups(self):
+        """(ngroups, roll_cus) in effect"""
+        g, c = ctypes.c_int(), ctypes.c_int()
+        _check(lib().ilqg_solver_get_groups(self._h, ctypes.byref(g), ctypes.byref(c)), "get_groups")
+        return g.value, c.value
 
     def set_timing(self, enable: bool):
         _check(lib().ilqg_solver_set_timing(self._h, int(enable)), "set_timing")

@@ -151,6 +151,18 @@ int ilqg_solver_set_stream(ilqg_solver* s, void* stream);
 int ilqg_solver_set_timing(ilqg_solver* s, int enable);
 /* synchronises; returns summed device ms and launch counts per kernel, then resets */
 int ilqg_solver_get_timing(ilqg_solver* s, double* ms, int* launches);
+/* MI355X extension (no reference counterpart; ILQR::iterate is one seed):
+   pipelined seed groups.  The solver's seeds as `ngroups` contiguous ranges;
+   each range's rollout + selection runs on a stream of its own, the ranges'
+   fused FD sweeps (with the Riccati recursion) take turns on one sweep
+   stream, so one range's latency-bound rollout overlaps another range's
+   throughput-bound sweep.  roll_cus > 0: the rollout streams run on that many
+   CUs (spread over every XCD), the sweep stream on the others.  Results are
+   bit-identical to ngroups = 1 (one stream).  ilqg_iterate returns with the
+   per-seed costs ordered on the solver stream (ilqg_solver_device_costs) and
+   the sweeps still running behind it; ilqg_synchronize waits for all of it. */
+int ilqg_solver_set_groups(ilqg_solver* s, int ngroups, int roll_cus);
+int ilqg_solver_get_groups(ilqg_solver* s, int* ngroups, int* roll_cus);
 /* device pointer to the per-seed selected-candidate cost (nseed doubles), for
    an in-stream collective (RCCL all-gather) without a host round trip */
 int ilqg_solver_device_costs(ilqg_solver* s, double** dptr);
