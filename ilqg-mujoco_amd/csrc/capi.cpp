@@ -68,16 +68,6 @@ bool use_static() {
   return v == 1;
 }
 
-// kernel family: cooperative (one wavefront per evaluation, LDS workspace,
-// default) or lane-per-evaluation (ILQG_PATH=lane; kept for A/B comparison)
-bool use_coop() {
-  static int v = -1;
-  if (v < 0) {
-    const char* e = getenv("ILQG_PATH");
-    v = (e && !strcmp(e, "lane")) ? 0 : 1;
-  }
-  return v == 1;
-}
 constexpr size_t kMaxLds = 160 * 1024;
 
 static int getenv_int(const char* name, int dflt) {
@@ -126,7 +116,6 @@ struct ilqg_model {
   int dev = -1;
   DevBuf buf;
   DevModel dm{};
-  WsLayout L{};   // lane-per-evaluation layout
   WsLayout Lc{};  // cooperative layout (union scratch)
   coop::CoopAux X{};
   coop::CoopLayout C{};
@@ -220,7 +209,6 @@ struct ilqg_model {
     dm.img = static_cast<const unsigned char*>(buf.p);
     dm.img_bytes = (int)img.size();
     dm.static_id = use_static() ? static_id : 0;
-    L = make_layout(dm);
     Lc = make_layout(dm, npair);
     X.isanc = reinterpret_cast<const int*>(static_cast<unsigned char*>(buf.p) + isanc_at);
     X.pair = reinterpret_cast<const int*>(static_cast<unsigned char*>(buf.p) + pair_at);
@@ -228,6 +216,9 @@ struct ilqg_model {
     X.pmask = h.nv <= 64 ? reinterpret_cast<const unsigned long long*>(static_cast<unsigned char*>(buf.p) + pmask_at)
                          : nullptr;
     C = coop::make_coop_layout(dm, npair);
+    // no LDS left for the model image (humanoid): the kernels read it from its
+    // global copy (stage_model with C.imgd == 0)
+    if (coop_lds_bytes(Lc, C) > kMaxLds) C.imgd = 0;
     if (getenv("ILQG_VERBOSE"))
       fprintf(stderr, "ilqg: model nq=%d nv=%d static_id=%d lds/team=%zu B (ws %d + coop %d + image %d doubles, %d ints)\n",
               h.nq, h.nv, dm.static_id, coop_lds_bytes(Lc, C), Lc.nd, C.nd, C.imgd, Lc.ni + C.ni);
@@ -251,8 +242,7 @@ struct ilqg_solver {
   hipStream_t stream = nullptr;
   DevBuf traj[5], cand[5], dinit[5];
   DevBuf qfrc_applied, xfrc_applied, K, k, deriv, warm_c, cost_c, V, v, cost_cand, cost_sel, sel, alphas, cost;
-  DevBuf wsd, wsi, cw, sync, fault;
-  int nlanes = 0;
+  DevBuf cw, sync, fault;
   std::vector<double> host_alphas;
   bool initialized = false;
   hipStream_t own_stream = nullptr;
@@ -329,7 +319,6 @@ struct ilqg_solver {
     return CostDev{c, c + nq, c + 2 * nq, c + 3 * nq, c + 3 * nq + nv, c + 3 * nq + 2 * nv,
                    c + 3 * nq + 3 * nv, c + 3 * nq + 3 * nv + nu, c + 3 * nq + 3 * nv + 2 * nu};
   }
-  WsDev ws() const { return WsDev{wsd.as<double>(), wsi.as<int>(), nlanes}; }
   // every stream the solver launches on
   hipError_t sync_all() {
     hipError_t e = hipStreamSynchronize(stream);
@@ -434,9 +423,10 @@ int ilqg_model_qpos0(const ilqg_model* m, double* q) {
 // cooperative kernels: LDS workspace within one CU's 160 KB, rollout record
 // prefetch within 4 registers per lane (kernels_coop.hip)
 static bool coop_ok(const ilqg_model* m) {
-  const HostModel& h = m->host;
-  const int rec = h.nq + h.nv + 2 * h.nu + 2 * h.nv * h.nu;
-  return use_coop() && coop_lds_bytes(m->Lc, m->C) <= kMaxLds && rec <= 4 * 64;
+  return coop_lds_bytes(m->Lc, m->C) <= kMaxLds;
+}
+static int lds_fail() {
+  return fail(ILQG_ERR_UNSUPPORTED, "model workspace exceeds one CU's LDS (160 KB)");
 }
 
 // fused FD sweep (kernels_coop.hip k_fd_fused_*): cooperative models whose
@@ -491,9 +481,9 @@ int ilqg_model_blob(const ilqg_model* m, void* buf, size_t cap, size_t* needed) 
 // ------------------------------------------------------ batched physics --
 namespace {
 struct Scratch {
-  DevBuf time, qpos, qvel, warm, ctrl, qa, xf, out, wsd, wsi, warm_c, cost_c, cost;
+  DevBuf time, qpos, qvel, warm, ctrl, qa, xf, out, warm_c, cost_c, cost;
 };
-int prep_batch(ilqg_model* m, int n, int lanes, Scratch& s, const double* time, const double* qpos,
+int prep_batch(ilqg_model* m, int n, Scratch& s, const double* time, const double* qpos,
                const double* qvel, const double* warm, const double* ctrl, const double* qfrc_applied,
                const double* xfrc_applied) {
   std::string why;
@@ -509,8 +499,7 @@ int prep_batch(ilqg_model* m, int n, int lanes, Scratch& s, const double* time, 
   HIPCHK(s.ctrl.alloc((size_t)n * h.nu * 8));
   HIPCHK(s.qa.alloc((size_t)n * h.nv * 8));
   HIPCHK(s.xf.alloc((size_t)n * 6 * h.nbody * 8));
-  HIPCHK(s.wsd.alloc((size_t)lanes * m->L.nd * 8));
-  HIPCHK(s.wsi.alloc((size_t)lanes * m->L.ni * 4));
+  if (!coop_ok(m)) return lds_fail();
   auto up = [&](DevBuf& b, const double* src, size_t cnt) -> hipError_t {
     if (!src) return hipSuccess;
     return hipMemcpy(b.p, src, cnt * 8, hipMemcpyHostToDevice);
@@ -532,11 +521,10 @@ int ilqg_step_batch(const ilqg_model* mc, int n, int nstep, double* time, double
   if (!m || n <= 0 || nstep < 0 || !qpos || !qvel || !warm || !ctrl) return fail(ILQG_ERR_ARG, "bad argument");
   Scratch s;
   std::vector<double> t0(n, 0.0);
-  int rc = prep_batch(m, n, n, s, time ? time : t0.data(), qpos, qvel, warm, ctrl, qfrc_applied, xfrc_applied);
+  int rc = prep_batch(m, n, s, time ? time : t0.data(), qpos, qvel, warm, ctrl, qfrc_applied, xfrc_applied);
   if (rc) return rc;
   TrajDev st{s.time.as<double>(), s.qpos.as<double>(), s.qvel.as<double>(), s.warm.as<double>(), s.ctrl.as<double>()};
-  HIPCHK(launch_step(m->dm, m->L, WsDev{s.wsd.as<double>(), s.wsi.as<int>(), n}, st, n, nstep, s.qa.as<double>(),
-                     s.xf.as<double>(), m->stream));
+  HIPCHK(launch_step_coop(m->dm, m->Lc, m->C, m->X, st, n, nstep, s.qa.as<double>(), s.xf.as<double>(), m->stream));
   HIPCHK(hipStreamSynchronize(m->stream));
   const HostModel& h = m->host;
   if (time) HIPCHK(hipMemcpy(time, s.time.p, n * 8, hipMemcpyDeviceToHost));
@@ -552,13 +540,13 @@ int ilqg_forward_batch(const ilqg_model* mc, int n, const double* qpos, const do
   if (!m || n <= 0 || !qpos || !qvel || !warm || !ctrl || !qacc) return fail(ILQG_ERR_ARG, "bad argument");
   Scratch s;
   std::vector<double> t0(n, 0.0);
-  int rc = prep_batch(m, n, n, s, t0.data(), qpos, qvel, warm, ctrl, qfrc_applied, xfrc_applied);
+  int rc = prep_batch(m, n, s, t0.data(), qpos, qvel, warm, ctrl, qfrc_applied, xfrc_applied);
   if (rc) return rc;
   const HostModel& h = m->host;
   HIPCHK(s.out.alloc((size_t)n * h.nv * 8));
   TrajDev st{s.time.as<double>(), s.qpos.as<double>(), s.qvel.as<double>(), s.warm.as<double>(), s.ctrl.as<double>()};
-  HIPCHK(launch_forward(m->dm, m->L, WsDev{s.wsd.as<double>(), s.wsi.as<int>(), n}, st, n, s.qa.as<double>(),
-                        s.xf.as<double>(), s.out.as<double>(), m->stream));
+  HIPCHK(launch_forward_coop(m->dm, m->Lc, m->C, m->X, st, n, s.qa.as<double>(), s.xf.as<double>(),
+                             s.out.as<double>(), m->stream));
   HIPCHK(hipStreamSynchronize(m->stream));
   HIPCHK(hipMemcpy(qacc, s.out.p, (size_t)n * h.nv * 8, hipMemcpyDeviceToHost));
   HIPCHK(hipMemcpy(warm, s.warm.p, (size_t)n * h.nv * 8, hipMemcpyDeviceToHost));
@@ -575,8 +563,7 @@ int ilqg_fd_batch(const ilqg_model* mc, int n, const double* qpos, const double*
   const int D = h.nv * (2 * h.nv + h.nu) + 2 * h.nv + h.nu;
   Scratch s;
   std::vector<double> t0(n, 0.0);
-  int lanes = n * ncol;
-  int rc = prep_batch(m, n, lanes, s, t0.data(), qpos, qvel, warm, ctrl, qfrc_applied, xfrc_applied);
+  int rc = prep_batch(m, n, s, t0.data(), qpos, qvel, warm, ctrl, qfrc_applied, xfrc_applied);
   if (rc) return rc;
   std::vector<double> cp = pack_cost(h, cost);
   HIPCHK(s.cost.alloc(cp.size() * 8));
@@ -589,7 +576,6 @@ int ilqg_fd_batch(const ilqg_model* mc, int n, const double* qpos, const double*
   CostDev cd{c, c + nq, c + 2 * nq, c + 3 * nq, c + 3 * nq + nv, c + 3 * nq + 2 * nv,
              c + 3 * nq + 3 * nv, c + 3 * nq + 3 * nv + nu, c + 3 * nq + 3 * nv + 2 * nu};
   TrajDev st{s.time.as<double>(), s.qpos.as<double>(), s.qvel.as<double>(), s.warm.as<double>(), s.ctrl.as<double>()};
-  WsDev ws{s.wsd.as<double>(), s.wsi.as<int>(), lanes};
   if (fused_ok(m)) {
     // n points as n one-point trajectories through the fused sweep (no backward roles)
     const int Dp = round16(D), WCp = round16(h.nv + 1), cv = fd_cv();
@@ -611,16 +597,11 @@ int ilqg_fd_batch(const ilqg_model* mc, int n, const double* qpos, const double*
     if (flt) return fail(ILQG_ERR_HIP, "fused FD sweep: a hand-off wait timed out");
     HIPCHK(hipMemcpy2D(deriv, (size_t)D * 8, outp.p, (size_t)Dp * 8, (size_t)D * 8, n, hipMemcpyDeviceToHost));
     return ILQG_OK;
-  } else if (coop_ok(m)) {
+  } else {
     HIPCHK(launch_fd_centre_coop(m->dm, m->Lc, m->C, m->X, st, n, 1, s.qa.as<double>(), s.xf.as<double>(), cd,
                                  s.warm_c.as<double>(), s.cost_c.as<double>(), m->stream));
     HIPCHK(launch_fd_cols_coop(m->dm, m->Lc, m->C, m->X, st, n, 1, s.qa.as<double>(), s.xf.as<double>(), cd,
                                s.warm_c.as<double>(), s.cost_c.as<double>(), s.out.as<double>(), D, m->stream));
-  } else {
-    HIPCHK(launch_fd_centre(m->dm, m->L, ws, st, n, 1, s.qa.as<double>(), s.xf.as<double>(), cd,
-                            s.warm_c.as<double>(), s.cost_c.as<double>(), m->stream));
-    HIPCHK(launch_fd_cols(m->dm, m->L, ws, st, n, 1, s.qa.as<double>(), s.xf.as<double>(), cd,
-                          s.warm_c.as<double>(), s.cost_c.as<double>(), s.out.as<double>(), D, m->stream));
   }
   HIPCHK(hipStreamSynchronize(m->stream));
   HIPCHK(hipMemcpy(deriv, s.out.p, (size_t)n * D * 8, hipMemcpyDeviceToHost));
@@ -637,6 +618,7 @@ int ilqg_solver_create(const ilqg_model* mc, const ilqg_solver_opts* o, const il
   if (rc) return fail(rc, why);
   rc = m->upload(o->device);
   if (rc) return rc;
+  if (!coop_ok(m)) return lds_fail();
   const HostModel& h = m->host;
   auto* s = new ilqg_solver();
   s->model = m;
@@ -692,9 +674,6 @@ int ilqg_solver_create(const ilqg_model* mc, const ilqg_solver_opts* o, const il
   ALLOC(s->alphas, A * 8);
   std::vector<double> cp = pack_cost(h, cost);
   ALLOC(s->cost, cp.size() * 8);
-  s->nlanes = (int)std::max({S * P * (size_t)s->ncol, S * A, S * P});
-  ALLOC(s->wsd, (size_t)s->nlanes * m->L.nd * 8);
-  ALLOC(s->wsi, (size_t)s->nlanes * m->L.ni * 4);
   e = hipMemcpy(s->alphas.p, s->host_alphas.data(), A * 8, hipMemcpyHostToDevice);
   if (e != hipSuccess) return fail_free(e, "alphas");
   e = hipMemcpy(s->cost.p, cp.data(), cp.size() * 8, hipMemcpyHostToDevice);
@@ -737,14 +716,9 @@ int ilqg_solver_init(ilqg_solver* s, const double* time, const double* qpos, con
     HIPCHK(hipMemcpy(s->xfrc_applied.p, xfrc_applied, (size_t)s->S * 6 * h.nbody * 8, hipMemcpyHostToDevice));
   // ILQR ctor: passive rollout with constant ctrl into dArray[N..0]
   TrajDev nom = s->tview(s->traj), di = s->tview(s->dinit);
-  if (coop_ok(m))
-    HIPCHK(launch_rollout_coop(m->dm, m->Lc, m->C, m->X, s->S, 1, s->P, nom, nom, 0, s->K.as<double>(),
-                               s->k.as<double>(), nullptr, di, s->qfrc_applied.as<double>(),
-                               s->xfrc_applied.as<double>(), 1, s->cview(), nullptr, s->stream));
-  else
-    HIPCHK(launch_rollout(m->dm, m->L, s->ws(), s->S, 1, s->P, nom, nom, 0, s->K.as<double>(), s->k.as<double>(),
-                          nullptr, di, s->qfrc_applied.as<double>(), s->xfrc_applied.as<double>(), 1, s->cview(),
-                          nullptr, s->stream));
+  HIPCHK(launch_rollout_coop(m->dm, m->Lc, m->C, m->X, s->S, 1, s->P, nom, nom, 0, s->K.as<double>(),
+                             s->k.as<double>(), nullptr, di, s->qfrc_applied.as<double>(),
+                             s->xfrc_applied.as<double>(), 1, s->cview(), nullptr, s->stream));
   HIPCHK(s->sync_all());
   // setDInit(dmain) as the MPC driver does before iterating (src/inverted_pendulum/inverted_pendulum.cpp:21)
   s->initialized = true;
@@ -851,11 +825,8 @@ static hipError_t forward_range(ilqg_solver* s, const SeedRange& r, hipEvent_t b
   const double* xf = s->xfrc_applied.as<double>() + s0 * 6 * h.nbody;
   double* cc = s->cost_cand.as<double>() + s0 * A;
   hipError_t e = s->timed(0, [&] {
-    if (coop_ok(m))
-      return launch_rollout_coop(m->dm, m->Lc, m->C, m->X, r.ns, s->A, s->P, nom, outv, multi ? 1 : 0, K, k,
-                                 s->alphas.as<double>(), di, qa, xf, 0, s->cview(), cc, r.st);
-    return launch_rollout(m->dm, m->L, s->ws(), r.ns, s->A, s->P, nom, outv, multi ? 1 : 0, K, k,
-                          s->alphas.as<double>(), di, qa, xf, 0, s->cview(), cc, r.st);
+    return launch_rollout_coop(m->dm, m->Lc, m->C, m->X, r.ns, s->A, s->P, nom, outv, multi ? 1 : 0, K, k,
+                               s->alphas.as<double>(), di, qa, xf, 0, s->cview(), cc, r.st);
   }, r.st);
   if (e != hipSuccess) return e;
   if (before_select) {
@@ -923,22 +894,14 @@ int ilqg_fd_sweep(ilqg_solver* s) {
     return ILQG_OK;
   }
   HIPCHK(s->timed(2, [&] {
-    if (coop_ok(m))
-      return launch_fd_centre_coop(m->dm, m->Lc, m->C, m->X, nom, npts, s->P, s->qfrc_applied.as<double>(),
-                                   s->xfrc_applied.as<double>(), s->cview(), s->warm_c.as<double>(),
-                                   s->cost_c.as<double>(), s->stream);
-    return launch_fd_centre(m->dm, m->L, s->ws(), nom, npts, s->P, s->qfrc_applied.as<double>(),
-                            s->xfrc_applied.as<double>(), s->cview(), s->warm_c.as<double>(),
-                            s->cost_c.as<double>(), s->stream);
+    return launch_fd_centre_coop(m->dm, m->Lc, m->C, m->X, nom, npts, s->P, s->qfrc_applied.as<double>(),
+                                 s->xfrc_applied.as<double>(), s->cview(), s->warm_c.as<double>(),
+                                 s->cost_c.as<double>(), s->stream);
   }));
   HIPCHK(s->timed(3, [&] {
-    if (coop_ok(m))
-      return launch_fd_cols_coop(m->dm, m->Lc, m->C, m->X, nom, npts, s->P, s->qfrc_applied.as<double>(),
-                                 s->xfrc_applied.as<double>(), s->cview(), s->warm_c.as<double>(),
-                                 s->cost_c.as<double>(), s->deriv.as<double>(), s->Dp, s->stream);
-    return launch_fd_cols(m->dm, m->L, s->ws(), nom, npts, s->P, s->qfrc_applied.as<double>(),
-                          s->xfrc_applied.as<double>(), s->cview(), s->warm_c.as<double>(), s->cost_c.as<double>(),
-                          s->deriv.as<double>(), s->Dp, s->stream);
+    return launch_fd_cols_coop(m->dm, m->Lc, m->C, m->X, nom, npts, s->P, s->qfrc_applied.as<double>(),
+                               s->xfrc_applied.as<double>(), s->cview(), s->warm_c.as<double>(),
+                               s->cost_c.as<double>(), s->deriv.as<double>(), s->Dp, s->stream);
   }));
   return ILQG_OK;
 }

@@ -46,6 +46,13 @@ __device__ inline Team make_team(const auto& L, const auto& C) {
 // read on the serial paths then costs an LDS round trip instead of an L2 one.
 __device__ inline void stage_model(const DevModel& g, const CoopAux& Xg, const WsLayout& L, const CoopLayout& C,
                                    const Team& T, DevModel& m, CoopAux& X) {
+  if (C.imgd == 0) {
+    // layouts without an image region (models whose workspace leaves no LDS
+    // for it, e.g. the humanoid): every model read goes to the global image
+    m = g;
+    X = Xg;
+    return;
+  }
   extern __shared__ double lds[];
   double* dst = lds + L.nd + C.nd;
   const double* src = reinterpret_cast<const double*>(g.img);

@@ -1,4 +1,4 @@
-// Launch interface of the hot-path kernels (implemented in kernels.hip).
+// Launch interface of the hot-path kernels (kernels_rollout.hip, kernels_fd.hip, riccati.hip).
 #pragma once
 
 #include <hip/hip_runtime.h>
@@ -21,26 +21,6 @@ struct CostDev {
   const double *wq, *tq, *lq, *wv, *tv, *lv, *wu, *tu, *lu;
 };
 
-// per-evaluation workspace
-struct WsDev {
-  double* d;
-  int* i;
-  int nlanes;
-};
-
-// FD centre: npts points (point -> seed = point / P), 1 lane each
-hipError_t launch_fd_centre(const DevModel& m, const WsLayout& L, WsDev ws, TrajDev tr, int npts, int P,
-                            const double* qfrc_applied, const double* xfrc_applied, CostDev cost,
-                            double* warm_c, double* cost_c, hipStream_t st);
-// FD columns: npts * (nctrl + 2nv) lanes, writes deriv[npts][D]
-hipError_t launch_fd_cols(const DevModel& m, const WsLayout& L, WsDev ws, TrajDev tr, int npts, int P,
-                          const double* qfrc_applied, const double* xfrc_applied, CostDev cost,
-                          const double* warm_c, const double* cost_c, double* deriv, int Ds, hipStream_t st);
-// rollout: S*A lanes; passive=1 keeps ctrl (ILQR ctor), else u = K dx + alpha k + u*
-hipError_t launch_rollout(const DevModel& m, const WsLayout& L, WsDev ws, int S, int A, int P, TrajDev nominal,
-                          TrajDev out, int out_is_cand, const double* K, const double* k, const double* alphas,
-                          TrajDev dinit, const double* qfrc_applied, const double* xfrc_applied, int passive,
-                          CostDev cost, double* cost_cand, hipStream_t st);
 // candidate selection + setDInit(dArray[N])
 hipError_t launch_select(const DevModel& m, int S, int A, int P, int mode, int copy_cand, const double* cost_cand,
                          int* sel, double* cost_sel, TrajDev cand, TrajDev nominal, TrajDev dinit, hipStream_t st);
@@ -48,13 +28,6 @@ hipError_t launch_select(const DevModel& m, int S, int A, int P, int mode, int c
 // deriv records at stride Ds (>= D) doubles
 hipError_t launch_backward(const DevModel& m, int S, int P, double mu, const double* deriv, int Ds, TrajDev tr,
                            double* K, double* k, double* V, double* v, hipStream_t st);
-// n independent states: nstep mj_step each (in place)
-hipError_t launch_step(const DevModel& m, const WsLayout& L, WsDev ws, TrajDev st_, int n, int nstep,
-                       const double* qfrc_applied, const double* xfrc_applied, hipStream_t st);
-// n independent states: mj_forward -> qacc
-hipError_t launch_forward(const DevModel& m, const WsLayout& L, WsDev ws, TrajDev st_, int n,
-                          const double* qfrc_applied, const double* xfrc_applied, double* qacc, hipStream_t st);
-
 size_t backward_lds_bytes(int nv, int nu);
 
 // fused FD sweep + streamed backward pass (kernels_coop.hip)
@@ -97,4 +70,12 @@ hipError_t launch_rollout_coop(const DevModel& m, const WsLayout& L, const coop:
                                int out_is_cand, const double* K, const double* k, const double* alphas, TrajDev dinit,
                                const double* qfrc_applied, const double* xfrc_applied, int passive, CostDev cost,
                                double* cost_cand, hipStream_t st);
+// n independent states, one wavefront each: nstep mj_step (in place)
+hipError_t launch_step_coop(const DevModel& m, const WsLayout& L, const coop::CoopLayout& C, const coop::CoopAux& X,
+                            TrajDev stt, int n, int nstep, const double* qfrc_applied, const double* xfrc_applied,
+                            hipStream_t st);
+// n independent states, one wavefront each: mj_forward -> qacc, warm start updated
+hipError_t launch_forward_coop(const DevModel& m, const WsLayout& L, const coop::CoopLayout& C,
+                               const coop::CoopAux& X, TrajDev stt, int n, const double* qfrc_applied,
+                               const double* xfrc_applied, double* qacc, hipStream_t st);
 }  // namespace ilqg

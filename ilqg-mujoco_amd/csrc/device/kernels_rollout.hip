@@ -44,6 +44,9 @@ __device__ inline void rollout_body(const auto& m, const auto& L, const auto& C,
   };
   constexpr int PFR = 4;  // registers per lane: R <= 4 * 64
   double pf[PFR];
+  // larger records (humanoid: K alone is nu x 2nv = 1134 doubles) are not
+  // prefetched: park() copies them from global memory directly
+  const bool pfok = R <= PFR * TEAM_SIZE;
   if (!passive) {
     FOR_T(t, R) rec[t] = fetch((size_t)s * P + (P - 1), t);
     TSYNC();
@@ -57,7 +60,7 @@ __device__ inline void rollout_body(const auto& m, const auto& L, const auto& C,
   // control law u = u* + alpha k + K (x - x*) for point n, its record and cost
   // (ilqr.h:116-133); the next point's nominal record is prefetched first
   auto pre_step = [&](int n) {
-    const bool pre = !passive && n > 0;
+    const bool pre = !passive && n > 0 && pfok;
     if (pre) {
       const size_t pn1 = (size_t)s * P + (n - 1);
 #pragma unroll
@@ -92,10 +95,14 @@ __device__ inline void rollout_body(const auto& m, const auto& L, const auto& C,
   // the prefetched record replaces the current one once the step no longer reads it
   auto park = [&](int n) {
     if (!passive && n > 0) {
+      if (pfok) {
 #pragma unroll
-      for (int q = 0; q < PFR; q++) {
-        const int t = T.tid + q * TEAM_SIZE;
-        if (t < R) rec[t] = pf[q];
+        for (int q = 0; q < PFR; q++) {
+          const int t = T.tid + q * TEAM_SIZE;
+          if (t < R) rec[t] = pf[q];
+        }
+      } else {
+        FOR_T(t, R) rec[t] = fetch((size_t)s * P + (n - 1), t);
       }
       TSYNC();
     }
@@ -167,6 +174,119 @@ __global__ __launch_bounds__(2 * TEAM) void k_rollout2_s(DevModel mg, int S, int
                passive, cost, cost_cand, (int)(threadIdx.x / TEAM), std::bool_constant<SM::nv <= RMAX>{});
 }
 
+// ---- batch physics (ilqg_step_batch / ilqg_forward_batch): one wavefront per state
+// mj_step x nstep from each state (cpMjData in, the state out)
+__device__ inline void step_batch_body(const auto& m, const auto& L, const auto& C, const auto& X, const Team& T,
+                                       TrajDev stt, int nstep, const double* qfrc_applied, const double* xfrc_applied) {
+  const int i = blockIdx.x;
+  load_state(m, L, T, stt, i, i, qfrc_applied, xfrc_applied);
+  for (int t = 0; t < nstep; t++) step(m, L, C, X, T);
+  if (T.tid == 0) stt.time[i] = T.w[L.time];
+  FOR_T(k, m.nq) stt.qpos[(size_t)i * m.nq + k] = T.w[L.qpos + k];
+  FOR_T(k, m.nv) {
+    stt.qvel[(size_t)i * m.nv + k] = T.w[L.qvel + k];
+    stt.warm[(size_t)i * m.nv + k] = T.w[L.warm + k];
+  }
+}
+// mj_forward at each state: qacc out, qacc_warmstart updated in place
+__device__ inline void fwd_batch_body(const auto& m, const auto& L, const auto& C, const auto& X, const Team& T,
+                                      TrajDev stt, const double* qfrc_applied, const double* xfrc_applied,
+                                      double* qacc) {
+  const int i = blockIdx.x;
+  load_state(m, L, T, stt, i, i, qfrc_applied, xfrc_applied);
+  forward_skip(m, L, C, X, T, STAGE_NONE, m.opt_iterations, m.opt_tolerance);
+  FOR_T(k, m.nv) {
+    qacc[(size_t)i * m.nv + k] = T.w[L.qacc + k];
+    stt.warm[(size_t)i * m.nv + k] = T.w[L.warm + k];
+  }
+}
+__global__ __launch_bounds__(TEAM) void k_step_coop(DevModel mg, WsLayout L, CoopLayout C, CoopAux Xg, TrajDev stt,
+                                                    int nstep, const double* qfrc_applied, const double* xfrc_applied) {
+  Team T = make_team(L, C);
+  DevModel m;
+  CoopAux X;
+  stage_model(mg, Xg, L, C, T, m, X);
+  step_batch_body(m, L, C, X, T, stt, nstep, qfrc_applied, xfrc_applied);
+}
+template <class SM, class SX>
+__global__ __launch_bounds__(TEAM) void k_step_s(DevModel mg, TrajDev stt, int nstep, const double* qfrc_applied,
+                                                 const double* xfrc_applied) {
+  static constexpr WsLayout L = make_layout(SM{}, SX::npair);
+  static constexpr CoopLayout C = make_coop_layout(SM{}, SX::npair);
+  static constexpr SX X{};
+  Team T = make_team(L, C);
+  SM m;
+  stage_model_sep(mg, T, m);
+  step_batch_body(m, L, C, X, T, stt, nstep, qfrc_applied, xfrc_applied);
+}
+__global__ __launch_bounds__(TEAM) void k_fwd_coop(DevModel mg, WsLayout L, CoopLayout C, CoopAux Xg, TrajDev stt,
+                                                   const double* qfrc_applied, const double* xfrc_applied,
+                                                   double* qacc) {
+  Team T = make_team(L, C);
+  DevModel m;
+  CoopAux X;
+  stage_model(mg, Xg, L, C, T, m, X);
+  fwd_batch_body(m, L, C, X, T, stt, qfrc_applied, xfrc_applied, qacc);
+}
+template <class SM, class SX>
+__global__ __launch_bounds__(TEAM) void k_fwd_s(DevModel mg, TrajDev stt, const double* qfrc_applied,
+                                                const double* xfrc_applied, double* qacc) {
+  static constexpr WsLayout L = make_layout(SM{}, SX::npair);
+  static constexpr CoopLayout C = make_coop_layout(SM{}, SX::npair);
+  static constexpr SX X{};
+  Team T = make_team(L, C);
+  SM m;
+  stage_model_sep(mg, T, m);
+  fwd_batch_body(m, L, C, X, T, stt, qfrc_applied, xfrc_applied, qacc);
+}
+
+// line-search selection + setDInit (inc/ilqr.h:110-113): per seed, the
+// candidate with the smallest trajectory cost (mode 1; a NaN cost never wins
+// over a number) or alpha = 1 (mode 0), copied to the nominal trajectory
+__global__ void k_select(int nq, int nv, int nu, int S, int A, int P, int mode, int copy_cand,
+                         const double* cost_cand, int* sel, double* cost_sel, TrajDev cand, TrajDev nom,
+                         TrajDev dinit) {
+  int s = blockIdx.x;
+  __shared__ int best_sh;
+  if (threadIdx.x == 0) {
+    int best = 0;
+    if (mode == 1 && cost_cand) {
+      double bc = cost_cand[(size_t)s * A];
+      for (int a = 1; a < A; a++) {
+        double c = cost_cand[(size_t)s * A + a];
+        if (c < bc || (bc != bc && c == c)) { bc = c; best = a; }
+      }
+    }
+    best_sh = best;
+    if (sel) sel[s] = best;
+    if (cost_sel && cost_cand) cost_sel[s] = cost_cand[(size_t)s * A + best];
+  }
+  __syncthreads();
+  int best = best_sh;
+  if (copy_cand) {
+    size_t src0 = ((size_t)s * A + best) * P, dst0 = (size_t)s * P;
+    for (int p = threadIdx.x; p < P; p += blockDim.x) {
+      nom.time[dst0 + p] = cand.time[src0 + p];
+      for (int i = 0; i < nq; i++) nom.qpos[(dst0 + p) * nq + i] = cand.qpos[(src0 + p) * nq + i];
+      for (int i = 0; i < nv; i++) nom.qvel[(dst0 + p) * nv + i] = cand.qvel[(src0 + p) * nv + i];
+      for (int i = 0; i < nv; i++) nom.warm[(dst0 + p) * nv + i] = cand.warm[(src0 + p) * nv + i];
+      for (int i = 0; i < nu; i++) nom.ctrl[(dst0 + p) * nu + i] = cand.ctrl[(src0 + p) * nu + i];
+    }
+  }
+  __syncthreads();
+  // setDInit(dArray[N]), inc/ilqr.h:183
+  if (threadIdx.x == 0) {
+    size_t src = (size_t)s * P + (P - 1);
+    const TrajDev& t = copy_cand ? cand : nom;
+    size_t sp = copy_cand ? ((size_t)s * A + best) * P + (P - 1) : src;
+    dinit.time[s] = t.time[sp];
+    for (int i = 0; i < nq; i++) dinit.qpos[(size_t)s * nq + i] = t.qpos[sp * nq + i];
+    for (int i = 0; i < nv; i++) dinit.qvel[(size_t)s * nv + i] = t.qvel[sp * nv + i];
+    for (int i = 0; i < nv; i++) dinit.warm[(size_t)s * nv + i] = t.warm[sp * nv + i];
+    for (int i = 0; i < nu; i++) dinit.ctrl[(size_t)s * nu + i] = t.ctrl[sp * nu + i];
+  }
+}
+
 }  // namespace
 
 static bool use_dual() {
@@ -236,6 +356,67 @@ hipError_t launch_rollout_coop(const DevModel& m, const WsLayout& L, const CoopL
   if (e != hipSuccess) return e;
   hipLaunchKernelGGL(k_rollout_coop, dim3(S * A), dim3(TEAM), coop_lds_bytes(L, C), st, m, L, C, X, S, A, P, nominal,
                      out, out_is_cand, K, k, alphas, dinit, qfrc_applied, xfrc_applied, passive, cost, cost_cand);
+  return hipGetLastError();
+}
+
+hipError_t launch_select(const DevModel& m, int S, int A, int P, int mode, int copy_cand, const double* cost_cand,
+                         int* sel, double* cost_sel, TrajDev cand, TrajDev nominal, TrajDev dinit, hipStream_t st) {
+  hipLaunchKernelGGL(k_select, dim3(S), dim3(256), 0, st, m.nq, m.nv, m.nu, S, A, P, mode, copy_cand, cost_cand,
+                     sel, cost_sel, cand, nominal, dinit);
+  return hipGetLastError();
+}
+
+hipError_t launch_step_coop(const DevModel& m, const WsLayout& L, const CoopLayout& C, const CoopAux& X,
+                            TrajDev stt, int n, int nstep, const double* qfrc_applied, const double* xfrc_applied,
+                            hipStream_t st) {
+  if (n <= 0) return hipSuccess;
+  hipError_t e;
+#define ILQG_CASE(id, SMT, SXT)                                                                                  \
+  case id: {                                                                                                     \
+    const size_t lds = coop_lds_bytes(make_layout(stat::SMT{}, stat::SXT::npair), C);                           \
+    e = allow_lds(k_step_s<stat::SMT, stat::SXT>, lds);                                                          \
+    if (e != hipSuccess) return e;                                                                               \
+    hipLaunchKernelGGL((k_step_s<stat::SMT, stat::SXT>), dim3(n), dim3(TEAM), lds, st, m, stt, nstep,           \
+                       qfrc_applied, xfrc_applied);                                                              \
+    return hipGetLastError();                                                                                    \
+  }
+  switch (m.static_id) {
+    ILQG_STATIC_MODELS(ILQG_CASE)
+    default:
+      break;
+  }
+#undef ILQG_CASE
+  e = allow_lds(k_step_coop, coop_lds_bytes(L, C));
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(k_step_coop, dim3(n), dim3(TEAM), coop_lds_bytes(L, C), st, m, L, C, X, stt, nstep,
+                     qfrc_applied, xfrc_applied);
+  return hipGetLastError();
+}
+
+hipError_t launch_forward_coop(const DevModel& m, const WsLayout& L, const CoopLayout& C, const CoopAux& X,
+                               TrajDev stt, int n, const double* qfrc_applied, const double* xfrc_applied,
+                               double* qacc, hipStream_t st) {
+  if (n <= 0) return hipSuccess;
+  hipError_t e;
+#define ILQG_CASE(id, SMT, SXT)                                                                                  \
+  case id: {                                                                                                     \
+    const size_t lds = coop_lds_bytes(make_layout(stat::SMT{}, stat::SXT::npair), C);                           \
+    e = allow_lds(k_fwd_s<stat::SMT, stat::SXT>, lds);                                                           \
+    if (e != hipSuccess) return e;                                                                               \
+    hipLaunchKernelGGL((k_fwd_s<stat::SMT, stat::SXT>), dim3(n), dim3(TEAM), lds, st, m, stt, qfrc_applied,     \
+                       xfrc_applied, qacc);                                                                      \
+    return hipGetLastError();                                                                                    \
+  }
+  switch (m.static_id) {
+    ILQG_STATIC_MODELS(ILQG_CASE)
+    default:
+      break;
+  }
+#undef ILQG_CASE
+  e = allow_lds(k_fwd_coop, coop_lds_bytes(L, C));
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(k_fwd_coop, dim3(n), dim3(TEAM), coop_lds_bytes(L, C), st, m, L, C, X, stt, qfrc_applied,
+                     xfrc_applied, qacc);
   return hipGetLastError();
 }
 

@@ -13,7 +13,8 @@ NAMES = {0: "kinematics", 1: "com_pos", 2: "trn+crb", 3: "factor_ld(M)", 4: "col
          24: "A: barrier 1 (wait for B)", 25: "A: barrier 2", 26: "A: barrier 3", 27: "A: barrier 4", 28: "A: barrier 5",
          32: "B: barrier 1 (wait for A kinematics)", 33: "B: collision", 34: "B: barrier 2", 35: "B: make_constraint",
          36: "B: barrier 3", 37: "B: passive+aref", 38: "B: euler prefactor", 39: "B: barrier 4 (A com vel + RNE)",
-         40: "B: barrier 6 (end of step)", 41: "B: control law + record", 42: "B: factor_ld(M)", 43: "B: barrier 5",
+         40: "B: barrier 6 (end of step)", 41: "B: control law + record", 42: "B: factor_ld(M) / limit rows+passive+act",
+         43: "B: barrier 5",
          29: "A: barrier 5b (Euler factor)", 30: "B: Newton warm-start prep"}
 L = ia.lib()
 acc = (ctypes.c_ulonglong * 48)(); cnt = (ctypes.c_ulonglong * 48)()
@@ -29,7 +30,10 @@ for what, fn, rd in (("rollout (1 seed)", g.forward_pass, L.ilqg_debug_stamps),
     fn(); g.synchronize()
     tm = g.timing()
     rd(acc, cnt, 1)
-    tot = sum(acc[i] for i in list(range(10)) + list(range(24, 30)))
+    # wave 0's stamps partition its time: top-level stages, their sub-stages
+    # (11-23: kinematics and Newton pieces, which restart the stage clock) and
+    # the barrier waits
+    tot = sum(acc[i] for i in list(range(10)) + list(range(11, 24)) + list(range(24, 30)))
     ms = sum(v[0] for v in tm.values())
     print(f"== {what}: block 0, lane 0, total {tot} ticks (wave-0 stages + barriers); kernel time {ms:.3f} ms "
           f"-> {tot / (ms * 1e3):.0f} ticks/us if the stages were all of it")
@@ -38,7 +42,8 @@ for what, fn, rd in (("rollout (1 seed)", g.forward_pass, L.ilqg_debug_stamps),
               f"{acc[44] / acc[45]:.2f} iterations per solve")
     if acc[46]:
         print(f"   block 0 lifetime: {acc[46] / 100:.0f} us realtime, {acc[47]} memtime ticks "
-              f"-> shader clock {acc[47] / (acc[46] / 100) :.0f} MHz")
+              f"-> shader clock {acc[47] / (acc[46] / 100) :.0f} MHz; the stamps attribute "
+              f"{tot / acc[47]:.1%} of wave 0's lifetime")
     for i in range(44):
         if cnt[i]:
             print(f"  {NAMES[i]:24s} calls {cnt[i]:6d}  cycles/call {acc[i]/cnt[i]:9.0f}  share {acc[i]/max(tot,1):6.1%}")
