@@ -239,6 +239,7 @@ struct ilqg_solver {
   // fused sweep (fd_fused) also streams the backward pass behind the FD teams
   int Dp = 0, WCp = 0, lag = 0, nvt = 0, cv = 0, nut = 0;
   bool fused = false;
+  int riccati = ILQG_RICCATI_EXACT;  // ilqg_solver_set_riccati
   hipStream_t stream = nullptr;
   DevBuf traj[5], cand[5], dinit[5];
   DevBuf qfrc_applied, xfrc_applied, K, k, deriv, warm_c, cost_c, V, v, cost_cand, cost_sel, sel, alphas, cost;
@@ -911,6 +912,10 @@ int ilqg_backward(ilqg_solver* s) {
   const ilqg_model* m = s->model;
   if (!s->groups.empty()) HIPCHK(s->sync_all());
   HIPCHK(s->timed(4, [&] {
+    if (s->riccati == ILQG_RICCATI_MFMA)
+      return launch_backward_mfma(m->dm, s->S, s->P, s->opts.mu, s->deriv.as<double>(), s->Dp, s->tview(s->traj),
+                                  s->K.as<double>(), s->k.as<double>(), s->V.as<double>(), s->v.as<double>(),
+                                  s->stream);
     return launch_backward(m->dm, s->S, s->P, s->opts.mu, s->deriv.as<double>(), s->Dp, s->tview(s->traj),
                            s->K.as<double>(), s->k.as<double>(), s->V.as<double>(), s->v.as<double>(), s->stream);
   }));
@@ -1011,6 +1016,23 @@ int ilqg_solver_get_timing(ilqg_solver* s, double* ms, int* launches) {
     if (launches) launches[k] = (int)s->ev[k].size();
     s->ev[k].clear();
   }
+  return ILQG_OK;
+}
+
+int ilqg_solver_set_riccati(ilqg_solver* s, int mode) {
+  if (!s || (mode != ILQG_RICCATI_EXACT && mode != ILQG_RICCATI_MFMA)) return fail(ILQG_ERR_ARG, "bad argument");
+  const HostModel& h = s->model->host;
+  if (mode == ILQG_RICCATI_MFMA) {
+    const int D = h.nv * (2 * h.nv + h.nu) + 2 * h.nv + h.nu;
+    if (h.nu > 32 || D > 4096 || backward_mfma_lds_bytes(h.nv, h.nu) > kMaxLds)
+      return fail(ILQG_ERR_UNSUPPORTED, "MFMA Riccati: nu <= 32, FD record <= 4096 doubles, LDS <= 160 KB");
+    if (!s->groups.empty()) return fail(ILQG_ERR_UNSUPPORTED, "MFMA Riccati with seed groups");
+  }
+  HIPCHK(s->sync_all());
+  s->riccati = mode;
+  // the fused sweep streams the bit-exact recursion; the MFMA one runs after a
+  // plain sweep (its workspace -- the hand-off block -- is allocated either way)
+  s->fused = mode == ILQG_RICCATI_EXACT && fused_ok(s->model) && s->sync.p;
   return ILQG_OK;
 }
 

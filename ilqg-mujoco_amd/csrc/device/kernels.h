@@ -29,6 +29,12 @@ hipError_t launch_select(const DevModel& m, int S, int A, int P, int mode, int c
 hipError_t launch_backward(const DevModel& m, int S, int P, double mu, const double* deriv, int Ds, TrajDev tr,
                            double* K, double* k, double* V, double* v, hipStream_t st);
 size_t backward_lds_bytes(int nv, int nu);
+// the same recursion with the matrix products on the fp64 matrix cores
+// (riccati_mfma.h): one 4-wave workgroup per seed; agrees with the oracle to
+// rounding (the product sums run in the matrix core's order)
+hipError_t launch_backward_mfma(const DevModel& m, int S, int P, double mu, const double* deriv, int Ds, TrajDev tr,
+                                double* K, double* k, double* V, double* v, hipStream_t st);
+size_t backward_mfma_lds_bytes(int nv, int nu);
 
 // fused FD sweep + streamed backward pass (kernels_coop.hip)
 struct FdFused {

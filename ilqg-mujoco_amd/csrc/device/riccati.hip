@@ -40,9 +40,17 @@ __device__ unsigned long long g_bstamp_cnt[16];
 }  // namespace ilqg
 
 #include "riccati.h"
+#include "riccati_mfma.h"
 
 namespace ilqg {
 namespace {
+
+__global__ __launch_bounds__(rmfma::THREADS) void k_backward_mfma(DevModel m, int nq, int nv, int nu, int P, double dt,
+                                                                  double mu, const double* deriv, int Ds, TrajDev tr,
+                                                                  double* Kg, double* kg, double* Vg, double* vg) {
+  extern __shared__ double sh[];
+  rmfma::backward_seed_mfma(m, nq, nv, nu, P, dt, mu, deriv, Ds, tr, Kg, kg, Vg, vg, blockIdx.x, sh);
+}
 
 template <int NV_, int NU_>
 __global__ __launch_bounds__(BW_THREADS) void k_backward(DevModel m, int nq, int nv_rt, int nu_rt, int P, double dt,
@@ -68,6 +76,22 @@ size_t backward_lds_bytes(int nv, int nu) {
   const size_t pre = D <= (size_t)BW_PF * BW_THREADS ? D : 0;
   size_t nd = 4 * nx * LX + 2 * nu * LX + 3 * (size_t)nu * nx + (size_t)nu * nu + 7 * nx + 4 * (size_t)nu + pre;
   return nd * sizeof(double) + (size_t)nu * sizeof(int) + 16;
+}
+
+size_t backward_mfma_lds_bytes(int nv, int nu) { return rmfma::lds_doubles(nv, nu) * sizeof(double); }
+
+hipError_t launch_backward_mfma(const DevModel& m, int S, int P, double mu, const double* deriv, int Ds, TrajDev tr,
+                                double* K, double* k, double* V, double* v, hipStream_t st) {
+  const int D = m.nv * (2 * m.nv + m.nu) + 2 * m.nv + m.nu;
+  if (m.nu > 32 || D > rmfma::MPF * rmfma::THREADS) return hipErrorInvalidValue;
+  const size_t lds = backward_mfma_lds_bytes(m.nv, m.nu);
+  if (lds > 160 * 1024) return hipErrorInvalidValue;
+  hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(k_backward_mfma),
+                                     hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(k_backward_mfma, dim3(S), dim3(rmfma::THREADS), lds, st, m, m.nq, m.nv, m.nu, P,
+                     m.opt_timestep, mu, deriv, Ds, tr, K, k, V, v);
+  return hipGetLastError();
 }
 
 hipError_t launch_backward(const DevModel& m, int S, int P, double mu, const double* deriv, int Ds, TrajDev tr,

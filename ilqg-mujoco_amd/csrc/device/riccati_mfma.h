@@ -1,0 +1,289 @@
+// initV + Riccati backward pass (inc/ilqr.h:100-107,133-176) with the matrix
+// products on the fp64 matrix cores (v_mfma_f64_16x16x4_f64) -- the
+// "MFMA on the Quu/Qux block products where nu x nx is large enough" of the
+// north star, for models whose nx x nx products dominate (humanoid: nx = 54,
+// nu = 21: 1.23 MFLOP per step).
+//
+// One workgroup of four wavefronts per seed; every matrix LDS-resident at an
+// odd leading dimension (the 16 lanes of an MFMA operand fetch walk a row or a
+// column: an odd stride keeps them on distinct banks).  Each product is a set
+// of 16x16 output tiles dealt round-robin to the waves; K advances 4 per
+// instruction; operands outside a matrix read as 0 (no padding in LDS).
+// Stage order and every non-product expression are those of riccati.h
+// (oracle/ilqr_ora.c ora_riccati_step); only the order of the additions inside
+// each matrix product differs (the matrix core's), so K, k, V, v agree with the
+// oracle to rounding, not bit for bit: tests/test_gpu_parity.py states the
+// tolerance (ilqg_solver_set_riccati selects this path; the default stays the
+// bit-exact one).
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include "dphys.h"
+#include "kernels.h"
+
+namespace ilqg {
+namespace rmfma {
+
+constexpr int THREADS = 256;  // four wavefronts
+constexpr int WAVES = THREADS / 64;
+constexpr int MPF = 16;  // record prefetch registers per thread: D <= 4096
+
+typedef double d4 __attribute__((ext_vector_type(4)));
+
+// one 16x16 tile of C = sum_k a(i, k) b(k, j), i in [i0, i0+16), j in [j0, j0+16):
+// lane l supplies a(i0 + l%16, k0 + l/16) and b(k0 + l/16, j0 + l%16); result
+// entry q of lane l is C(i0 + l/16 + 4q, j0 + l%16)
+template <class GA, class GB>
+__device__ __forceinline__ d4 tile(int i0, int j0, int K, const GA& ga, const GB& gb, int lane) {
+  const int r = lane & 15, kq = lane >> 4;
+  d4 acc = {0.0, 0.0, 0.0, 0.0};
+  for (int k0 = 0; k0 < K; k0 += 4) {
+    const double a = ga(i0 + r, k0 + kq);
+    const double b = gb(k0 + kq, j0 + r);
+    acc = __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, acc, 0, 0, 0);
+  }
+  return acc;
+}
+
+// C (rows x cols) = A B over K, tiles dealt to the waves; out(i, j, value) stores
+template <class GA, class GB, class OUT>
+__device__ __forceinline__ void product(int rows, int cols, int K, const GA& ga, const GB& gb, const OUT& out,
+                                        int wave, int lane) {
+  const int mt = (rows + 15) / 16, nt = (cols + 15) / 16;
+  for (int t = wave; t < mt * nt; t += WAVES) {
+    const int i0 = (t % mt) * 16, j0 = (t / mt) * 16;
+    const d4 acc = tile(i0, j0, K, ga, gb, lane);
+    const int j = j0 + (lane & 15);
+#pragma unroll
+    for (int q = 0; q < 4; q++) {
+      const int i = i0 + (lane >> 4) + 4 * q;
+      if (i < rows && j < cols) out(i, j, acc[q]);
+    }
+  }
+}
+
+// LDS (doubles) for (nv, nu): see the layout in backward_seed_mfma
+__host__ __device__ inline size_t lds_doubles(int nv, int nu) {
+  const size_t nx = 2 * (size_t)nv, LX = nx | 1, LU = (size_t)nu | 1;
+  const size_t D = (size_t)nv * (2 * nv + nu) + 2 * nv + nu;
+  const size_t x1 = nx * LU > nu * LX ? nx * LU : nu * LX;
+  return 4 * nx * LX + nu * LX + x1 + nx * LU + (size_t)nu * nu + 7 * nx + 5 * (size_t)nu + D;
+}
+
+// Eigen-style LDLT with symmetric pivoting (oracle ora_ldlt_factor) and its
+// solve: riccati.h ldlt_factor / ldlt_solve (one thread)
+template <class MD>
+__device__ inline void backward_seed_mfma(const MD& m, int nq, int nv, int nu, int P, double dt, double mu,
+                                          const double* deriv, int Ds, TrajDev tr, double* Kg, double* kg,
+                                          double* Vg, double* vg, int s, double* sh) {
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int nx = 2 * nv, D = nv * (2 * nv + nu) + 2 * nv + nu;
+  const int LX = nx | 1, LU = nu | 1;
+  double* V = sh;            // nx x nx (ld LX); V_new from stage 8
+  double* Vs = V + nx * LX;  // symmetrised V + mu I
+  double* A = Vs + nx * LX;  // A; T4 from stage 7
+  double* ABK = A + nx * LX;
+  double* B = ABK + nx * LX;  // nx x nu (ld LX)
+  double* X1 = B + nu * LX;   // T1 (nu x nx, ld LU); T6 (nx x nu, ld LX) from stage 6
+  double* Y1 = X1 + (nx * LU > nu * LX ? nx * LU : nu * LX);  // T3, then K (nu x nx, ld LU)
+  double* Mm = Y1 + nx * LU;  // nu x nu (ld nu): -2 B'VsB - 2R, then its LDLT factor
+  double* v = Mm + nu * nu;
+  double* c = v + nx;
+  double* w = c + nx;
+  double* y = w + nx;
+  double* z = y + nx;
+  double* vn = z + nx;
+  double* q = vn + nx;
+  double* kl = q + nx;
+  double* kR = kl + nu;
+  double* col = kR + nu;
+  double* r = col + nu;
+  double* tmp = r + nu;  // nu: LDLT scratch
+  double* dl = tmp + nu;  // FD record of the current step, D doubles
+  __shared__ int trn[32];
+  double* T4 = A;
+  double* Vn = V;
+
+  // initV at the terminal point dArray[0] (inc/ilqr.h:100-107)
+  {
+    const double* q0 = deriv + ((size_t)s * P) * Ds + 2 * nv * nv + nv * nu;
+    for (int i = tid; i < nx; i += THREADS) v[i] = q0[i];
+    const double* d1 = deriv + ((size_t)s * P + (P > 1 ? 1 : 0)) * Ds;
+    for (int i = tid; i < D; i += THREADS) dl[i] = d1[i];
+    __syncthreads();
+    for (int e = tid; e < nx * nx; e += THREADS) {
+      const int i = e % nx, j = e / nx;
+      V[i + j * LX] = v[i] * v[j];
+    }
+    __syncthreads();
+  }
+  for (int n = 1; n < P; n++) {
+    const size_t pc = (size_t)s * P + n, pp = pc - 1;
+    // next step's FD record, consumed at the end of this step
+    double pf[MPF];
+    if (n + 1 < P) {
+      const double* dn1 = deriv + (pc + 1) * Ds;
+#pragma unroll
+      for (int t = 0; t < MPF; t++) {
+        const int i = tid + t * THREADS;
+        pf[t] = i < D ? dn1[i] : 0.0;
+      }
+    }
+    const double* dn = dl;
+    // stage 1: symmetrise V, assemble A/B (differentiator.h:66-71,89-92), q, r, c
+    for (int e = tid; e < nx * nx; e += THREADS) {
+      const int i = e % nx, j = e / nx;
+      Vs[i + j * LX] = (V[i + j * LX] + V[j + i * LX]) / 2;
+      double val;
+      if (i < nv && j < nv) val = (i == j) ? 1 : 0;
+      else if (i < nv) val = (i == j - nv) ? dt : 0;
+      else if (j < nv) val = dn[(i - nv) + j * nv] * dt;
+      else val = ((i - nv) == (j - nv) ? 1 : 0) + dn[nv * nv + (i - nv) + (j - nv) * nv] * dt;
+      A[i + j * LX] = val;
+    }
+    for (int e = tid; e < nx * nu; e += THREADS) {
+      const int i = e % nx, j = e / nx;
+      B[i + j * LX] = (i < nv) ? 0 : dn[2 * nv * nv + (i - nv) + j * nv] * dt;
+    }
+    for (int i = tid; i < nx; i += THREADS) {
+      q[i] = dn[2 * nv * nv + nv * nu + i];
+      // c = x*_{n-1} (-) x*_n (inc/ilqr.h:154-157; tangent space for quaternion joints)
+      if (i < nv && nq != nv) {
+        c[i] = dev::state_diff_dof(m, i, tr.qpos + pp * nq, tr.qpos + pc * nq);
+      } else {
+        const double xp = i < nv ? tr.qpos[pp * nq + i] : tr.qvel[pp * nv + i - nv];
+        const double xc = i < nv ? tr.qpos[pc * nq + i] : tr.qvel[pc * nv + i - nv];
+        c[i] = xp - xc;
+      }
+    }
+    for (int a = tid; a < nu; a += THREADS) r[a] = dn[2 * nv * nv + nv * nu + nx + a];
+    __syncthreads();
+    for (int i = tid; i < nx; i += THREADS) Vs[i + i * LX] += mu;
+    __syncthreads();
+    // stage 2: T1 = B' Vs (nu x nx)
+    product(
+        nu, nx, nx, [&](int a, int k) { return (a < nu && k < nx) ? B[k + a * LX] : 0.0; },
+        [&](int k, int j) { return (k < nx && j < nx) ? Vs[k + j * LX] : 0.0; },
+        [&](int a, int j, double x) { X1[a + j * LU] = x; }, wave, lane);
+    __syncthreads();
+    // stage 3: Mm = -2 T1 B - 2 R ; T3 = T1 A ; w = v + 2 Vs c
+    auto gT1 = [&](int a, int k) { return (a < nu && k < nx) ? X1[a + k * LU] : 0.0; };
+    product(
+        nu, nu, nx, gT1, [&](int k, int b) { return (k < nx && b < nu) ? B[k + b * LX] : 0.0; },
+        [&](int a, int b, double x) { Mm[a + b * nu] = -2 * x - 2 * (r[a] * r[b]); }, wave, lane);
+    product(
+        nu, nx, nx, gT1, [&](int k, int j) { return (k < nx && j < nx) ? A[k + j * LX] : 0.0; },
+        [&](int a, int j, double x) { Y1[a + j * LU] = x; }, wave, lane);
+    for (int i = tid; i < nx; i += THREADS) {
+      double sm = 0;
+      for (int j = 0; j < nx; j++) sm += Vs[i + j * LX] * c[j];
+      w[i] = v[i] + 2 * sm;
+    }
+    __syncthreads();
+    // stage 4: LDLT of Mm (one thread); col = B'w + r beside it (wave 1)
+    if (tid == 0) ldlt_factor(nu, Mm, trn, tmp);
+    for (int a = tid - 64; a >= 0 && a < nu; a += THREADS) {
+      double sm = 0;
+      for (int kk = 0; kk < nx; kk++) sm += B[kk + a * LX] * w[kk];
+      col[a] = sm + r[a];
+    }
+    __syncthreads();
+    // stage 5: K = ldlt.solve(2 T3) column-parallel (in place), k = ldlt.solve(B'w + r)
+    for (int j = tid; j < nx + 1; j += THREADS) {
+      double* x = j < nx ? Y1 + j * LU : kl;
+      if (j < nx)
+        for (int a = 0; a < nu; a++) x[a] = 2 * x[a];
+      else
+        for (int a = 0; a < nu; a++) x[a] = col[a];
+      ldlt_solve(nu, Mm, trn, x);
+    }
+    __syncthreads();
+    // stage 6: ABK = A + B K ; T6 = K'R ; y = B k + c ; kR = k'R
+    auto gK = [&](int a, int j) { return (a < nu && j < nx) ? Y1[a + j * LU] : 0.0; };
+    product(
+        nx, nx, nu, [&](int i, int a) { return (i < nx && a < nu) ? B[i + a * LX] : 0.0; }, gK,
+        [&](int i, int j, double x) { ABK[i + j * LX] = A[i + j * LX] + x; }, wave, lane);
+    product(
+        nx, nu, nu, [&](int i, int a) { return (i < nx && a < nu) ? Y1[a + i * LU] : 0.0; },
+        [&](int a, int b) { return (a < nu && b < nu) ? r[a] * r[b] : 0.0; },
+        [&](int i, int b, double x) { X1[i + b * LX] = x; }, wave, lane);
+    for (int i = tid; i < nx; i += THREADS) {
+      double sm = 0;
+      for (int a = 0; a < nu; a++) sm += B[i + a * LX] * kl[a];
+      y[i] = sm + c[i];
+    }
+    for (int b = tid; b < nu; b += THREADS) {
+      double sm = 0;
+      for (int a = 0; a < nu; a++) sm += kl[a] * (r[a] * r[b]);
+      kR[b] = sm;
+    }
+    __syncthreads();
+    // stage 7: T4 = ABK' Vs (into A's buffer: A is dead)
+    product(
+        nx, nx, nx, [&](int i, int k) { return (i < nx && k < nx) ? ABK[k + i * LX] : 0.0; },
+        [&](int k, int j) { return (k < nx && j < nx) ? Vs[k + j * LX] : 0.0; },
+        [&](int i, int j, double x) { T4[i + j * LX] = x; }, wave, lane);
+    __syncthreads();
+    // stage 8: V_new = (T4 ABK + q q') + T6 K (into V's buffer: V is dead)
+    {
+      const int mt = (nx + 15) / 16;
+      for (int t = wave; t < mt * mt; t += WAVES) {
+        const int i0 = (t % mt) * 16, j0 = (t / mt) * 16;
+        const d4 a1 = tile(
+            i0, j0, nx, [&](int i, int k) { return (i < nx && k < nx) ? T4[i + k * LX] : 0.0; },
+            [&](int k, int j) { return (k < nx && j < nx) ? ABK[k + j * LX] : 0.0; }, lane);
+        const d4 a2 = tile(
+            i0, j0, nu, [&](int i, int b) { return (i < nx && b < nu) ? X1[i + b * LX] : 0.0; }, gK, lane);
+        const int j = j0 + (lane & 15);
+#pragma unroll
+        for (int qq = 0; qq < 4; qq++) {
+          const int i = i0 + (lane >> 4) + 4 * qq;
+          if (i < nx && j < nx) Vn[i + j * LX] = (a1[qq] + q[i] * q[j]) + a2[qq];
+        }
+      }
+    }
+    __syncthreads();
+    // stage 9: z = (2y)' V_new ; v_new (reads the NEW V, quirk Q14)
+    for (int j = tid; j < nx; j += THREADS) {
+      double sm = 0;
+      for (int i = 0; i < nx; i++) sm += (2 * y[i]) * Vn[i + j * LX];
+      z[j] = sm;
+    }
+    __syncthreads();
+    for (int j = tid; j < nx; j += THREADS) {
+      double ta = 0, tb = 0, td = 0;
+      for (int i = 0; i < nx; i++) {
+        ta += z[i] * ABK[i + j * LX];
+        tb += v[i] * ABK[i + j * LX];
+      }
+      for (int b = 0; b < nu; b++) td += (2 * kR[b]) * Y1[b + j * LU];
+      vn[j] = ((ta + tb) + q[j]) + td;
+    }
+    // gains out (Eigen col-major K[a + j nu])
+    for (int e = tid; e < nu * nx; e += THREADS) {
+      const int a = e % nu, j = e / nu;
+      Kg[pc * nu * nx + e] = Y1[a + j * LU];
+    }
+    for (int a = tid; a < nu; a += THREADS) kg[pc * nu + a] = kl[a];
+    __syncthreads();
+    for (int i = tid; i < nx; i += THREADS) v[i] = vn[i];
+    if (n + 1 < P) {
+#pragma unroll
+      for (int t = 0; t < MPF; t++) {
+        const int i = tid + t * THREADS;
+        if (i < D) dl[i] = pf[t];
+      }
+    }
+    __syncthreads();
+  }
+  if (Vg)
+    for (int e = tid; e < nx * nx; e += THREADS) {
+      const int i = e % nx, j = e / nx;
+      Vg[(size_t)s * nx * nx + e] = V[i + j * LX];
+    }
+  if (vg)
+    for (int i = tid; i < nx; i += THREADS) vg[(size_t)s * nx + i] = v[i];
+}
+
+}  // namespace rmfma
+}  // namespace ilqg

@@ -63,6 +63,7 @@ EXPORTS = [
     "ilqg_solver_stream", "ilqg_solver_device_costs", "ilqg_solver_set_stream", "ilqg_solver_set_timing",
     "ilqg_solver_get_timing",
     "ilqg_solver_debug_set_fault", "ilqg_solver_device_traj", "ilqg_solver_set_groups", "ilqg_solver_get_groups",
+    "ilqg_solver_set_riccati",
 ]
 KERNELS = ("rollout", "select", "fd_centre", "fd_cols", "backward", "fd_backward")
 
@@ -390,6 +391,11 @@ class ILQR:
         rollouts overlap each other's FD sweeps; roll_cus > 0 puts the rollouts on
         that many CUs and the sweeps on the rest.  Bit-identical to ngroups = 1."""
         _check(lib().ilqg_solver_set_groups(self._h, int(ngroups), int(roll_cus)), "set_groups")
+
+    def set_riccati(self, mode: str):
+        """'exact' (bit-identical to the oracle, default) or 'mfma' (matrix-core
+        products, fp64; agrees to rounding): ilqg_solver_set_riccati"""
+        _check(lib().ilqg_solver_set_riccati(self._h, {"exact": 0, "mfma": 1}[mode]), "set_riccati")
 
     def groups(self):
         """(ngroups, roll_cus) in effect"""

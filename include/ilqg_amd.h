@@ -162,6 +162,17 @@ int ilqg_solver_get_timing(ilqg_solver* s, double* ms, int* launches);
    per-seed costs ordered on the solver stream (ilqg_solver_device_costs) and
    the sweeps still running behind it; ilqg_synchronize waits for all of it. */
 int ilqg_solver_set_groups(ilqg_solver* s, int ngroups, int roll_cus);
+/* Riccati recursion (inc/ilqr.h:133-176) engine.  EXACT (default): the
+   oracle's loops, bit-identical K, k, V, v (streamed behind the FD sweep on
+   cooperative models).  MFMA: every matrix product (B'V, Quu = -2B'VB - 2R,
+   Qux = B'VA, A + BK, (A+BK)'V(A+BK), K'RK) on the fp64 matrix cores
+   (v_mfma_f64_16x16x4_f64), four wavefronts per seed -- the north star's
+   "MFMA on the Quu/Qux block products" for large nu x nx (humanoid 21 x 54);
+   results agree with EXACT to rounding (product sums in the matrix core's
+   order).  BASELINE.json configs[4]. */
+#define ILQG_RICCATI_EXACT 0
+#define ILQG_RICCATI_MFMA 1
+int ilqg_solver_set_riccati(ilqg_solver* s, int mode);
 int ilqg_solver_get_groups(ilqg_solver* s, int* ngroups, int* roll_cus);
 /* device pointer to the per-seed selected-candidate cost (nseed doubles), for
    an in-stream collective (RCCL all-gather) without a host round trip */

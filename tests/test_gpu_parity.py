@@ -331,6 +331,92 @@ def test_humanoid_iterate_tangent_space(ia, ora):
     exact(v[0], oa["v"], "v")
 
 
+def _humanoid_cfg5(ia, ora, H, iters, riccati):
+    """BASELINE.json configs[4] state: humanoid qpos0 standing at z = 1.4
+    (humanoid.xml:49-50), qvel = 0, ctrl = 0; the GPU solver and the oracle
+    iterate from it"""
+    m, om = setup(ia, ora, "humanoid", ia.HUMANOID_COST)
+    st = m.reset_state(1)
+    st.qpos[0, 2] = 1.4
+    il = _oracle_ilqr(ora, om, _state_dict(st, 0), H, "ora_cost_desc_fn", iters)
+    g = ia.ILQR(m, st, H, ia.HUMANOID_COST)
+    g.set_riccati(riccati)
+    for _ in range(iters):
+        g.iterate()
+    g.synchronize()
+    return g, il
+
+
+def test_humanoid_cfg5_exact(ia, ora):
+    """cfg 5 (humanoid, H = 200) on the cooperative kernels with the exact
+    Riccati engine: two iterations, every trajectory field, FD record, K, k,
+    V, v bit for bit against the oracle"""
+    g, il = _humanoid_cfg5(ia, ora, 200, 2, "exact")
+    ot, oa, gt = il.traj(), il.arrays(), g.traj()
+    for k in ("qpos", "qvel", "warm", "ctrl"):
+        exact(getattr(gt, k).reshape(ot[k].shape), ot[k], f"traj.{k}")
+    K, k = g.gains()
+    exact(g.deriv()[0], oa["deriv"], "deriv")
+    exact(K[0], oa["K"], "K")
+    exact(k[0], oa["k"], "k")
+    V, v = g.value()
+    exact(V[0], oa["V"], "V")
+    exact(v[0], oa["v"], "v")
+
+
+# MFMA Riccati tolerance: every matrix product sums in the matrix core's order,
+# so each step's K, k, V, v differ from the oracle's by rounding (~1e-16
+# relative), carried through the recursion; after one backward pass over
+# H = 200 steps the gains and value function stay within 1e-9 relative to the
+# largest entry of each array (SURVEY.md §8d asks 1e-12 per isolated step;
+# tests/test_gpu_parity.py::test_riccati_mfma_step checks that)
+MFMA_RTOL = 1e-9
+
+
+def _rel(a, b):
+    a, b = np.asarray(a), np.asarray(b)
+    return float(np.max(np.abs(a - b)) / max(np.max(np.abs(b)), 1e-300))
+
+
+def test_humanoid_cfg5_mfma(ia, ora):
+    """cfg 5 with the MFMA Riccati engine: one iteration (the FD records and
+    the rollout before it are bit-exact; the backward pass runs on the matrix
+    cores): K, k, V, v within MFMA_RTOL of the oracle"""
+    g, il = _humanoid_cfg5(ia, ora, 200, 1, "mfma")
+    oa = il.arrays()
+    exact(g.deriv()[0], oa["deriv"], "deriv")
+    K, k = g.gains()
+    V, v = g.value()
+    errs = {n: _rel(a, b) for n, a, b in (("K", K[0], oa["K"]), ("k", k[0], oa["k"]), ("V", V[0], oa["V"]),
+                                          ("v", v[0], oa["v"]))}
+    print("cfg5 MFMA Riccati max relative deviation:", errs)
+    assert all(e <= MFMA_RTOL for e in errs.values()), errs
+
+
+@pytest.mark.parametrize("fixture", ["riccati_pendulum.npz", "riccati_hopper.npz"])
+def test_riccati_mfma_step(ia, fixture):
+    """SURVEY.md §8d Riccati tolerance (rel <= 1e-12), stage-isolated: the MFMA
+    engine on the committed Riccati fixtures (the oracle's K, k, V, v for
+    seeded FD records and trajectory)"""
+    g = load_golden(fixture)
+    m = ia.Model.load(model_path(str(g["model"])))
+    P = g["deriv"].shape[0]
+    tr = _fixture_traj(ia, g, "traj_")
+    s = ia.ILQR(m, ia.State(tr.time[:1], tr.qpos[:1], tr.qvel[:1], tr.warm[:1], tr.ctrl[:1]), P - 1,
+                ia.HOPPER_COST if str(g["model"]) == "hopper" else ia.PENDULUM_COST)
+    s.set_riccati("mfma")
+    s.set_traj(tr)
+    s.set_deriv(g["deriv"][None])
+    s.riccati_pass()
+    s.synchronize()
+    K, k = s.gains()
+    V, v = s.value()
+    errs = {n: _rel(a, b) for n, a, b in (("K", K[0, 1:], g["K"][1:]), ("k", k[0, 1:], g["k"][1:]),
+                                          ("V", V[0], g["V"]), ("v", v[0], g["v"]))}
+    print(fixture, "MFMA Riccati max relative deviation:", errs)
+    assert all(e <= 1e-12 for e in errs.values()), errs
+
+
 @pytest.mark.parametrize("env", [{"ILQG_FUSED": "0"}, {"ILQG_FD_LAG": "0"}, {"ILQG_FD_LAG": "1"},
                                  {"ILQG_FD_LAG": "7", "ILQG_FD_CV": "1"}, {"ILQG_FD_CV": "6"},
                                  {"ILQG_FD_USPLIT": "0"}, {"ILQG_FD_USPLIT": "0", "ILQG_FD_LAG": "3"},
