@@ -67,3 +67,71 @@ def test_single_rank_exchange_is_local_argmin():
     from seed_shard import CostExchange
     c = torch.tensor([3.0, 1.0, 2.0], dtype=torch.float64)
     assert int(CostExchange(c, 1)().item()) == 1
+
+
+# ---- the exchange driven by real per-seed solver costs (the oracle's iLQR,
+# the product has no CPU path): each rank iterates its own seeds of the bench
+# workload (hopper, cfg-4 perturbations, 3 line-search candidates, H = 15)
+SR, H_SMALL, ALPHAS = 2, 15, (1.0, 0.5, 0.25)
+
+
+def _oracle_seed_costs(seeds):
+    """per seed: the selected candidate's trajectory cost after two line-search
+    iterations and the first control u*_N of the selected trajectory"""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import ilqg_amd as ia
+    import oracle as ora
+    import workloads
+    m = ia.Model.load(workloads.model_file("hopper"))
+    om = ora.OModel(m.blob())
+    om.lib.L.ora_set_cost_desc(ora.CostDesc.from_cost(ia.HOPPER_COST, m.nq, m.nv, m.nu))
+    om.lib.L.ora_set_nthread(1)
+    # workloads.hopper_dmain's state, on the oracle: reset, 500 passive steps,
+    # ctrl -0.1, then the seed's N(0, 0.01^2) perturbation of qpos and qvel
+    base = om.make_data()
+    base.step(500)
+    base.arr("ctrl")[:] -= 0.1
+    st0 = base.state()
+    costs, u0 = [], []
+    for g in seeds:
+        z = workloads.normals(g, m.nq + m.nv)
+        d = om.make_data()
+        d.set_state(time=st0["time"], qpos=st0["qpos"] + 0.01 * z[:m.nq], qvel=st0["qvel"] + 0.01 * z[m.nq:],
+                    warm=st0["warm"], ctrl=st0["ctrl"])
+        il = ora.OILQR(om, d, H_SMALL, cost_fn="ora_cost_desc_fn")
+        il.set_dinit(d)
+        for _ in range(2):
+            c, sel = il.iterate_ls(ALPHAS)
+        costs.append(float(c[sel]))
+        u0.append(il.traj()["ctrl"][H_SMALL].copy())
+    return np.array(costs), np.stack(u0)
+
+
+def _worker_real(rank, port, outdir):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=WORLD)
+    try:
+        from seed_shard import CostExchange, broadcast_winner_control, seed_offset
+        off = seed_offset(rank, SR)
+        costs, u0 = _oracle_seed_costs(range(off, off + SR))
+        ex = CostExchange(torch.tensor(costs, dtype=torch.float64), WORLD)
+        best = int(ex().item())
+        u = broadcast_winner_control(best, torch.tensor(u0), SR, WORLD)
+        np.savez(os.path.join(outdir, f"q{rank}.npz"), best=best, gathered=ex.gather().numpy().copy(),
+                 u=u.numpy().copy())
+    finally:
+        dist.destroy_process_group()
+
+
+def test_exchange_with_solver_costs_gloo(tmp_path):
+    """world size 2: the all-gather of the selected-candidate costs and the
+    winner's first-control broadcast, fed by the oracle's line-search iLQR on
+    each rank's seeds, equal the single-process computation over all seeds"""
+    mp.spawn(_worker_real, args=(_free_port(), str(tmp_path)), nprocs=WORLD, join=True)
+    r = [np.load(tmp_path / f"q{i}.npz") for i in range(WORLD)]
+    allc, allu = _oracle_seed_costs(range(WORLD * SR))
+    best = int(np.argmin(allc))
+    for x in r:
+        assert np.array_equal(x["gathered"], allc)
+        assert int(x["best"]) == best
+        assert np.array_equal(x["u"], allu[best])
