@@ -70,6 +70,76 @@ __device__ inline void ldlt_factor(int n, double* mat, int* transp, double* temp
       for (int i = k + 1; i < n; i++) mat[i + k * n] /= mat[k + k * n];
   }
 }
+// The same factorization by one wavefront (lane = the calling thread's lane,
+// every lane of the wave calls it; n <= 32): each matrix entry receives
+// exactly ldlt_factor's operations in ldlt_factor's order -- the pivot scan,
+// the four swap groups (disjoint entries: one lane each), temp, the dot
+// products of row k and of every row below it (one lane per row, ascending j)
+// and the column scaling -- so the factor is bit-identical; the phases of
+// column k are separated by wavefront-scope barriers.
+__device__ __forceinline__ void wave_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+__device__ inline void ldlt_factor_wave(int n, double* mat, int* transp, double* temp, int lane) {
+  for (int k = 0; k < n; k++) {
+    // pivot: the first row of largest |diagonal| among k..n-1 (strict >, as the oracle)
+    const double dg = (lane >= k && lane < n) ? fabs(mat[lane + lane * n]) : 0.0;
+    int big = k;
+    double bigv = __shfl(dg, k);
+    for (int i = k + 1; i < n; i++) {
+      const double a = __shfl(dg, i);
+      if (a > bigv) {
+        bigv = a;
+        big = i;
+      }
+    }
+    if (lane == 0) transp[k] = big;
+    if (k != big) {
+      const int s = n - big - 1;
+      double t;
+      if (lane < k) {  // row k <-> row big, columns j < k
+        const int j = lane;
+        t = mat[k + j * n]; mat[k + j * n] = mat[big + j * n]; mat[big + j * n] = t;
+      }
+      if (lane < s) {  // rows below big: column k <-> column big
+        const int i = lane;
+        t = mat[(big + 1 + i) + k * n];
+        mat[(big + 1 + i) + k * n] = mat[(big + 1 + i) + big * n];
+        mat[(big + 1 + i) + big * n] = t;
+      }
+      if (lane == 32) {
+        t = mat[k + k * n]; mat[k + k * n] = mat[big + big * n]; mat[big + big * n] = t;
+      }
+      if (lane > 32 + k && lane < 32 + big) {  // between: column k <-> row big
+        const int i = lane - 32;
+        t = mat[i + k * n]; mat[i + k * n] = mat[big + i * n]; mat[big + i * n] = t;
+      }
+    }
+    wave_sync();
+    if (k > 0) {
+      if (lane < k) temp[lane] = mat[lane + lane * n] * mat[k + lane * n];
+      wave_sync();
+      // lane i >= k: row i's dot with temp (row k: the diagonal update)
+      if (lane >= k && lane < n) {
+        double si = 0;
+        for (int j = 0; j < k; j++) si += mat[lane + j * n] * temp[j];
+        mat[lane + k * n] -= si;
+      }
+      wave_sync();
+    }
+    if (k == 0 && !(fabs(mat[0]) > 0)) {
+      for (int j = lane; j < n; j += 64) transp[j] = j;
+      wave_sync();
+      return;
+    }
+    const double d = mat[k + k * n];
+    if (n - k - 1 > 0 && fabs(d) > 0 && lane > k && lane < n) mat[lane + k * n] /= d;
+    wave_sync();
+  }
+}
+
 __device__ inline void ldlt_solve(int n, const double* Lm, const int* transp, double* x) {
   const double tol = 2.2250738585072014e-308;
   for (int k = 0; k < n; k++) { double t = x[k]; x[k] = x[transp[k]]; x[transp[k]] = t; }
@@ -82,6 +152,61 @@ __device__ inline void ldlt_solve(int n, const double* Lm, const int* transp, do
   for (int i = n - 1; i >= 0; i--)
     for (int j = i + 1; j < n; j++) x[i] -= Lm[j + i * n] * x[j];
   for (int k = n - 1; k >= 0; k--) { double t = x[k]; x[k] = x[transp[k]]; x[transp[k]] = t; }
+}
+
+// ldlt_solve with the vector in registers (n <= 32, every index a compile-time
+// constant): the pivot swaps before and after the substitutions are one
+// gather and one scatter through perm (ldlt_perm), and every entry receives
+// ldlt_solve's operations in ldlt_solve's order.  Lm reads are uniform LDS
+// loads independent of x, so they issue ahead of the dependent chain.
+// Each calling lane solves its own vector x (active lanes only).
+// perm[i] = the source position of entry i after ldlt_solve's forward swaps:
+// lane i applies the transpositions to its index, last one first
+__device__ inline void ldlt_perm(int n, const int* transp, int* perm, int lane) {
+  if (lane < n) {
+    int p = lane;
+    for (int k = n - 1; k >= 0; k--) {
+      const int t = transp[k];
+      p = p == k ? t : (p == t ? k : p);
+    }
+    perm[lane] = p;
+  }
+}
+__device__ inline void ldlt_solve_reg(int n, const double* Lm, const int* perm, double* x, bool active) {
+  constexpr int NM = 32;
+  const double tol = 2.2250738585072014e-308;
+  double r[NM];
+  rreg::sf<0, NM>([&](auto ii) __attribute__((always_inline)) {
+    constexpr int i = decltype(ii)::value;
+    r[i] = (active && i < n) ? x[perm[i]] : 0.0;
+  });
+  rreg::sf<0, NM>([&](auto ii) __attribute__((always_inline)) {
+    constexpr int i = decltype(ii)::value;
+    if (i < n)
+      rreg::sf<0, i>([&](auto jj) __attribute__((always_inline)) {
+        constexpr int j = decltype(jj)::value;
+        r[i] -= Lm[i + j * n] * r[j];
+      });
+  });
+  rreg::sf<0, NM>([&](auto ii) __attribute__((always_inline)) {
+    constexpr int i = decltype(ii)::value;
+    if (i < n) {
+      const double d = Lm[i + i * n];
+      r[i] = fabs(d) > tol ? r[i] / d : 0.0;
+    }
+  });
+  rreg::sf<0, NM>([&](auto ii) __attribute__((always_inline)) {
+    constexpr int i = NM - 1 - decltype(ii)::value;
+    if (i < n)
+      rreg::sf<i + 1, NM>([&](auto jj) __attribute__((always_inline)) {
+        constexpr int j = decltype(jj)::value;
+        if (j < n) r[i] -= Lm[j + i * n] * r[j];
+      });
+  });
+  rreg::sf<0, NM>([&](auto ii) __attribute__((always_inline)) {
+    constexpr int i = decltype(ii)::value;
+    if (active && i < n) x[perm[i]] = r[i];
+  });
 }
 
 // Three independent fixed-order dot products per lane (ILP 3): each output
@@ -282,7 +407,7 @@ __device__ inline void backward_seed(const MD& m, int nq, int nv_rt, int nu_rt, 
       w[i] = v[i] + 2 * sm;
     }
     __syncthreads();
-    if (tid == 0) ldlt_factor(nu, Mm, trn, y);  // y is free until stage 5
+    ldlt_factor_wave(nu, Mm, trn, y, tid);  // y is free until stage 5
     for (int a = tid; a < nu; a += BW_THREADS) {
       double sm = 0;
       for (int kk = 0; kk < nx; kk++) sm += B[kk + a * LX] * w[kk];
@@ -291,13 +416,21 @@ __device__ inline void backward_seed(const MD& m, int nq, int nv_rt, int nu_rt, 
     __syncthreads();
     BSTAMP(2);
     // stage 4: K = ldlt.solve(2 T3) column-parallel; k = ldlt.solve(B'w + r), in place in LDS
+    int* perm = trn + nu;
+    ldlt_perm(nu, trn, perm, tid);
     for (int j = tid; j < nx + 1; j += BW_THREADS) {
       double* x = j < nx ? Kl + j * nu : kl;
       if (j < nx)
         for (int a = 0; a < nu; a++) x[a] = 2 * T3[a + j * nu];
       else
         for (int a = 0; a < nu; a++) x[a] = col[a];
-      ldlt_solve(nu, Mm, trn, x);
+    }
+    __syncthreads();
+    if (nu <= 32 && nx + 1 <= BW_THREADS) {
+      const int j = tid;
+      ldlt_solve_reg(nu, Mm, perm, j < nx ? Kl + j * nu : kl, j < nx + 1);
+    } else {
+      for (int j = tid; j < nx + 1; j += BW_THREADS) ldlt_solve(nu, Mm, trn, j < nx ? Kl + j * nu : kl);
     }
     __syncthreads();
     BSTAMP(3);

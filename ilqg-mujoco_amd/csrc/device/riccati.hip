@@ -75,7 +75,7 @@ size_t backward_lds_bytes(int nv, int nu) {
   const size_t D = (size_t)nv * (2 * nv + nu) + 2 * nv + nu;
   const size_t pre = D <= (size_t)BW_PF * BW_THREADS ? D : 0;
   size_t nd = 4 * nx * LX + 2 * nu * LX + 3 * (size_t)nu * nx + (size_t)nu * nu + 7 * nx + 4 * (size_t)nu + pre;
-  return nd * sizeof(double) + (size_t)nu * sizeof(int) + 16;
+  return nd * sizeof(double) + 2 * (size_t)nu * sizeof(int) + 16;  // + transp, perm
 }
 
 size_t backward_mfma_lds_bytes(int nv, int nu) { return rmfma::lds_doubles(nv, nu) * sizeof(double); }

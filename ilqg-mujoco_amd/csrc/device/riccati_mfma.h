@@ -71,7 +71,7 @@ __host__ __device__ inline size_t lds_doubles(int nv, int nu) {
 }
 
 // Eigen-style LDLT with symmetric pivoting (oracle ora_ldlt_factor) and its
-// solve: riccati.h ldlt_factor / ldlt_solve (one thread)
+// solve: riccati.h ldlt_factor_wave (one wavefront) / ldlt_solve (per column)
 template <class MD>
 __device__ inline void backward_seed_mfma(const MD& m, int nq, int nv, int nu, int P, double dt, double mu,
                                           const double* deriv, int Ds, TrajDev tr, double* Kg, double* kg,
@@ -100,7 +100,7 @@ __device__ inline void backward_seed_mfma(const MD& m, int nq, int nv, int nu, i
   double* r = col + nu;
   double* tmp = r + nu;  // nu: LDLT scratch
   double* dl = tmp + nu;  // FD record of the current step, D doubles
-  __shared__ int trn[32];
+  __shared__ int trn[32], perm[32];
   double* T4 = A;
   double* Vn = V;
 
@@ -180,8 +180,8 @@ __device__ inline void backward_seed_mfma(const MD& m, int nq, int nv, int nu, i
       w[i] = v[i] + 2 * sm;
     }
     __syncthreads();
-    // stage 4: LDLT of Mm (one thread); col = B'w + r beside it (wave 1)
-    if (tid == 0) ldlt_factor(nu, Mm, trn, tmp);
+    // stage 4: LDLT of Mm (wave 0); col = B'w + r beside it (wave 1)
+    if (wave == 0) ldlt_factor_wave(nu, Mm, trn, tmp, lane);
     for (int a = tid - 64; a >= 0 && a < nu; a += THREADS) {
       double sm = 0;
       for (int kk = 0; kk < nx; kk++) sm += B[kk + a * LX] * w[kk];
@@ -189,13 +189,20 @@ __device__ inline void backward_seed_mfma(const MD& m, int nq, int nv, int nu, i
     }
     __syncthreads();
     // stage 5: K = ldlt.solve(2 T3) column-parallel (in place), k = ldlt.solve(B'w + r)
-    for (int j = tid; j < nx + 1; j += THREADS) {
+    // (columns dealt over the four waves: one solve per lane, every SIMD busy;
+    // the vector in registers, ldlt_solve_reg)
+    if (wave == 0) ldlt_perm(nu, trn, perm, lane);
+    __syncthreads();
+    for (int j = lane * WAVES + wave; j < nx + 1; j += THREADS) {
       double* x = j < nx ? Y1 + j * LU : kl;
       if (j < nx)
         for (int a = 0; a < nu; a++) x[a] = 2 * x[a];
       else
         for (int a = 0; a < nu; a++) x[a] = col[a];
-      ldlt_solve(nu, Mm, trn, x);
+    }
+    {
+      const int j = lane * WAVES + wave;
+      ldlt_solve_reg(nu, Mm, perm, j < nx ? Y1 + j * LU : kl, j < nx + 1);
     }
     __syncthreads();
     // stage 6: ABK = A + B K ; T6 = K'R ; y = B k + c ; kR = k'R
