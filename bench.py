@@ -130,7 +130,7 @@ def cpu_baseline(budget_s, horizon, threads, nalpha):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--seeds-per-gpu", type=int, default=8)
     ap.add_argument("--alphas", type=int, default=8)
@@ -138,6 +138,10 @@ def main():
     ap.add_argument("--cpu-budget", type=float, default=15.0)
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    # pipelined seed groups (ilqg_solver_set_groups), off by default: G groups,
+    # rollouts on --roll-cus CUs and the FD sweeps on the rest
+    ap.add_argument("--groups", type=int, default=1)
+    ap.add_argument("--roll-cus", type=int, default=128)
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -159,6 +163,8 @@ def main():
     # legacy null stream, which does not order against the solver's own)
     stream = torch.cuda.Stream()
     solver.set_stream(stream.cuda_stream)
+    if args.groups > 1:
+        solver.set_groups(args.groups, args.roll_cus)
     exchange = CostExchange(device_view(solver.device_costs_ptr(), S), world, solver=solver)
 
     def one_step():
@@ -230,7 +236,8 @@ def main():
         "data": "synthetic (cfg-3 hopper state + splitmix64/Box-Muller N(0,0.01^2) seed perturbations)",
         "config": {"workload": f"hopper_H{H}_{S}seeds_x_{A}alphas_per_gpu", "model": "hopper.xml",
                    "horizon": H, "seeds_per_gpu": S, "linesearch_candidates": A, "global_seeds": world * S,
-                   "parallelism": f"seed-sharded x{world} (RCCL all-gather of per-seed costs)"},
+                   "parallelism": f"seed-sharded x{world} (RCCL all-gather of per-seed costs)",
+                   "seed_groups": args.groups},
         "roofline": {"bound": "hbm", "kernel": dom, "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                      "algorithmic_bytes_per_launch": abytes[dom], "avg_launch_ms": dom_avg_ms,
