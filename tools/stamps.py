@@ -12,7 +12,7 @@ NAMES = {0: "kinematics", 1: "com_pos", 2: "trn+crb", 3: "factor_ld(M)", 4: "col
          20: "empty sync", 21: "empty sync 2", 22: " kin: quat chain (lane 0)", 23: " kin: rotations (lanes)",
          24: "A: barrier 1 (wait for B)", 25: "A: barrier 2", 26: "A: barrier 3", 27: "A: barrier 4", 28: "A: barrier 5",
          32: "B: barrier 1 (wait for A kinematics)", 33: "B: collision", 34: "B: barrier 2", 35: "B: make_constraint",
-         36: "B: barrier 3", 37: "B: passive+aref", 38: "B: euler prefactor", 39: "B: barrier 4 (A com vel + RNE)",
+         36: "B: barrier 3", 37: "B: passive+aref / contact rows+aref", 38: "B: euler prefactor / M and M+hD factors", 39: "B: barrier 4 (A com vel + RNE)",
          40: "B: barrier 6 (end of step)", 41: "B: control law + record", 42: "B: factor_ld(M) / limit rows+passive+act",
          43: "B: barrier 5",
          29: "A: barrier 5b (Euler factor)", 30: "B: Newton warm-start prep"}
