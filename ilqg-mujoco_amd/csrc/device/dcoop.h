@@ -2188,36 +2188,39 @@ __device__ inline void factor_m_and_euler(const auto& m, const auto& L, const au
   factor_ld_rows2(nv, X.pmask, T.tid, qM, T.w + L.qLD, T.w + L.qLDinv, qH, qHLD, qHinv);
 }
 
-// step_dual for the split layout (L.split: RNE / com-velocity scratch outside
-// the union) and register-row models.  Work moves to where the helper wave
+// step_dual for the split layout (L.split: RNE / com-velocity / Euler scratch
+// outside the union) and register-row models, on a THREE-wave team (wave 0
+// the dependency chain, waves 1 and 2 helpers).  Work moves to where a helper
 // has slack, without changing any value:
-//   phase 1 (beside the kinematics): control law + record, the limit rows of
-//     make_constraint (qpos only), passive forces, transmission and actuator
-//     forces (ctrl only);
-//   phase 3 (beside crb): contact jacobians and row allocation;
-//   phase 4 (beside com velocities + RNE): the contact rows' jacobians and
-//     parameters, constraint reference accelerations, and the factors of M
-//     and of M + h D in one register-row pass;
-//   phase 5 (beside the acceleration stage): the warm-start half of the
-//     Newton start.
+//   phase 1 (beside the kinematics), wave 1: control law + record, the limit
+//     rows of make_constraint (qpos only), passive forces, transmission and
+//     actuator forces (ctrl only);
+//   phase 2 (beside com_pos), wave 1: collision;
+//   phase 3 (beside crb), wave 1: contact jacobians and row allocation;
+//   phase 4 (beside com velocities + RNE), wave 1: the contact rows'
+//     jacobians and parameters, constraint reference accelerations and the
+//     warm-start half of the Newton start; wave 2: the factors of M and of
+//     M + h D in one register-row pass;
+//   phase 5: the primary's acceleration stage and constraint solve find the
+//     Newton warm start ready.
 __device__ inline void step_dual_split(const auto& m, const auto& L, const auto& C, const auto& X, const Team& T,
                                        int wave, auto&& pre) {
-  const bool A = wave == 0;
+  const bool A = wave == 0, B = wave == 1;
   const bool eul = m.opt_integrator != 1;
   STAMP(-1);
   STAMPB(-1);
   const bool bad = any_bad(T, C, T.w + L.qpos, m.nq) || any_bad(T, C, T.w + L.qvel, m.nv);
   if (bad) {
-    if (!A) pre();
+    if (B) pre();
     __syncthreads();
     if (A) reset_data(m, L, T);
-    __syncthreads();  // the helper's phase-1 work reads the reset state
+    __syncthreads();  // the helpers' phase-1 work reads the reset state
   }
   int nlim = 0;
   if (A) {
     kinematics(m, L, C, T);
     STAMP(0);
-  } else {
+  } else if (B) {
     if (!bad) pre();
     STAMPB(41);
     nlim = limit_rows_pre(m, L, C, T);
@@ -2233,7 +2236,7 @@ __device__ inline void step_dual_split(const auto& m, const auto& L, const auto&
   if (A) {
     com_pos(m, L, T);
     STAMP(1);
-  } else {
+  } else if (B) {
     collision(m, L, C, X, T);
     STAMPB(33);
   }
@@ -2244,7 +2247,7 @@ __device__ inline void step_dual_split(const auto& m, const auto& L, const auto&
   if (A) {
     crb(m, L, C, X, T);
     STAMP(2);
-  } else {
+  } else if (B) {
     mc_contact_jac(m, L, X, T);
     TSYNC();
     const bool par = mc_alloc(m, L, C, T);
@@ -2260,10 +2263,12 @@ __device__ inline void step_dual_split(const auto& m, const auto& L, const auto&
   __syncthreads();
   STAMP(26);
   STAMPB(36);
+  const int ne5 = T.iw[L.nefc];
+  const bool spec = ne5 > 0 && ne5 <= TEAM_SIZE && m.nv <= RMAX;
   if (A) {
     fwd_velocity(m, L, C, T, 1);
     STAMP(6);
-  } else {
+  } else if (B) {
     if (!rows_done) {
       mc_rows(m, L, C, T, nlim, T.iw[L.nefc]);
       TSYNC();
@@ -2271,14 +2276,14 @@ __device__ inline void step_dual_split(const auto& m, const auto& L, const auto&
     constraint_ref(m, L, T);
     TSYNC();
     STAMPB(37);
+    if (spec) newton_warm_prep(m, L, C, T);
+    STAMPB(30);
+  } else {
     factor_m_and_euler(m, L, C, X, T, eul);
-    STAMPB(38);
   }
   __syncthreads();
   STAMP(27);
   STAMPB(39);
-  const int ne5 = T.iw[L.nefc];
-  const bool spec = ne5 > 0 && ne5 <= TEAM_SIZE && m.nv <= RMAX;
   if (A) {
     fwd_acceleration(m, L, X, T, true);
     STAMP(7);
@@ -2290,9 +2295,8 @@ __device__ inline void step_dual_split(const auto& m, const auto& L, const auto&
     }
     STAMP(8);
   } else {
-    if (spec) newton_warm_prep(m, L, C, T);
-    STAMPB(30);
-    __syncthreads();
+    __syncthreads();  // the primary's barrier inside its Newton start
+    STAMPB(38);
   }
   __syncthreads();
   STAMP(29);

@@ -106,6 +106,7 @@ constexpr WsLayout make_layout(const M& m, int npair = -1, bool split = false) {
     L.split = 1;
     L.s_rne = take(12 * nb);
     L.s_con = take(10 * nv);
+    L.s_euler = take(2 * nv + 2 * nv * nv);  // factored beside the contact rows' reads
   }
   if (coop) {
     const int u = o;
@@ -122,7 +123,9 @@ constexpr WsLayout make_layout(const M& m, int npair = -1, bool split = false) {
       L.s_con = b; b += 10 * nv;
     }
     L.s_newton = b; b += 4 * nv + nv * nv + 2 * ne;
-    L.s_euler = b; b += 2 * nv + 2 * nv * nv;
+    if (!split) {
+      L.s_euler = b; b += 2 * nv + 2 * nv * nv;
+    }
     L.efc_b = b; b += ne;
     L.efc_vel = b; b += ne;
     // reference accelerations (velocity stage) and forces (constraint solve):

@@ -55,7 +55,7 @@ __device__ inline void rollout_body(const auto& m, const auto& L, const auto& C,
   const int ob = out_is_cand ? lane : s;
   // the wave that runs the control law and writes the record: the helper wave
   // of a two-wave team (beside the primary's kinematics), else the only wave
-  const bool ctl = wave != 0;
+  const bool ctl = wave < 0 || wave == 1;
   double c = 0;
   // control law u = u* + alpha k + K (x - x*) for point n, its record and cost
   // (ilqr.h:116-133); the next point's nominal record is prefetched first
@@ -162,8 +162,12 @@ __global__ __launch_bounds__(2 * TEAM) void k_rollout2_coop(DevModel mg, WsLayou
   rollout_body(m, L, C, X, T, S, A, P, nom, out, out_is_cand, K, k, alphas, dinit, qfrc_applied, xfrc_applied,
                passive, cost, cost_cand, (int)(threadIdx.x / TEAM), std::false_type{});
 }
+// three-wave teams for the compile-time register-row models (step_dual_split),
+// two-wave otherwise
+template <class SM>
+constexpr int rollout_waves() { return SM::nv <= RMAX ? 3 : 2; }
 template <class SM, class SX>
-__global__ __launch_bounds__(2 * TEAM) void k_rollout2_s(DevModel mg, int S, int A, int P, TrajDev nom, TrajDev out, int out_is_cand, const double* K, const double* k, const double* alphas, TrajDev dinit, const double* qfrc_applied, const double* xfrc_applied, int passive, CostDev cost, double* cost_cand) {
+__global__ __launch_bounds__(3 * TEAM) void k_rollout2_s(DevModel mg, int S, int A, int P, TrajDev nom, TrajDev out, int out_is_cand, const double* K, const double* k, const double* alphas, TrajDev dinit, const double* qfrc_applied, const double* xfrc_applied, int passive, CostDev cost, double* cost_cand) {
   static constexpr WsLayout L = make_layout(SM{}, SX::npair, true);
   static constexpr CoopLayout C = make_coop_layout(SM{}, SX::npair);
   static constexpr SX X{};
@@ -321,7 +325,8 @@ hipError_t launch_rollout_coop(const DevModel& m, const WsLayout& L, const CoopL
     const size_t lds2 = rollout_lds(coop_lds_bytes(make_layout(stat::SMT{}, stat::SXT::npair, true), C));       \
     e = allow_lds(k_rollout2_s<stat::SMT, stat::SXT>, lds2);                                                    \
     if (e != hipSuccess) return e;                                                                              \
-    hipLaunchKernelGGL((k_rollout2_s<stat::SMT, stat::SXT>), dim3(S * A), dim3(2 * TEAM), lds2, st, m, S, A, P,  \
+    hipLaunchKernelGGL((k_rollout2_s<stat::SMT, stat::SXT>), dim3(S * A),                                       \
+                       dim3(rollout_waves<stat::SMT>() * TEAM), lds2, st, m, S, A, P,                            \
                        nominal, out, out_is_cand, K, k, alphas, dinit, qfrc_applied, xfrc_applied, passive, cost, \
                        cost_cand);                                                                              \
     return hipGetLastError();                                                                                   \
