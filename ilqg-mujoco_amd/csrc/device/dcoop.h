@@ -264,9 +264,10 @@ struct KinPlan {
   }
 };
 
-template <class M>
+template <class M, class F>
 __device__ inline void kin_chain_par(const M& m, const Team& T, const double* qpos, const double* qloc, double* xpos,
-                                     double* xquat, double* xanchor, double* xaxis, double* scratch) {
+                                     double* xquat, double* xanchor, double* xaxis, double* scratch,
+                                     F&& after_quats) {
   static constexpr KinPlan<M> P{};
   constexpr int NB = M::nbody;
   double* QS = scratch;                 // parked quaternions, 4 per slot
@@ -307,6 +308,7 @@ __device__ inline void kin_chain_par(const M& m, const Team& T, const double* qp
     xquat[1] = xquat[2] = xquat[3] = 0;
   }
   team_sync();
+  after_quats();  // every body quaternion is final
   STAMP(22);
   // 2. every rotation on a lane of its own
   if (T.tid < P.nrot) {
@@ -411,7 +413,7 @@ __device__ inline void kinematics(const auto& m, const auto& L, const auto& C, c
     static constexpr KinPlan<MT> plan{};
     // the split chain needs its scratch in the union (dead until collision) and a lane per rotation
     if constexpr (plan.ok && 4 * plan.nslot + 3 * plan.nrot <= 12 * MT::nbody + 10 * MT::nv && KIN_SPLIT)
-      kin_chain_par(m, T, qpos, qloc, xpos, xquat, xanchor, xaxis, T.w + L.con);
+      kin_chain_par(m, T, qpos, qloc, xpos, xquat, xanchor, xaxis, T.w + L.con, []() {});
     else if (T.tid == 0)
       kin_chain_static(m, qpos, qloc, xpos, xquat, xanchor, xaxis);
   } else if (T.tid == 0) {
@@ -507,6 +509,135 @@ __device__ inline void kinematics(const auto& m, const auto& L, const auto& C, c
     for (int k = 0; k < 9; k++) gxmat[9 * g + k] = mat[k];
   }
   TSYNC();
+}
+
+// the compile-time models whose kinematics() takes the split chain (kin_chain_par)
+template <class MT>
+constexpr bool kin_split_ok() {
+  if constexpr (StaticModel<MT>) {
+    constexpr KinPlan<MT> p{};
+    return p.ok && 4 * p.nslot + 3 * p.nrot <= 12 * MT::nbody + 10 * MT::nv && KIN_SPLIT;
+  } else {
+    return false;
+  }
+}
+
+// Hand-off between two waves of a team through an LDS word, without the third
+// wave (unlike __syncthreads): the signaller's earlier LDS stores are ordered
+// before the flag (workgroup release), the waiter's later loads after it
+// (acquire).  Flags carry an increasing step id; the wait is bounded.
+__device__ inline void wave_signal(int* f, int v) {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+  if ((threadIdx.x & (TEAM_SIZE - 1)) == 0) __hip_atomic_store(f, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+__device__ inline void wave_wait(const int* f, int v) {
+  for (int it = 0; it < (1 << 22); it++) {
+    if (__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) >= v) break;
+    __builtin_amdgcn_s_sleep(1);
+  }
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+}
+
+// kinematics() of a compile-time model on two waves (three-wave rollout):
+// the primary computes the joint rotations and walks the quaternion chain,
+// signals, then walks the positions; the helper waits for the quaternions
+// and computes every frame rotation -- xmat, ximat, gxmat are functions of the
+// quaternions alone -- which the primary's xipos / geom positions then read.
+// Each value is the expression kinematics() evaluates, on another wave.
+__device__ inline void kinematics_primary(const auto& m, const auto& L, const auto& C, const Team& T, int* fq,
+                                          const int* ff, int sid) {
+  double* qpos = T.w + L.qpos;
+  double* xpos = T.w + L.xpos;
+  double* xquat = T.w + L.xquat;
+  double* xmat = T.w + L.xmat;
+  double* xipos = T.w + L.xipos;
+  double* xanchor = T.w + L.xanchor;
+  double* xaxis = T.w + L.xaxis;
+  double* qloc = T.c + C.qloc;
+  FOR_T(j, m.njnt) {
+    int type = m.jnt_type[j], qadr = m.jnt_qposadr[j];
+    double q[4], ja[3];
+    if (type == JNT_HINGE) {
+      ldm<3>(ja, m.jnt_axis + 3 * j);
+      axis_angle2quat(q, ja, qpos[qadr] - m.qpos0[qadr]);
+      for (int k = 0; k < 4; k++) qloc[4 * j + k] = q[k];
+    } else if (type == JNT_BALL) {
+      q[0] = qpos[qadr]; q[1] = qpos[qadr + 1]; q[2] = qpos[qadr + 2]; q[3] = qpos[qadr + 3];
+      normalize4(q);
+      for (int k = 0; k < 4; k++) qloc[4 * j + k] = q[k];
+    }
+  }
+  TSYNC();
+  STAMP(11);
+  kin_chain_par(m, T, qpos, qloc, xpos, xquat, xanchor, xaxis, T.w + L.con, [&]() { wave_signal(fq, sid); });
+  TSYNC();
+  STAMP(12);
+  wave_wait(ff, sid);
+  // body inertial positions and geom positions (body frame rotations from the helper)
+  double* gxpos = T.w + L.gxpos;
+  FOR_T(e, m.nbody + m.ngeom) {
+    if (e < m.nbody) {
+      const int i = e;
+      if (i == 0) {
+        xipos[0] = xipos[1] = xipos[2] = 0;
+      } else {
+        double mat[9], tmp[3], ip[3];
+        ldm<9>(mat, xmat + 9 * i);
+        ldm<3>(ip, m.body_ipos + 3 * i);
+        rot_vec_mat(tmp, ip, mat);
+        xipos[3 * i] = tmp[0] + xpos[3 * i];
+        xipos[3 * i + 1] = tmp[1] + xpos[3 * i + 1];
+        xipos[3 * i + 2] = tmp[2] + xpos[3 * i + 2];
+      }
+    } else {
+      const int g = e - m.nbody;
+      const int b = m.geom_bodyid[g];
+      double bm[9], gp[3], tmp[3];
+      ldm<9>(bm, xmat + 9 * b);
+      ldm<3>(gp, m.geom_pos + 3 * g);
+      rot_vec_mat(tmp, gp, bm);
+      gxpos[3 * g] = tmp[0] + xpos[3 * b];
+      gxpos[3 * g + 1] = tmp[1] + xpos[3 * b + 1];
+      gxpos[3 * g + 2] = tmp[2] + xpos[3 * b + 2];
+    }
+  }
+  TSYNC();
+}
+__device__ inline void kinematics_frames(const auto& m, const auto& L, const Team& T, const int* fq, int* ff,
+                                         int sid) {
+  double* xquat = T.w + L.xquat;
+  double* xmat = T.w + L.xmat;
+  double* ximat = T.w + L.ximat;
+  double* gxmat = T.w + L.gxmat;
+  wave_wait(fq, sid);
+  FOR_T(e, m.nbody + m.ngeom) {
+    if (e < m.nbody) {
+      const int i = e;
+      double xq[4], mat[9], iq[4], q2[4];
+      ldm<4>(xq, xquat + 4 * i);
+      quat2mat(mat, xq);
+      for (int k = 0; k < 9; k++) xmat[9 * i + k] = mat[k];
+      if (i == 0) {
+        for (int k = 0; k < 9; k++) ximat[k] = mat[k];
+      } else {
+        ldm<4>(iq, m.body_iquat + 4 * i);
+        quat_mul(q2, xq, iq);
+        quat2mat(mat, q2);
+        for (int k = 0; k < 9; k++) ximat[9 * i + k] = mat[k];
+      }
+    } else {
+      const int g = e - m.nbody;
+      const int b = m.geom_bodyid[g];
+      double bq[4], gq[4], q[4], mat[9];
+      ldm<4>(bq, xquat + 4 * b);
+      ldm<4>(gq, m.geom_quat + 4 * g);
+      quat_mul(q, bq, gq);
+      quat2mat(mat, q);
+      for (int k = 0; k < 9; k++) gxmat[9 * g + k] = mat[k];
+    }
+  }
+  TSYNC();
+  wave_signal(ff, sid);
 }
 
 __device__ inline void com_pos(const auto& m, const auto& L, const Team& T) {
@@ -2204,8 +2335,10 @@ __device__ inline void factor_m_and_euler(const auto& m, const auto& L, const au
 //   phase 5: the primary's acceleration stage and constraint solve find the
 //     Newton warm start ready.
 __device__ inline void step_dual_split(const auto& m, const auto& L, const auto& C, const auto& X, const Team& T,
-                                       int wave, auto&& pre) {
+                                       int wave, int sid, auto&& pre) {
   const bool A = wave == 0, B = wave == 1;
+  int* fq = T.ci + C.ibc + 6;  // quaternions final (primary -> frames helper)
+  int* ff = T.ci + C.ibc + 7;  // frame rotations final (helper -> primary)
   const bool eul = m.opt_integrator != 1;
   STAMP(-1);
   STAMPB(-1);
@@ -2216,21 +2349,28 @@ __device__ inline void step_dual_split(const auto& m, const auto& L, const auto&
     if (A) reset_data(m, L, T);
     __syncthreads();  // the helpers' phase-1 work reads the reset state
   }
-  int nlim = 0;
+  int* nlim_sh = T.ci + C.ibc + 5;  // the limit rows' count, from wave 2 to wave 1
+  constexpr bool ksplit = kin_split_ok<std::remove_cvref_t<decltype(m)>>();
   if (A) {
-    kinematics(m, L, C, T);
+    if constexpr (ksplit) kinematics_primary(m, L, C, T, fq, ff, sid);
+    else kinematics(m, L, C, T);
     STAMP(0);
-  } else if (B) {
+  } else if (!B) {
+    // wave 2: the qpos/qvel-only rows and forces, then the frame rotations
+    const int nl = limit_rows_pre(m, L, C, T);
+    if (T.tid == 0) *nlim_sh = nl;
+    passive_forces(m, L, T);
+    if constexpr (ksplit) kinematics_frames(m, L, T, fq, ff, sid);
+  } else {
     if (!bad) pre();
     STAMPB(41);
-    nlim = limit_rows_pre(m, L, C, T);
-    passive_forces(m, L, T);
     transmission(m, L, T);
     TSYNC();
     actuator_force(m, L, T);
     STAMPB(42);
   }
   __syncthreads();
+  const int nlim = *nlim_sh;
   STAMP(24);
   STAMPB(32);
   if (A) {

@@ -107,7 +107,11 @@ __device__ inline void rollout_body(const auto& m, const auto& L, const auto& C,
       TSYNC();
     }
   };
-  if (wave >= 0) __syncthreads();
+  if (wave >= 0) {
+    // the step ids of the two-wave hand-off flags (step_dual_split) start above 0
+    if (threadIdx.x == 0) T.ci[C.ibc + 6] = T.ci[C.ibc + 7] = 0;
+    __syncthreads();
+  }
   for (int n = P - 1; n >= 0; n--) {
     if (wave < 0) {
       pre_step(n);
@@ -119,7 +123,7 @@ __device__ inline void rollout_body(const auto& m, const auto& L, const auto& C,
         park(n);
       };
       // split layout (compile-time models): the rebalanced two-wave schedule
-      if constexpr (decltype(split)::value) step_dual_split(m, L, C, X, T, wave, pre);
+      if constexpr (decltype(split)::value) step_dual_split(m, L, C, X, T, wave, P - n, pre);
       else step_dual(m, L, C, X, T, wave, pre);
     }
   }
