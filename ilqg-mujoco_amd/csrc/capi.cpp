@@ -978,6 +978,24 @@ int ilqg_solver_device_traj(ilqg_solver* s, int field, double** dptr) {
   return ILQG_OK;
 }
 
+int ilqg_selftest_div(const double* a, const double* b, double* q, double* q2, int n) {
+  if (!a || !b || !q || n < 0 || n > (1 << 24)) return fail(ILQG_ERR_ARG, "bad argument");
+  if (!n) return ILQG_OK;
+  const size_t bytes = (size_t)n * 8;
+  DevBuf da, db, dq, dq2;
+  HIPCHK(da.alloc(bytes));
+  HIPCHK(db.alloc(bytes));
+  HIPCHK(dq.alloc(bytes));
+  if (q2) HIPCHK(dq2.alloc(bytes));
+  HIPCHK(hipMemcpy(da.p, a, bytes, hipMemcpyHostToDevice));
+  HIPCHK(hipMemcpy(db.p, b, bytes, hipMemcpyHostToDevice));
+  HIPCHK(launch_selftest_div((const double*)da.p, (const double*)db.p, (double*)dq.p, (double*)dq2.p, n, nullptr));
+  HIPCHK(hipDeviceSynchronize());
+  HIPCHK(hipMemcpy(q, dq.p, bytes, hipMemcpyDeviceToHost));
+  if (q2) HIPCHK(hipMemcpy(q2, dq2.p, bytes, hipMemcpyDeviceToHost));
+  return ILQG_OK;
+}
+
 int ilqg_solver_debug_set_fault(ilqg_solver* s, unsigned value) {
   if (!s) return fail(ILQG_ERR_ARG, "null solver");
   HIPCHK(s->sync_all());

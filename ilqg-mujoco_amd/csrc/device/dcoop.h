@@ -1963,7 +1963,7 @@ __device__ inline void fwd_constraint_fast(const auto& m, const auto& L, const a
         // alone, so it is summed again only when the set changes
         unsigned long long pmask = 0;
         bool have = false;
-        double d2c = 0;
+        double d2c = 0, rd2 = 0;
         const double c2 = Di * jv * jv;
         auto eval = [&](double a) {
           const double x = jr + a * jv;
@@ -1973,6 +1973,7 @@ __device__ inline void fwd_constraint_fast(const auto& m, const auto& L, const a
           d1 = lane_sum_mask(g1 + g2 * a, c1, am);
           if (!have || am != pmask) {
             d2c = lane_sum_mask(g2, c2, am);
+            rd2 = rcp_ref(d2c);  // d1 / d2 below: the divisor's part, once per active set
             pmask = am;
             have = true;
           }
@@ -1982,7 +1983,7 @@ __device__ inline void fwd_constraint_fast(const auto& m, const auto& L, const a
         if (!(d1 >= 0)) {
           double gtol = LS_TOL * fabs(d1);
           for (int it = 0; it < LS_ITER; it++) {
-            double anew = alpha - d1 / d2;
+            double anew = alpha - div_ref_lane<0>(d1, d2, rd2);
             if (hi >= 0 && !(anew > lo && anew < hi)) anew = 0.5 * (lo + hi);
             alpha = anew;
             eval(alpha);

@@ -59,6 +59,57 @@ __device__ __forceinline__ double bcast(double x, int lane) {
   return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
 }
 
+// ---- fp64 division with the divisor's refined reciprocal computed early ----
+// The compiler's f64 division is ten dependent operations: v_div_scale of the
+// divisor, v_rcp, four fma refining that reciprocal, v_div_scale of the
+// dividend, mul, fma, v_div_fmas, v_div_fixup.  The reciprocal part reads only
+// the (scaled) divisor.  When the divisor is known before the dividend (a
+// Cholesky diagonal, the line search's curvature), rcp_ref() runs that part
+// once, off the critical path, and div_ref() runs the rest of the same
+// sequence on the same operands: the same IEEE quotient, bit for bit.
+// v_div_scale leaves the divisor unscaled except at extreme exponents
+// (|a| >= 2^768 |b|, denormal b or 1/b) and for a == 0, NaN or Inf; there the
+// precomputed reciprocal is not the sequence's, and the ordinary division runs.
+__device__ __forceinline__ double rcp_ref(double b) {
+  double r = __builtin_amdgcn_rcp(b);
+  double t = __builtin_fma(-b, r, 1.0);
+  r = __builtin_fma(r, t, r);
+  t = __builtin_fma(-b, r, 1.0);
+  return __builtin_fma(r, t, r);
+}
+// the quotient's tail; `den_ok` is false where the divisor would be scaled
+__device__ __forceinline__ double div_tail(double a, double b, double r, bool& den_ok) {
+  bool fd, fn;
+  const double ds = __builtin_amdgcn_div_scale(a, b, false, &fd);
+  const double ns = __builtin_amdgcn_div_scale(a, b, true, &fn);
+  den_ok = __builtin_bit_cast(long long, ds) == __builtin_bit_cast(long long, b);
+  const double q = ns * r;
+  const double e = __builtin_fma(-b, q, ns);
+  return __builtin_amdgcn_div_fixup(__builtin_amdgcn_div_fmas(e, r, q, fn), b, a);
+}
+// the ordinary division, kept behind its branch: the empty volatile asm stops
+// the compiler from speculating it (and its ten-operation chain) beside the tail
+__device__ __forceinline__ double div_slow(double a, double b) {
+  asm volatile("" : "+v"(a));
+  return a / b;
+}
+// a / b on every lane (r = rcp_ref(b))
+__device__ __forceinline__ double div_ref(double a, double b, double r) {
+  bool ok;
+  double q = div_tail(a, b, r, ok);
+  if (__builtin_expect(!ok, 0)) q = div_slow(a, b);
+  return q;
+}
+// a / b where only lane k's quotient is used (the other lanes' operands may
+// be anything): the fallback is taken only when lane k needs it (uniform)
+template <int K>
+__device__ __forceinline__ double div_ref_lane(double a, double b, double r) {
+  bool ok;
+  double q = div_tail(a, b, r, ok);
+  if (__builtin_expect((__ballot(!ok) >> K) & 1, 0)) q = div_slow(a, b);
+  return q;
+}
+
 // r[idx] for a per-lane index: select chain over constant indices (written
 // with sfor so SROA sees constant subscripts and keeps r in registers)
 __device__ __forceinline__ double rsel(const double (&r)[RMAX], int idx) {
@@ -283,42 +334,44 @@ __device__ inline void chol_solve_rows(int nv, int tid, const double* H, const d
   });
   if (own) g = grad[tid];
   const double dg = own ? rsel(row, tid) : 1.0;
-  // forward: s[i] = (s[i] - sum_{j<i} H[i][j] s[j]) / H[i][i]
-  double sf[RMAX];
+  const double rg = rcp_ref(dg);
+  // forward: s[i] = (s[i] - sum_{j<i} H[i][j] s[j]) / H[i][i].  Every lane
+  // accumulates its dot product as the s[j] arrive (ascending j, from +0: the
+  // oracle's dotn), so step i is one subtraction and the division's tail; no
+  // lane-divergent branches
+  double sf[RMAX], acc = 0, gf = 0;
   sfor<0, RMAX>(SLAM(ii) {
     constexpr int i = SK(ii);
     if (i >= nv) {
       sf[i] = 0;
       return;
     }
-    if (tid == i) {
-      if (i) {
-        double s = 0;
-        sfor<0, i>(SLAM(jj) { s += row[SK(jj)] * sf[SK(jj)]; });
-        g -= s;
-      }
-      g /= dg;
-    }
-    sf[i] = bcast(g, i);
+    const double q = div_ref_lane<i>(i ? g - acc : g, dg, rg);
+    sf[i] = bcast(q, i);
+    acc += row[i] * sf[i];
+    gf = tid == i ? sf[i] : gf;
   });
-  // backward: s[i] -= H[j][i] s[j] for j = i+1.. ascending, then / H[i][i]
-  double sb[RMAX];
+  g = gf;
+  // backward: s[i] -= H[j][i] s[j] for j = i+1.. ascending, then / H[i][i];
+  // the products are formed as the s[j] arrive
+  double sb[RMAX], pr[RMAX];
   sfor<0, RMAX>(SLAM(ii) {
     constexpr int i = RMAX - 1 - SK(ii);
     if (i >= nv) {
       sb[i] = 0;
+      pr[i] = 0;
       return;
     }
-    if (tid == i) {
-      sfor<i + 1, RMAX>(SLAM(jj) {
-        constexpr int j = SK(jj);
-        if (j < nv) g -= col[j] * sb[j];
-      });
-      g /= dg;
-    }
-    sb[i] = bcast(g, i);
+    double t = g;
+    sfor<i + 1, RMAX>(SLAM(jj) {
+      constexpr int j = SK(jj);
+      if (j < nv) t -= pr[j];
+    });
+    sb[i] = bcast(div_ref_lane<i>(t, dg, rg), i);
+    pr[i] = col[i] * sb[i];
+    gf = tid == i ? sb[i] : gf;
   });
-  if (own) search[tid] = -g;
+  if (own) search[tid] = -gf;
   team_sync();
 }
 

@@ -22,6 +22,7 @@ struct CostDev {
 };
 
 // candidate selection + setDInit(dArray[N])
+hipError_t launch_selftest_div(const double* a, const double* b, double* q, double* q2, int n, hipStream_t st);
 hipError_t launch_select(const DevModel& m, int S, int A, int P, int mode, int copy_cand, const double* cost_cand,
                          int* sel, double* cost_sel, TrajDev cand, TrajDev nominal, TrajDev dinit, hipStream_t st);
 // Riccati backward pass, one workgroup per seed

@@ -41,6 +41,7 @@ __device__ unsigned long long g_bstamp_cnt[16];
 
 #include "riccati.h"
 #include "riccati_mfma.h"
+#include "dsmall.h"
 
 namespace ilqg {
 namespace {
@@ -109,6 +110,29 @@ hipError_t launch_backward(const DevModel& m, int S, int P, double mu, const dou
   if (m.nv == 6 && m.nu == 3) launch_t<6, 3>(m, S, P, mu, deriv, Ds, tr, K, k, V, v, lds, st);
   else if (m.nv == 2 && m.nu == 1) launch_t<2, 1>(m, S, P, mu, deriv, Ds, tr, K, k, V, v, lds, st);
   else launch_t<0, 0>(m, S, P, mu, deriv, Ds, tr, K, k, V, v, lds, st);
+  return hipGetLastError();
+}
+
+// ilqg_selftest_div: the split division (dsmall.h) against nothing but the
+// host's IEEE quotient -- every-lane form into q, one-lane form into q2
+__global__ void k_selftest_div(const double* a, const double* b, double* q, double* q2, int n) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  const int lane = threadIdx.x & 63;
+  const double x = i < n ? a[i] : 1.0, y = i < n ? b[i] : 1.0;
+  const double r = coop::rcp_ref(y);
+  const double v = coop::div_ref(x, y, r);
+  double w = 0;
+  coop::sfor<0, 64>(SLAM(kk) {
+    const double t = coop::div_ref_lane<SK(kk)>(x, y, r);
+    if (lane == SK(kk)) w = t;
+  });
+  if (i < n) {
+    q[i] = v;
+    if (q2) q2[i] = w;
+  }
+}
+hipError_t launch_selftest_div(const double* a, const double* b, double* q, double* q2, int n, hipStream_t st) {
+  hipLaunchKernelGGL(k_selftest_div, dim3((n + 255) / 256), dim3(256), 0, st, a, b, q, q2, n);
   return hipGetLastError();
 }
 

@@ -63,7 +63,7 @@ EXPORTS = [
     "ilqg_solver_stream", "ilqg_solver_device_costs", "ilqg_solver_set_stream", "ilqg_solver_set_timing",
     "ilqg_solver_get_timing",
     "ilqg_solver_debug_set_fault", "ilqg_solver_device_traj", "ilqg_solver_set_groups", "ilqg_solver_get_groups",
-    "ilqg_solver_set_riccati",
+    "ilqg_solver_set_riccati", "ilqg_selftest_div",
 ]
 KERNELS = ("rollout", "select", "fd_centre", "fd_cols", "backward", "fd_backward")
 
@@ -109,6 +109,18 @@ def device_count() -> int:
     n = ctypes.c_int(0)
     rc = lib().ilqg_device_count(ctypes.byref(n))
     return n.value if rc == 0 else 0
+
+
+def selftest_div(a, b):
+    """a / b through the device's split fp64 division (ilqg_selftest_div):
+    returns (every-lane form, one-lane form)."""
+    a = _f64(a).ravel()
+    b = _f64(b).ravel()
+    assert a.shape == b.shape
+    q = np.empty_like(a)
+    q2 = np.empty_like(a)
+    _check(lib().ilqg_selftest_div(_ptr(a), _ptr(b), _ptr(q), _ptr(q2), ctypes.c_int(a.size)), "ilqg_selftest_div")
+    return q, q2
 
 
 @dataclass

@@ -182,6 +182,12 @@ int ilqg_solver_device_costs(ilqg_solver* s, double** dptr);
    applied control): the multi-GPU MPC broadcast of the winning seed's first
    control reads it in place */
 int ilqg_solver_device_traj(ilqg_solver* s, int field, double** dptr);
+/* test hook: q[i] = a[i] / b[i] (host arrays, n <= 2^24) through the device's
+   split fp64 division (divisor reciprocal computed ahead, dsmall.h rcp_ref /
+   div_ref), both the every-lane and the one-lane form; q2 may be NULL.  The
+   physics kernels use it for the Cholesky solve and the line search, so it
+   must equal IEEE division bit for bit */
+int ilqg_selftest_div(const double* a, const double* b, double* q, double* q2, int n);
 #ifdef __cplusplus
 }
 #endif
