@@ -240,6 +240,7 @@ struct ilqg_solver {
   int Dp = 0, WCp = 0, lag = 0, nvt = 0, cv = 0, nut = 0;
   bool fused = false;
   int riccati = ILQG_RICCATI_EXACT;  // ilqg_solver_set_riccati
+  int fdprec = ILQG_FD_F64;          // ilqg_solver_set_fd_precision
   hipStream_t stream = nullptr;
   DevBuf traj[5], cand[5], dinit[5];
   DevBuf qfrc_applied, xfrc_applied, K, k, deriv, warm_c, cost_c, V, v, cost_cand, cost_sel, sel, alphas, cost;
@@ -894,6 +895,14 @@ int ilqg_fd_sweep(ilqg_solver* s) {
     HIPCHK(s->timed(3, [&] { return fused_launch(s, whole(s), 0); }));
     return ILQG_OK;
   }
+  if (s->fdprec == ILQG_FD_F32) {
+    HIPCHK(s->timed(3, [&] {
+      return launch_fd_sweep_f32(m->dm, m->Lc, m->C, m->X, nom, npts, s->P, s->qfrc_applied.as<double>(),
+                                 s->xfrc_applied.as<double>(), s->cview(), s->warm_c.as<double>(),
+                                 s->cost_c.as<double>(), s->deriv.as<double>(), s->Dp, ILQG_FD32_EPS, s->stream);
+    }));
+    return ILQG_OK;
+  }
   HIPCHK(s->timed(2, [&] {
     return launch_fd_centre_coop(m->dm, m->Lc, m->C, m->X, nom, npts, s->P, s->qfrc_applied.as<double>(),
                                  s->xfrc_applied.as<double>(), s->cview(), s->warm_c.as<double>(),
@@ -1050,7 +1059,20 @@ int ilqg_solver_set_riccati(ilqg_solver* s, int mode) {
   s->riccati = mode;
   // the fused sweep streams the bit-exact recursion; the MFMA one runs after a
   // plain sweep (its workspace -- the hand-off block -- is allocated either way)
-  s->fused = mode == ILQG_RICCATI_EXACT && fused_ok(s->model) && s->sync.p;
+  s->fused = mode == ILQG_RICCATI_EXACT && s->fdprec == ILQG_FD_F64 && fused_ok(s->model) && s->sync.p;
+  return ILQG_OK;
+}
+
+int ilqg_solver_set_fd_precision(ilqg_solver* s, int prec) {
+  if (!s || (prec != ILQG_FD_F64 && prec != ILQG_FD_F32)) return fail(ILQG_ERR_ARG, "bad argument");
+  if (prec == ILQG_FD_F32) {
+    if (!s->groups.empty()) return fail(ILQG_ERR_UNSUPPORTED, "fp32 FD with seed groups");
+    if (coop_lds_bytes_f32(s->model->Lc, s->model->C) > kMaxLds) return lds_fail();
+  }
+  HIPCHK(s->sync_all());
+  s->fdprec = prec;
+  // the fused sweep is the fp64 one: fp32 FD runs the two-kernel sweep, then the recursion
+  s->fused = s->riccati == ILQG_RICCATI_EXACT && prec == ILQG_FD_F64 && fused_ok(s->model) && s->sync.p;
   return ILQG_OK;
 }
 

@@ -1,0 +1,2558 @@
+// Body of the cooperative device physics, included by dcoop.h (namespace
+// coop, real = double: the bit-exact fp64 pipeline) and dcoop_f32.h
+// (namespace coopf, real = float: the fp32 FD sweep of BASELINE.json cfg 5).
+// Not a standalone header: the includer opens the namespace and defines
+// `real`.  Model data stays fp64 (read and rounded where used); workspace,
+// state and arithmetic on workspace values are `real`.
+using namespace dev;
+
+struct Team {
+  real* w;   // WsLayout doubles (stride 1)
+  int* iw;     // WsLayout ints
+  real* c;   // CoopLayout doubles
+  int* ci;     // CoopLayout ints
+  int tid, nt;
+};
+
+// Team synchronisation: team_sync() (dsmall.h).
+#define TSYNC() team_sync()
+
+// diagnostic build only (-DILQG_STAMPS): per-stage s_memtime deltas of
+// workgroup 0, lane 0, accumulated in LDS (a global read-modify-write per
+// stamp would itself wait on memory) and flushed once at kernel end
+#ifdef ILQG_STAMPS
+#define STAMP_N 44
+// (per translation unit: the rollout and the FD kernels each read their own copy)
+static __device__ unsigned long long g_stamp_acc[48];
+static __device__ unsigned long long g_stamp_cnt[48];
+static __device__ unsigned long long g_newton_iters;  // all workgroups: Newton iterations
+static __device__ unsigned long long g_newton_calls;  // all workgroups: solver calls
+__shared__ unsigned long long s_stamp_acc[STAMP_N], s_stamp_cnt[STAMP_N], s_stamp_prev, s_stamp_prevb;
+#define STAMP_AT(lane, prev, id)                                             \
+  do {                                                                       \
+    if (threadIdx.x == (lane) && blockIdx.x == 0) {                          \
+      unsigned long long t_ = __builtin_amdgcn_s_memtime();                  \
+      if ((id) >= 0) {                                                       \
+        s_stamp_acc[(id) < 0 ? 0 : (id)] += t_ - prev;                       \
+        s_stamp_cnt[(id) < 0 ? 0 : (id)]++;                                  \
+      }                                                                      \
+      prev = t_;                                                             \
+    }                                                                        \
+  } while (0)
+// wave 0 lane 0; STAMPB: lane 0 of the helper wave of a two-wave team
+#define STAMP(id) STAMP_AT(0, s_stamp_prev, id)
+#define STAMPB(id) STAMP_AT(64, s_stamp_prevb, id)
+#define STAMP_INIT()                                                         \
+  do {                                                                       \
+    if (threadIdx.x == 0 && blockIdx.x == 0) {                               \
+      for (int i_ = 0; i_ < STAMP_N; i_++) s_stamp_acc[i_] = s_stamp_cnt[i_] = 0; \
+      s_stamp_prev = s_stamp_prevb = __builtin_amdgcn_s_memtime();           \
+    }                                                                        \
+  } while (0)
+#define STAMP_FLUSH()                                                        \
+  do {                                                                       \
+    if (threadIdx.x == 0 && blockIdx.x == 0)                                 \
+      for (int i_ = 0; i_ < STAMP_N; i_++) {                                 \
+        g_stamp_acc[i_] += s_stamp_acc[i_];                                  \
+        g_stamp_cnt[i_] += s_stamp_cnt[i_];                                  \
+      }                                                                      \
+  } while (0)
+#else
+#define STAMP(id) \
+  do {            \
+  } while (0)
+#define STAMPB(id) STAMP(id)
+#define STAMP_INIT() STAMP(-1)
+#define STAMP_FLUSH() STAMP(-1)
+#endif
+#define FOR_T(v, n) for (int v = T.tid; v < (n); v += T.nt)
+
+#ifndef KIN_SPLIT
+#define KIN_SPLIT 1
+#endif
+// below this many dofs the small factorizations run on lane 0 (fewer LDS round trips)
+constexpr int SERIAL_NV = 12;
+
+__device__ __forceinline__ real tdot(const real* a, const real* b, int n) {
+  real r = 0;
+  for (int i = 0; i < n; i++) r += a[i] * b[i];
+  return r;
+}
+
+// ------------------------------------------------------ position stage ---
+// model traits with compile-time sizes and tables (static_models.h)
+template <class M>
+concept StaticModel = requires { std::integral_constant<int, M::nbody>{}; };
+
+// rot_vec_quat / normalize4 with their special cases as selects instead of
+// branches: the same doubles in every case (the general formula is computed
+// and discarded where MuJoCo takes the shortcut), no exec-mask round trips on
+// the serial chain
+__device__ __forceinline__ void rot_vec_quat_sel(real* r, const real* v, const real* q) {
+  const bool vz = v[0] == 0 && v[1] == 0 && v[2] == 0;
+  const bool qi = q[0] == 1 && q[1] == 0 && q[2] == 0 && q[3] == 0;
+  const real t0 = q[0] * v[0] + q[2] * v[2] - q[3] * v[1];
+  const real t1 = q[0] * v[1] + q[3] * v[0] - q[1] * v[2];
+  const real t2 = q[0] * v[2] + q[1] * v[1] - q[2] * v[0];
+  const real r0 = v[0] + 2 * (q[2] * t2 - q[3] * t1);
+  const real r1 = v[1] + 2 * (q[3] * t0 - q[1] * t2);
+  const real r2 = v[2] + 2 * (q[1] * t1 - q[2] * t0);
+  r[0] = vz ? 0.0 : (qi ? v[0] : r0);
+  r[1] = vz ? 0.0 : (qi ? v[1] : r1);
+  r[2] = vz ? 0.0 : (qi ? v[2] : r2);
+}
+__device__ __forceinline__ void normalize4_sel(real* q) {
+  const real norm = sqrt(q[0] * q[0] + q[1] * q[1] + q[2] * q[2] + q[3] * q[3]);
+  const bool tiny = norm < MINVAL;
+  const bool scale = !tiny && fabs(norm - 1) > MINVAL;
+  const real inv = 1 / norm;
+  const real s0 = q[0] * inv, s1 = q[1] * inv, s2 = q[2] * inv, s3 = q[3] * inv;
+  q[0] = tiny ? 1.0 : (scale ? s0 : q[0]);
+  q[1] = tiny ? 0.0 : (scale ? s1 : q[1]);
+  q[2] = tiny ? 0.0 : (scale ? s2 : q[2]);
+  q[3] = tiny ? 0.0 : (scale ? s3 : q[3]);
+}
+
+// normalize4_sel when the squared norm already decides that q stays as it is:
+// |fl(sqrt(s)) - 1| <= MINVAL exactly for s in [S_LO, S_HI] (sqrt correctly
+// rounded and monotone; the bounds are the ends of that run of doubles,
+// tests/test_oracle_physics.py::test_normalize4_window).  Unit quaternion
+// products land there almost always, so the chain skips the sqrt and divide.
+constexpr real NORM4_S_LO = 0x1.fffffffffffeep-1, NORM4_S_HI = 0x1.0000000000009p+0;
+__device__ __forceinline__ void normalize4_fast(real* q) {
+  const real s = q[0] * q[0] + q[1] * q[1] + q[2] * q[2] + q[3] * q[3];
+  if (s >= NORM4_S_LO && s <= NORM4_S_HI) return;
+  normalize4_sel(q);
+}
+
+// The kinematic chain of a compile-time model on lane 0 with every body frame
+// in registers (no store->load round trip through LDS between a body and its
+// children): the tree walk is unrolled with compile-time parent indices and
+// joint types.  Same operations in the same order as the loop in kinematics().
+template <class M>
+__device__ inline void kin_chain_static(const M& m, const real* qpos, const real* qloc, real* xpos,
+                                        real* xquat, real* xanchor, real* xaxis) {
+  constexpr int NB = M::nbody;
+  real xp[NB][3], xq[NB][4];
+  xp[0][0] = xp[0][1] = xp[0][2] = 0;
+  xq[0][0] = 1;
+  xq[0][1] = xq[0][2] = xq[0][3] = 0;
+  sfor<1, NB>(SLAM(ii) {
+    constexpr int i = SK(ii);
+    constexpr int pid = M::body_parentid[i];
+    real tmp[3], bpos[3], bquat[4];
+    ldm<3>(bpos, m.body_pos + 3 * i);
+    ldm<4>(bquat, m.body_quat + 4 * i);
+    rot_vec_quat_sel(tmp, bpos, xq[pid]);
+    xp[i][0] = xp[pid][0] + tmp[0];
+    xp[i][1] = xp[pid][1] + tmp[1];
+    xp[i][2] = xp[pid][2] + tmp[2];
+    quat_mul(xq[i], xq[pid], bquat);
+    sfor<0, M::body_jntnum[i]>(SLAM(jj) {
+      constexpr int jid = M::body_jntadr[i] + SK(jj);
+      constexpr int type = M::jnt_type[jid], qadr = M::jnt_qposadr[jid];
+      real jpos[3], jaxis[3];
+      ldm<3>(jpos, m.jnt_pos + 3 * jid);
+      ldm<3>(jaxis, m.jnt_axis + 3 * jid);
+      if constexpr (type == JNT_FREE) {
+        for (int k = 0; k < 3; k++) xp[i][k] = qpos[qadr + k];
+        for (int k = 0; k < 4; k++) xq[i][k] = qpos[qadr + 3 + k];
+        normalize4_sel(xq[i]);
+        for (int k = 0; k < 3; k++) { xanchor[3 * jid + k] = xp[i][k]; xaxis[3 * jid + k] = jaxis[k]; }
+      } else {
+        real anc[3], ax[3];
+        rot_vec_quat_sel(anc, jpos, xq[i]);
+        anc[0] += xp[i][0]; anc[1] += xp[i][1]; anc[2] += xp[i][2];
+        rot_vec_quat_sel(ax, jaxis, xq[i]);
+        if constexpr (type == JNT_SLIDE) {
+          const real dq = qpos[qadr] - m.qpos0[qadr];
+          xp[i][0] += ax[0] * dq; xp[i][1] += ax[1] * dq; xp[i][2] += ax[2] * dq;
+        } else {
+          real ql[4];
+          ldm<4>(ql, qloc + 4 * jid);
+          quat_mul(xq[i], xq[i], ql);
+          rot_vec_quat_sel(tmp, jpos, xq[i]);
+          xp[i][0] = anc[0] - tmp[0];
+          xp[i][1] = anc[1] - tmp[1];
+          xp[i][2] = anc[2] - tmp[2];
+        }
+        for (int k = 0; k < 3; k++) { xanchor[3 * jid + k] = anc[k]; xaxis[3 * jid + k] = ax[k]; }
+      }
+    });
+    normalize4_sel(xq[i]);
+    for (int k = 0; k < 3; k++) xpos[3 * i + k] = xp[i][k];
+    for (int k = 0; k < 4; k++) xquat[4 * i + k] = xq[i][k];
+  });
+  for (int k = 0; k < 3; k++) xpos[k] = 0;
+  xquat[0] = 1;
+  xquat[1] = xquat[2] = xquat[3] = 0;
+}
+
+// The same chain as kin_chain_static, split by dependency (compile-time models):
+//   1. lane 0 walks the quaternion chain alone (body quat products, joint
+//      rotations, normalisation) -- it never reads a position -- and parks
+//      every quaternion a rotation below needs;
+//   2. every vector rotation of the walk (body offsets, joint anchors, axes and
+//      post-rotation anchors) runs on a lane of its own;
+//   3. lane 0 walks the position chain: additions only.
+// Each output is produced by the same operations in the same order as in
+// kin_chain_static (and the oracle), only on another lane or earlier.
+template <class M>
+struct KinPlan {
+  // rotation r: vector kind (0 body_pos, 1 jnt_pos, 2 jnt_axis) and index, quaternion
+  // source (>= 0: parked slot, < 0: final quaternion of body -1 - src), role
+  // (0 body offset, 1 anchor, 2 axis, 3 post-rotation anchor) and its joint
+  static constexpr int MAXR = 64;
+  int nrot = 0, nslot = 0;
+  int vkind[MAXR] = {}, vidx[MAXR] = {}, qsrc[MAXR] = {}, role[MAXR] = {}, jnt[MAXR] = {};
+  int body_rot[M::nbody > 0 ? M::nbody : 1] = {};            // rotation of body i's offset
+  int anc_rot[M::njnt > 0 ? M::njnt : 1] = {}, ax_rot[M::njnt > 0 ? M::njnt : 1] = {},
+      tmp_rot[M::njnt > 0 ? M::njnt : 1] = {};
+  int qb_slot[M::nbody > 0 ? M::nbody : 1] = {};             // quat after the body quat (-1: not parked)
+  int qj_slot[M::njnt > 0 ? M::njnt : 1] = {};               // quat after joint j's rotation (-1)
+  bool ok = true;
+  struct Packed {
+    unsigned long long w[MAXR / 4];
+    __host__ __device__ constexpr unsigned long long operator[](int i) const { return w[i]; }
+  };
+  constexpr Packed packed() const {
+    Packed p{};
+    for (int r = 0; r < nrot; r++) {
+      const unsigned long long d = (unsigned long long)(vkind[r] | (vidx[r] << 2) | ((qsrc[r] + 64) << 9));
+      p.w[r / 4] |= d << (16 * (r % 4));
+    }
+    return p;
+  }
+  constexpr KinPlan() {
+    auto add = [&](int kind, int idx, int q, int rl, int j) {
+      if (nrot >= MAXR) { ok = false; return 0; }
+      vkind[nrot] = kind; vidx[nrot] = idx; qsrc[nrot] = q; role[nrot] = rl; jnt[nrot] = j;
+      return nrot++;
+    };
+    for (int i = 0; i < M::nbody; i++) qb_slot[i] = -1;
+    for (int j = 0; j < M::njnt; j++) qj_slot[j] = anc_rot[j] = ax_rot[j] = tmp_rot[j] = -1;
+    for (int i = 1; i < M::nbody; i++) {
+      body_rot[i] = add(0, i, -1 - M::body_parentid[i], 0, -1);
+      int cur = -2;  // quaternion the next joint starts from: -2 = q_b (not parked yet)
+      for (int jj = 0; jj < M::body_jntnum[i]; jj++) {
+        const int j = M::body_jntadr[i] + jj, type = M::jnt_type[j];
+        if (type == JNT_FREE) { cur = -3; continue; }  // no rotations; later joints unsupported
+        if (cur == -3) { ok = false; continue; }
+        if (cur == -2) { qb_slot[i] = nslot++; cur = qb_slot[i]; }
+        anc_rot[j] = add(1, j, cur, 1, j);
+        ax_rot[j] = add(2, j, cur, 2, j);
+        if (type != JNT_SLIDE) {
+          if (nslot >= 63 || j >= 127 || i >= 64) ok = false;
+          qj_slot[j] = nslot++;
+          cur = qj_slot[j];
+          tmp_rot[j] = add(1, j, cur, 3, j);
+        }
+      }
+    }
+  }
+};
+
+template <class M, class F>
+__device__ inline void kin_chain_par(const M& m, const Team& T, const real* qpos, const real* qloc, real* xpos,
+                                     real* xquat, real* xanchor, real* xaxis, real* scratch,
+                                     F&& after_quats) {
+  static constexpr KinPlan<M> P{};
+  constexpr int NB = M::nbody;
+  real* QS = scratch;                 // parked quaternions, 4 per slot
+  real* RS = scratch + 4 * P.nslot;   // rotation results, 3 per rotation
+  // 1. quaternion chain (lane 0)
+  if (T.tid == 0) {
+    // every LDS operand of the walk is loaded up front: one wait, none inside the walk
+    real bq[NB][4], ql[M::njnt > 0 ? M::njnt : 1][4];
+    sfor<1, NB>(SLAM(ii) { ldm<4>(bq[SK(ii)], m.body_quat + 4 * SK(ii)); });
+    sfor<0, M::njnt>(SLAM(jj) {
+      constexpr int j = SK(jj);
+      if constexpr (M::jnt_type[j] != JNT_FREE && M::jnt_type[j] != JNT_SLIDE) ldm<4>(ql[j], qloc + 4 * j);
+    });
+    real xq[NB][4];
+    xq[0][0] = 1;
+    xq[0][1] = xq[0][2] = xq[0][3] = 0;
+    sfor<1, NB>(SLAM(ii) {
+      constexpr int i = SK(ii);
+      constexpr int pid = M::body_parentid[i];
+      quat_mul(xq[i], xq[pid], bq[i]);
+      if constexpr (P.qb_slot[i] >= 0)
+        for (int k = 0; k < 4; k++) QS[4 * P.qb_slot[i] + k] = xq[i][k];
+      sfor<0, M::body_jntnum[i]>(SLAM(jj) {
+        constexpr int jid = M::body_jntadr[i] + SK(jj);
+        constexpr int type = M::jnt_type[jid], qadr = M::jnt_qposadr[jid];
+        if constexpr (type == JNT_FREE) {
+          for (int k = 0; k < 4; k++) xq[i][k] = qpos[qadr + 3 + k];
+          normalize4_fast(xq[i]);
+        } else if constexpr (type != JNT_SLIDE) {
+          quat_mul(xq[i], xq[i], ql[jid]);
+          for (int k = 0; k < 4; k++) QS[4 * P.qj_slot[jid] + k] = xq[i][k];
+        }
+      });
+      normalize4_fast(xq[i]);
+      for (int k = 0; k < 4; k++) xquat[4 * i + k] = xq[i][k];
+    });
+    xquat[0] = 1;
+    xquat[1] = xquat[2] = xquat[3] = 0;
+  }
+  team_sync();
+  after_quats();  // every body quaternion is final
+  STAMP(22);
+  // 2. every rotation on a lane of its own
+  if (T.tid < P.nrot) {
+    // lane -> plan entry: 16-bit descriptors packed 4 per 64-bit immediate
+    // (kind 2 bits | vector index 7 bits | quaternion source + 64 7 bits)
+    static constexpr auto D = P.packed();
+    const int l = T.tid;
+    unsigned long long w = D[0];
+    sfor<1, (P.nrot + 3) / 4>(SLAM(kk) { w = (l >> 2) == SK(kk) ? D[SK(kk)] : w; });
+    const unsigned d = (unsigned)(w >> (16 * (l & 3))) & 0xffffu;
+    const int kind = d & 3, idx = (d >> 2) & 127, q = (int)(d >> 9) - 64, j = idx;
+    const int rl = kind == 2 ? 2 : 0;
+    // integer offsets from one base each (a select between pointers becomes a
+    // lookup table in scratch and a flat load)
+    const int d1 = (int)(m.jnt_pos - m.body_pos), d2 = (int)(m.jnt_axis - m.body_pos);
+    const real* v = m.body_pos + (3 * idx + (kind == 1 ? d1 : 0) + (kind == 2 ? d2 : 0));
+    const int dq = (int)(xquat - QS);
+    const real* qq = QS + (q >= 0 ? 4 * q : dq + 4 * (-1 - q));
+    real vv[3], q4[4], r3[3];
+    ldm<3>(vv, v);
+    ldm<4>(q4, qq);
+    rot_vec_quat_sel(r3, vv, q4);
+    for (int k = 0; k < 3; k++) RS[3 * T.tid + k] = r3[k];
+    if (rl == 2)
+      for (int k = 0; k < 3; k++) xaxis[3 * j + k] = r3[k];
+  }
+  team_sync();
+  STAMP(23);
+  // 3. position chain (lane 0): the additions of kin_chain_static in its order
+  if (T.tid == 0) {
+    real R[P.nrot][3];
+    sfor<0, P.nrot>(SLAM(rr) { ldm<3>(R[SK(rr)], RS + 3 * SK(rr)); });
+    real xp[NB][3];
+    xp[0][0] = xp[0][1] = xp[0][2] = 0;
+    sfor<1, NB>(SLAM(ii) {
+      constexpr int i = SK(ii);
+      constexpr int pid = M::body_parentid[i];
+      const real* tmp = R[P.body_rot[i]];
+      xp[i][0] = xp[pid][0] + tmp[0];
+      xp[i][1] = xp[pid][1] + tmp[1];
+      xp[i][2] = xp[pid][2] + tmp[2];
+      sfor<0, M::body_jntnum[i]>(SLAM(jj) {
+        constexpr int jid = M::body_jntadr[i] + SK(jj);
+        constexpr int type = M::jnt_type[jid], qadr = M::jnt_qposadr[jid];
+        if constexpr (type == JNT_FREE) {
+          real jaxis[3];
+          ldm<3>(jaxis, m.jnt_axis + 3 * jid);
+          for (int k = 0; k < 3; k++) xp[i][k] = qpos[qadr + k];
+          for (int k = 0; k < 3; k++) { xanchor[3 * jid + k] = xp[i][k]; xaxis[3 * jid + k] = jaxis[k]; }
+        } else {
+          const real* ra = R[P.anc_rot[jid]];
+          real anc[3];
+          anc[0] = ra[0] + xp[i][0]; anc[1] = ra[1] + xp[i][1]; anc[2] = ra[2] + xp[i][2];
+          if constexpr (type == JNT_SLIDE) {
+            const real* ax = R[P.ax_rot[jid]];
+            const real dq = qpos[qadr] - m.qpos0[qadr];
+            xp[i][0] += ax[0] * dq; xp[i][1] += ax[1] * dq; xp[i][2] += ax[2] * dq;
+          } else {
+            const real* tmp2 = R[P.tmp_rot[jid]];
+            xp[i][0] = anc[0] - tmp2[0];
+            xp[i][1] = anc[1] - tmp2[1];
+            xp[i][2] = anc[2] - tmp2[2];
+          }
+          for (int k = 0; k < 3; k++) xanchor[3 * jid + k] = anc[k];
+        }
+      });
+      for (int k = 0; k < 3; k++) xpos[3 * i + k] = xp[i][k];
+    });
+    xpos[0] = xpos[1] = xpos[2] = 0;
+  }
+}
+
+__device__ inline void kinematics(const auto& m, const auto& L, const auto& C, const Team& T) {
+  real* qpos = T.w + L.qpos;
+  real* xpos = T.w + L.xpos;
+  real* xquat = T.w + L.xquat;
+  real* xmat = T.w + L.xmat;
+  real* xipos = T.w + L.xipos;
+  real* ximat = T.w + L.ximat;
+  real* xanchor = T.w + L.xanchor;
+  real* xaxis = T.w + L.xaxis;
+  real* qloc = T.c + C.qloc;
+  // joint-local rotations depend on qpos only: all joints at once
+  FOR_T(j, m.njnt) {
+    int type = m.jnt_type[j], qadr = m.jnt_qposadr[j];
+    real q[4], ja[3];
+    if (type == JNT_HINGE) {
+      ldm<3>(ja, m.jnt_axis + 3 * j);
+      axis_angle2quat(q, ja, qpos[qadr] - m.qpos0[qadr]);
+      for (int k = 0; k < 4; k++) qloc[4 * j + k] = q[k];
+    } else if (type == JNT_BALL) {
+      q[0] = qpos[qadr]; q[1] = qpos[qadr + 1]; q[2] = qpos[qadr + 2]; q[3] = qpos[qadr + 3];
+      normalize4(q);
+      for (int k = 0; k < 4; k++) qloc[4 * j + k] = q[k];
+    }
+  }
+  TSYNC();
+  STAMP(11);
+  // the kinematic chain: lane 0
+  using MT = std::remove_cvref_t<decltype(m)>;
+  if constexpr (StaticModel<MT>) {
+    static constexpr KinPlan<MT> plan{};
+    // the split chain needs its scratch in the union (dead until collision) and a lane per rotation
+    if constexpr (plan.ok && 4 * plan.nslot + 3 * plan.nrot <= 12 * MT::nbody + 10 * MT::nv && KIN_SPLIT)
+      kin_chain_par(m, T, qpos, qloc, xpos, xquat, xanchor, xaxis, T.w + L.con, []() {});
+    else if (T.tid == 0)
+      kin_chain_static(m, qpos, qloc, xpos, xquat, xanchor, xaxis);
+  } else if (T.tid == 0) {
+    xpos[0] = xpos[1] = xpos[2] = 0;
+    xquat[0] = 1; xquat[1] = xquat[2] = xquat[3] = 0;
+    for (int i = 1; i < m.nbody; i++) {
+      int pid = m.body_parentid[i];
+      real xp[3], xq[4], tmp[3], pq[4], bp[3], bq[4];
+      ldm<4>(pq, xquat + 4 * pid);
+      ldm<3>(bp, m.body_pos + 3 * i);
+      ldm<4>(bq, m.body_quat + 4 * i);
+      rot_vec_quat(tmp, bp, pq);
+      xp[0] = xpos[3 * pid] + tmp[0];
+      xp[1] = xpos[3 * pid + 1] + tmp[1];
+      xp[2] = xpos[3 * pid + 2] + tmp[2];
+      quat_mul(xq, pq, bq);
+      for (int j = 0; j < m.body_jntnum[i]; j++) {
+        int jid = m.body_jntadr[i] + j;
+        int qadr = m.jnt_qposadr[jid];
+        int type = m.jnt_type[jid];
+        real anc[3], ax[3], jp[3], ja[3];
+        ldm<3>(jp, m.jnt_pos + 3 * jid);
+        ldm<3>(ja, m.jnt_axis + 3 * jid);
+        if (type == JNT_FREE) {
+          xp[0] = qpos[qadr]; xp[1] = qpos[qadr + 1]; xp[2] = qpos[qadr + 2];
+          xq[0] = qpos[qadr + 3]; xq[1] = qpos[qadr + 4]; xq[2] = qpos[qadr + 5]; xq[3] = qpos[qadr + 6];
+          normalize4(xq);
+          for (int k = 0; k < 3; k++) { xanchor[3 * jid + k] = xp[k]; xaxis[3 * jid + k] = ja[k]; }
+          continue;
+        }
+        rot_vec_quat(anc, jp, xq);
+        anc[0] += xp[0]; anc[1] += xp[1]; anc[2] += xp[2];
+        rot_vec_quat(ax, ja, xq);
+        if (type == JNT_SLIDE) {
+          real dq = qpos[qadr] - m.qpos0[qadr];
+          xp[0] += ax[0] * dq; xp[1] += ax[1] * dq; xp[2] += ax[2] * dq;
+        } else {
+          real ql[4];
+          ldm<4>(ql, qloc + 4 * jid);
+          quat_mul(xq, xq, ql);
+          rot_vec_quat(tmp, jp, xq);
+          xp[0] = anc[0] - tmp[0];
+          xp[1] = anc[1] - tmp[1];
+          xp[2] = anc[2] - tmp[2];
+        }
+        for (int k = 0; k < 3; k++) { xanchor[3 * jid + k] = anc[k]; xaxis[3 * jid + k] = ax[k]; }
+      }
+      normalize4(xq);
+      for (int k = 0; k < 3; k++) xpos[3 * i + k] = xp[k];
+      for (int k = 0; k < 4; k++) xquat[4 * i + k] = xq[k];
+    }
+  }
+  TSYNC();
+  STAMP(12);
+  // body frames and inertial frames: one lane per body
+  FOR_T(i, m.nbody) {
+    real xq[4], mat[9], tmp[3], ip[3], iq[4], q2[4];
+    ldm<4>(xq, xquat + 4 * i);
+    quat2mat(mat, xq);
+    for (int k = 0; k < 9; k++) xmat[9 * i + k] = mat[k];
+    if (i == 0) {
+      xipos[0] = xipos[1] = xipos[2] = 0;
+      for (int k = 0; k < 9; k++) ximat[k] = mat[k];
+    } else {
+      ldm<3>(ip, m.body_ipos + 3 * i);
+      ldm<4>(iq, m.body_iquat + 4 * i);
+      rot_vec_mat(tmp, ip, mat);
+      xipos[3 * i] = tmp[0] + xpos[3 * i];
+      xipos[3 * i + 1] = tmp[1] + xpos[3 * i + 1];
+      xipos[3 * i + 2] = tmp[2] + xpos[3 * i + 2];
+      quat_mul(q2, xq, iq);
+      quat2mat(mat, q2);
+      for (int k = 0; k < 9; k++) ximat[9 * i + k] = mat[k];
+    }
+  }
+  TSYNC();
+  STAMP(13);
+  real* gxpos = T.w + L.gxpos;
+  real* gxmat = T.w + L.gxmat;
+  FOR_T(g, m.ngeom) {
+    int b = m.geom_bodyid[g];
+    real tmp[3], q[4], bm[9], bq[4], gp[3], gq[4], mat[9];
+    ldm<9>(bm, xmat + 9 * b);
+    ldm<4>(bq, xquat + 4 * b);
+    ldm<3>(gp, m.geom_pos + 3 * g);
+    ldm<4>(gq, m.geom_quat + 4 * g);
+    rot_vec_mat(tmp, gp, bm);
+    gxpos[3 * g] = tmp[0] + xpos[3 * b];
+    gxpos[3 * g + 1] = tmp[1] + xpos[3 * b + 1];
+    gxpos[3 * g + 2] = tmp[2] + xpos[3 * b + 2];
+    quat_mul(q, bq, gq);
+    quat2mat(mat, q);
+    for (int k = 0; k < 9; k++) gxmat[9 * g + k] = mat[k];
+  }
+  TSYNC();
+}
+
+// the compile-time models whose kinematics() takes the split chain (kin_chain_par)
+template <class MT>
+constexpr bool kin_split_ok() {
+  if constexpr (StaticModel<MT>) {
+    constexpr KinPlan<MT> p{};
+    return p.ok && 4 * p.nslot + 3 * p.nrot <= 12 * MT::nbody + 10 * MT::nv && KIN_SPLIT;
+  } else {
+    return false;
+  }
+}
+
+// Hand-off between two waves of a team through an LDS word, without the third
+// wave (unlike __syncthreads): the signaller's earlier LDS stores are ordered
+// before the flag (workgroup release), the waiter's later loads after it
+// (acquire).  Flags carry an increasing step id; the wait is bounded.
+__device__ inline void wave_signal(int* f, int v) {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+  if ((threadIdx.x & (TEAM_SIZE - 1)) == 0) __hip_atomic_store(f, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+__device__ inline void wave_wait(const int* f, int v) {
+  for (int it = 0; it < (1 << 22); it++) {
+    if (__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) >= v) break;
+    __builtin_amdgcn_s_sleep(1);
+  }
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+}
+
+// kinematics() of a compile-time model on two waves (three-wave rollout):
+// the primary computes the joint rotations and walks the quaternion chain,
+// signals, then walks the positions; the helper waits for the quaternions
+// and computes every frame rotation -- xmat, ximat, gxmat are functions of the
+// quaternions alone -- which the primary's xipos / geom positions then read.
+// Each value is the expression kinematics() evaluates, on another wave.
+__device__ inline void kinematics_primary(const auto& m, const auto& L, const auto& C, const Team& T, int* fq,
+                                          const int* ff, int sid) {
+  real* qpos = T.w + L.qpos;
+  real* xpos = T.w + L.xpos;
+  real* xquat = T.w + L.xquat;
+  real* xmat = T.w + L.xmat;
+  real* xipos = T.w + L.xipos;
+  real* xanchor = T.w + L.xanchor;
+  real* xaxis = T.w + L.xaxis;
+  real* qloc = T.c + C.qloc;
+  FOR_T(j, m.njnt) {
+    int type = m.jnt_type[j], qadr = m.jnt_qposadr[j];
+    real q[4], ja[3];
+    if (type == JNT_HINGE) {
+      ldm<3>(ja, m.jnt_axis + 3 * j);
+      axis_angle2quat(q, ja, qpos[qadr] - m.qpos0[qadr]);
+      for (int k = 0; k < 4; k++) qloc[4 * j + k] = q[k];
+    } else if (type == JNT_BALL) {
+      q[0] = qpos[qadr]; q[1] = qpos[qadr + 1]; q[2] = qpos[qadr + 2]; q[3] = qpos[qadr + 3];
+      normalize4(q);
+      for (int k = 0; k < 4; k++) qloc[4 * j + k] = q[k];
+    }
+  }
+  TSYNC();
+  STAMP(11);
+  kin_chain_par(m, T, qpos, qloc, xpos, xquat, xanchor, xaxis, T.w + L.con, [&]() { wave_signal(fq, sid); });
+  TSYNC();
+  STAMP(12);
+  wave_wait(ff, sid);
+  // body inertial positions and geom positions (body frame rotations from the helper)
+  real* gxpos = T.w + L.gxpos;
+  FOR_T(e, m.nbody + m.ngeom) {
+    if (e < m.nbody) {
+      const int i = e;
+      if (i == 0) {
+        xipos[0] = xipos[1] = xipos[2] = 0;
+      } else {
+        real mat[9], tmp[3], ip[3];
+        ldm<9>(mat, xmat + 9 * i);
+        ldm<3>(ip, m.body_ipos + 3 * i);
+        rot_vec_mat(tmp, ip, mat);
+        xipos[3 * i] = tmp[0] + xpos[3 * i];
+        xipos[3 * i + 1] = tmp[1] + xpos[3 * i + 1];
+        xipos[3 * i + 2] = tmp[2] + xpos[3 * i + 2];
+      }
+    } else {
+      const int g = e - m.nbody;
+      const int b = m.geom_bodyid[g];
+      real bm[9], gp[3], tmp[3];
+      ldm<9>(bm, xmat + 9 * b);
+      ldm<3>(gp, m.geom_pos + 3 * g);
+      rot_vec_mat(tmp, gp, bm);
+      gxpos[3 * g] = tmp[0] + xpos[3 * b];
+      gxpos[3 * g + 1] = tmp[1] + xpos[3 * b + 1];
+      gxpos[3 * g + 2] = tmp[2] + xpos[3 * b + 2];
+    }
+  }
+  TSYNC();
+}
+__device__ inline void kinematics_frames(const auto& m, const auto& L, const Team& T, const int* fq, int* ff,
+                                         int sid) {
+  real* xquat = T.w + L.xquat;
+  real* xmat = T.w + L.xmat;
+  real* ximat = T.w + L.ximat;
+  real* gxmat = T.w + L.gxmat;
+  wave_wait(fq, sid);
+  FOR_T(e, m.nbody + m.ngeom) {
+    if (e < m.nbody) {
+      const int i = e;
+      real xq[4], mat[9], iq[4], q2[4];
+      ldm<4>(xq, xquat + 4 * i);
+      quat2mat(mat, xq);
+      for (int k = 0; k < 9; k++) xmat[9 * i + k] = mat[k];
+      if (i == 0) {
+        for (int k = 0; k < 9; k++) ximat[k] = mat[k];
+      } else {
+        ldm<4>(iq, m.body_iquat + 4 * i);
+        quat_mul(q2, xq, iq);
+        quat2mat(mat, q2);
+        for (int k = 0; k < 9; k++) ximat[9 * i + k] = mat[k];
+      }
+    } else {
+      const int g = e - m.nbody;
+      const int b = m.geom_bodyid[g];
+      real bq[4], gq[4], q[4], mat[9];
+      ldm<4>(bq, xquat + 4 * b);
+      ldm<4>(gq, m.geom_quat + 4 * g);
+      quat_mul(q, bq, gq);
+      quat2mat(mat, q);
+      for (int k = 0; k < 9; k++) gxmat[9 * g + k] = mat[k];
+    }
+  }
+  TSYNC();
+  wave_signal(ff, sid);
+}
+
+__device__ inline void com_pos(const auto& m, const auto& L, const Team& T) {
+  const int nb = m.nbody;
+  real* xipos = T.w + L.xipos;
+  real* scom = T.w + L.scom;
+  real* cinert = T.w + L.cinert;
+  real* ximat = T.w + L.ximat;
+  real* cdof = T.w + L.cdof;
+  real* xanchor = T.w + L.xanchor;
+  real* xaxis = T.w + L.xaxis;
+  real* xmat = T.w + L.xmat;
+  FOR_T(i, nb) {
+    real ms = m.body_mass[i];
+    scom[3 * i] = xipos[3 * i] * ms;
+    scom[3 * i + 1] = xipos[3 * i + 1] * ms;
+    scom[3 * i + 2] = xipos[3 * i + 2] * ms;
+  }
+  TSYNC();
+  FOR_T(k, 3) {
+    for (int i = nb - 1; i > 0; i--) scom[3 * m.body_parentid[i] + k] += scom[3 * i + k];
+  }
+  TSYNC();
+  FOR_T(i, nb) {
+    if (m.body_subtreemass[i] < MINVAL) {
+      scom[3 * i] = xipos[3 * i];
+      scom[3 * i + 1] = xipos[3 * i + 1];
+      scom[3 * i + 2] = xipos[3 * i + 2];
+    } else {
+      real inv = 1 / m.body_subtreemass[i];
+      scom[3 * i] *= inv;
+      scom[3 * i + 1] *= inv;
+      scom[3 * i + 2] *= inv;
+    }
+  }
+  TSYNC();
+  FOR_T(i, nb) {
+    if (i == 0) {
+      for (int k = 0; k < 10; k++) cinert[k] = 0;
+    } else {
+      real off[3], mat[9], in[3], res[10];
+      const real* rc = scom + 3 * m.body_rootid[i];
+      off[0] = xipos[3 * i] - rc[0];
+      off[1] = xipos[3 * i + 1] - rc[1];
+      off[2] = xipos[3 * i + 2] - rc[2];
+      ldm<9>(mat, ximat + 9 * i);
+      ldm<3>(in, m.body_inertia + 3 * i);
+      inert_com(res, in, mat, off, m.body_mass[i]);
+      for (int k = 0; k < 10; k++) cinert[10 * i + k] = res[k];
+    }
+  }
+  FOR_T(j, m.njnt) {
+    int da = 6 * m.jnt_dofadr[j];
+    int bi = m.jnt_bodyid[j];
+    const real* rc = scom + 3 * m.body_rootid[bi];
+    real off[3] = {rc[0] - xanchor[3 * j], rc[1] - xanchor[3 * j + 1], rc[2] - xanchor[3 * j + 2]};
+    real out[6];
+    int type = m.jnt_type[j];
+    int skip = 0;
+    if (type == JNT_FREE) {
+      for (int k = 0; k < 18; k++) cdof[da + k] = 0;
+      for (int i = 0; i < 3; i++) cdof[da + 3 + 7 * i] = 1;
+      skip = 18;
+    }
+    if (type == JNT_FREE || type == JNT_BALL) {
+      for (int i = 0; i < 3; i++) {
+        real axis[3] = {xmat[9 * bi + i], xmat[9 * bi + i + 3], xmat[9 * bi + i + 6]};
+        out[0] = axis[0]; out[1] = axis[1]; out[2] = axis[2];
+        cross3(out + 3, axis, off);
+        for (int k = 0; k < 6; k++) cdof[da + skip + 6 * i + k] = out[k];
+      }
+    } else if (type == JNT_SLIDE) {
+      out[0] = out[1] = out[2] = 0;
+      out[3] = xaxis[3 * j]; out[4] = xaxis[3 * j + 1]; out[5] = xaxis[3 * j + 2];
+      for (int k = 0; k < 6; k++) cdof[da + k] = out[k];
+    } else {
+      real ax[3] = {xaxis[3 * j], xaxis[3 * j + 1], xaxis[3 * j + 2]};
+      out[0] = ax[0]; out[1] = ax[1]; out[2] = ax[2];
+      cross3(out + 3, ax, off);
+      for (int k = 0; k < 6; k++) cdof[da + k] = out[k];
+    }
+  }
+  TSYNC();
+}
+
+__device__ inline void crb(const auto& m, const auto& L, const auto& C, const auto& X,
+                           const Team& T) {
+  const int nv = m.nv, nb = m.nbody;
+  real* crbv = T.w + L.crb;
+  real* cinert = T.w + L.cinert;
+  real* qM = T.w + L.qM;
+  real* cdof = T.w + L.cdof;
+  real* buf = T.c + C.buf6;
+  FOR_T(e, 10 * nb) crbv[e] = cinert[e];
+  TSYNC();
+  FOR_T(k, 10) {
+    for (int i = nb - 1; i > 0; i--) {
+      int p = m.body_parentid[i];
+      if (p > 0) crbv[10 * p + k] += crbv[10 * i + k];
+    }
+  }
+  TSYNC();
+  FOR_T(i, nv) {
+    real ci[10], cd[6], r[6];
+    ldm<10>(ci, crbv + 10 * m.dof_bodyid[i]);
+    ldm<6>(cd, cdof + 6 * i);
+    mul_inert_vec(r, ci, cd);
+    for (int k = 0; k < 6; k++) buf[6 * i + k] = r[k];
+  }
+  TSYNC();
+  FOR_T(e, nv * nv) {
+    int i = e / nv, j = e % nv;
+    if (j <= i) {
+      real v = (i == j) ? m.dof_armature[i] : 0.0;
+      if (X.isanc[e]) v += tdot(cdof + 6 * j, buf + 6 * i, 6);
+      qM[e] = v;
+      qM[j * nv + i] = v;
+    }
+  }
+  TSYNC();
+}
+
+// tree L'DL (oracle factor_ld), parallel over ancestor pairs for each k
+__device__ inline void factor_ld(const auto& m, const auto& X, const Team& T, const real* mat, real* LD,
+                                 real* diaginv, real* tmpv) {
+  const int nv = m.nv;
+  if (nv <= RMAX && X.pmask) {
+    factor_ld_rows(nv, X.pmask, T.tid, mat, LD, diaginv);
+    return;
+  }
+  FOR_T(e, nv * nv) {
+    int i = e / nv, j = e % nv;
+    LD[e] = (j <= i) ? mat[e] : 0;
+  }
+  TSYNC();
+  if (nv <= SERIAL_NV) {
+    // small trees: the oracle's loop on lane 0 beats 4 LDS round trips per k
+    if (T.tid == 0) {
+      if (X.pmask) {
+        // ancestor bitmasks replace the dependent parent-pointer chase
+        for (int k = nv - 1; k >= 0; k--) {
+          if (LD[k * nv + k] < MINVAL) LD[k * nv + k] = MINVAL;
+          const real dk = LD[k * nv + k];
+          for (unsigned long long mi = X.pmask[k]; mi;) {
+            const int i = 63 - __builtin_clzll(mi);
+            mi &= ~(1ull << i);
+            real tmp = LD[k * nv + i] / dk;
+            // the ancestors of k below i are exactly i's ancestors (one root path)
+            for (unsigned long long mj = mi | (1ull << i); mj;) {
+              const int j = 63 - __builtin_clzll(mj);
+              mj &= ~(1ull << j);
+              LD[i * nv + j] -= tmp * LD[k * nv + j];
+            }
+            LD[k * nv + i] = tmp;
+          }
+        }
+      } else {
+        for (int k = nv - 1; k >= 0; k--) {
+          if (LD[k * nv + k] < MINVAL) LD[k * nv + k] = MINVAL;
+          for (int i = m.dof_parentid[k]; i >= 0; i = m.dof_parentid[i]) {
+            real tmp = LD[k * nv + i] / LD[k * nv + k];
+            for (int j = i; j >= 0; j = m.dof_parentid[j]) LD[i * nv + j] -= tmp * LD[k * nv + j];
+            LD[k * nv + i] = tmp;
+          }
+        }
+      }
+      for (int i = 0; i < nv; i++) diaginv[i] = 1 / LD[i * nv + i];
+    }
+    TSYNC();
+    return;
+  }
+  for (int k = nv - 1; k >= 0; k--) {
+    if (T.tid == 0 && LD[k * nv + k] < MINVAL) LD[k * nv + k] = MINVAL;
+    TSYNC();
+    FOR_T(i, nv) {
+      if (i != k && X.isanc[k * nv + i]) tmpv[i] = LD[k * nv + i] / LD[k * nv + k];
+    }
+    TSYNC();
+    FOR_T(e, nv * nv) {
+      int i = e / nv, j = e % nv;
+      if (i != k && X.isanc[k * nv + i] && X.isanc[i * nv + j]) LD[e] -= tmpv[i] * LD[k * nv + j];
+    }
+    TSYNC();
+    FOR_T(i, nv) {
+      if (i != k && X.isanc[k * nv + i]) LD[k * nv + i] = tmpv[i];
+    }
+    TSYNC();
+  }
+  FOR_T(i, nv) diaginv[i] = 1 / LD[i * nv + i];
+  TSYNC();
+}
+
+// oracle solve_ld on lane 0 (ends with a barrier)
+__device__ inline void solve_ld(const auto& m, const auto& X, const Team& T, const real* LD,
+                                const real* diaginv, real* x) {
+  const int nv = m.nv;
+  if (nv <= RMAX && X.pmask) {
+    solve_ld_rows(nv, X.pmask, T.tid, LD, diaginv, x);
+    return;
+  }
+  if (T.tid == 0) {
+    if (X.pmask) {
+      for (int i = nv - 1; i >= 0; i--) {
+        real tmp = x[i];
+        if (tmp != 0)
+          for (unsigned long long mj = X.pmask[i]; mj;) {
+            const int j = 63 - __builtin_clzll(mj);
+            mj &= ~(1ull << j);
+            x[j] -= LD[i * nv + j] * tmp;
+          }
+      }
+      for (int i = 0; i < nv; i++) x[i] *= diaginv[i];
+      for (int i = 0; i < nv; i++) {
+        real xi = x[i];
+        for (unsigned long long mj = X.pmask[i]; mj;) {
+          const int j = 63 - __builtin_clzll(mj);
+          mj &= ~(1ull << j);
+          xi -= LD[i * nv + j] * x[j];
+        }
+        x[i] = xi;
+      }
+    } else {
+      for (int i = nv - 1; i >= 0; i--) {
+        real tmp = x[i];
+        if (tmp != 0)
+          for (int j = m.dof_parentid[i]; j >= 0; j = m.dof_parentid[j]) x[j] -= LD[i * nv + j] * tmp;
+      }
+      for (int i = 0; i < nv; i++) x[i] *= diaginv[i];
+      for (int i = 0; i < nv; i++)
+        for (int j = m.dof_parentid[i]; j >= 0; j = m.dof_parentid[j]) x[i] -= LD[i * nv + j] * x[j];
+    }
+  }
+  TSYNC();
+}
+
+__device__ inline void jac_col(const auto& m, const auto& X, const real* scom, const real* cdof,
+                               const real* point, int body, int k, real* out3) {
+  // one dof column of jac_point (oracle): zero unless dof k lies on the chain of `body`
+  const int nv = m.nv;
+  out3[0] = out3[1] = out3[2] = 0;
+  const real* rc = scom + 3 * m.body_rootid[body];
+  real off[3] = {point[0] - rc[0], point[1] - rc[1], point[2] - rc[2]};
+  while (body && !m.body_dofnum[body]) body = m.body_parentid[body];
+  if (!body) return;
+  int last = m.body_dofadr[body] + m.body_dofnum[body] - 1;
+  if (!X.isanc[last * nv + k]) return;
+  real tmp[3], cd[6];
+  ldm<6>(cd, cdof + 6 * k);
+  cross3(tmp, cd, off);
+  out3[0] = cd[3] + tmp[0];
+  out3[1] = cd[4] + tmp[1];
+  out3[2] = cd[5] + tmp[2];
+}
+
+__device__ inline void collision(const auto& m, const auto& L, const auto& C, const auto& X,
+                                 const Team& T) {
+  real* gxpos = T.w + L.gxpos;
+  real* gxmat = T.w + L.gxmat;
+  real* con = T.w + L.con;
+  int* coni = T.iw + L.coni;
+  real* pcon = T.w + L.pcon;
+  int* pcnt = T.ci + C.pcnt;
+  FOR_T(p, X.npair) {
+    int g1 = X.pair[2 * p], g2 = X.pair[2 * p + 1];
+    int n = 0;
+    real margin = maxd(m.geom_margin[g1], m.geom_margin[g2]);
+    bool ok = true;
+    if (m.geom_rbound[g1] > 0 && m.geom_rbound[g2] > 0) {
+      real dd[3] = {gxpos[3 * g1] - gxpos[3 * g2], gxpos[3 * g1 + 1] - gxpos[3 * g2 + 1],
+                      gxpos[3 * g1 + 2] - gxpos[3 * g2 + 2]};
+      if (sqrt(dot3(dd, dd)) > m.geom_rbound[g1] + m.geom_rbound[g2] + margin) ok = false;
+    }
+    if (ok) {
+      int ga = g1, gb = g2;
+      if (m.geom_type[g1] > m.geom_type[g2]) { ga = g2; gb = g1; }
+      real pos1[3], mat1[9], sz1[3], pos2[3], mat2[9], sz2[3];
+      ldm<3>(pos1, gxpos + 3 * ga);
+      ldm<9>(mat1, gxmat + 9 * ga);
+      ldm<3>(sz1, m.geom_size + 3 * ga);
+      ldm<3>(pos2, gxpos + 3 * gb);
+      ldm<9>(mat2, gxmat + 9 * gb);
+      ldm<3>(sz2, m.geom_size + 3 * gb);
+      // contacts straight into the pair's LDS records
+      n = narrow(m, m.geom_type[ga], m.geom_type[gb], pos1, mat1, sz1, pos2, mat2, sz2, margin,
+                 LdsConSinkT<real>{pcon + 14 * p});
+    }
+    pcnt[p] = n;
+  }
+  TSYNC();
+  // ordered compaction with the oracle's truncation at nconmax
+  const int lim = m.nconmax < m.maxcon ? m.nconmax : m.maxcon;
+  // offsets as ballot prefix counts when nothing is truncated (n <= 2 per pair),
+  // else the oracle's loop on lane 0
+  bool par = X.npair <= TEAM_SIZE;
+  if (par) {
+    const int t = T.tid;
+    const int n = t < X.npair ? pcnt[t] : 0;
+    const unsigned long long b0 = __ballot(n & 1), b1 = __ballot(n & 2);
+    const int total = __popcll(b0) + 2 * __popcll(b1);
+    par = total <= lim && __ballot(n > 3) == 0ull;
+    if (par) {
+      const unsigned long long below = t < 64 ? (1ull << t) - 1 : ~0ull;
+      if (t < X.npair) pcnt[t] = ((__popcll(b0 & below) + 2 * __popcll(b1 & below)) << 8) | n;
+      if (t == 0) T.iw[L.ncon] = total;
+    }
+  }
+  if (!par && T.tid == 0) {
+    int ncon = 0;
+    for (int p = 0; p < X.npair; p++) {
+      int n = pcnt[p];
+      int take = 0;
+      for (int k = 0; k < n; k++)
+        if (ncon + take < lim) take++;
+      pcnt[p] = (ncon << 8) | take;  // offset, count
+      ncon += take;
+    }
+    T.iw[L.ncon] = ncon;
+  }
+  TSYNC();
+  FOR_T(e, 2 * X.npair) {
+    int p = e >> 1, k = e & 1;
+    int off = pcnt[p] >> 8, take = pcnt[p] & 255;
+    if (k < take) {
+      int g1 = X.pair[2 * p], g2 = X.pair[2 * p + 1];
+      int ga = g1, gb = g2;
+      if (m.geom_type[g1] > m.geom_type[g2]) { ga = g2; gb = g1; }
+      real margin = maxd(m.geom_margin[g1], m.geom_margin[g2]);
+      real gap = maxd(m.geom_gap[ga], m.geom_gap[gb]);
+      real s1 = m.geom_solmix[ga], s2 = m.geom_solmix[gb], mix;
+      if (s1 < MINVAL && s2 < MINVAL) mix = 0.5;
+      else if (s1 < MINVAL) mix = 0;
+      else if (s2 < MINVAL) mix = 1;
+      else mix = s1 / (s1 + s2);
+      const real* pc = pcon + 14 * p + 7 * k;
+      real* c = con + CON_ND * (off + k);
+      real fr[9];
+      fr[0] = pc[4]; fr[1] = pc[5]; fr[2] = pc[6];
+      make_frame(fr);
+      c[CON_DIST] = pc[0];
+      c[CON_POS] = pc[1]; c[CON_POS + 1] = pc[2]; c[CON_POS + 2] = pc[3];
+      for (int r = 0; r < 9; r++) c[CON_FRAME + r] = fr[r];
+      c[CON_INCLM] = margin - gap;
+      real f0 = maxd(m.geom_friction[3 * ga], m.geom_friction[3 * gb]);
+      real f1 = maxd(m.geom_friction[3 * ga + 1], m.geom_friction[3 * gb + 1]);
+      real f2 = maxd(m.geom_friction[3 * ga + 2], m.geom_friction[3 * gb + 2]);
+      c[CON_FRIC] = f0; c[CON_FRIC + 1] = f0; c[CON_FRIC + 2] = f1; c[CON_FRIC + 3] = f2; c[CON_FRIC + 4] = f2;
+      for (int r = 0; r < 2; r++)
+        c[CON_SOLREF + r] = mix * m.geom_solref[2 * ga + r] + (1 - mix) * m.geom_solref[2 * gb + r];
+      for (int r = 0; r < 5; r++)
+        c[CON_SOLIMP + r] = mix * m.geom_solimp[5 * ga + r] + (1 - mix) * m.geom_solimp[5 * gb + r];
+      int cd1 = m.geom_condim[ga], cd2 = m.geom_condim[gb];
+      int* ci = coni + CON_NI * (off + k);
+      ci[CONI_DIM] = cd1 > cd2 ? cd1 : cd2;
+      ci[CONI_G1] = ga;
+      ci[CONI_G2] = gb;
+      ci[CONI_EFCADR] = -1;
+    }
+  }
+  TSYNC();
+}
+
+// make_constraint, in pieces the two-wave rollout schedules separately
+// (step_dual_split); make_constraint() runs them in the oracle's order.
+
+// which limit sides are violated (bit 0 lower, bit 1 upper): qpos only
+__device__ inline void mc_limit_masks(const auto& m, const auto& L, const auto& C, const Team& T) {
+  real* qpos = T.w + L.qpos;
+  int* jcnt = T.ci + C.jcnt;
+  FOR_T(j, m.njnt) {
+    int type = m.jnt_type[j], mask = 0;
+    if (m.jnt_limited[j] && (type == JNT_SLIDE || type == JNT_HINGE)) {
+      real value = qpos[m.jnt_qposadr[j]];
+      for (int side = -1; side <= 1; side += 2) {
+        real dist = side * (m.jnt_range[2 * j + (side + 1) / 2] - value);
+        if (dist < m.jnt_margin[j]) mask |= (side < 0 ? 1 : 2);
+      }
+    }
+    jcnt[j] = mask;
+  }
+}
+
+// contact jacobians in the contact frame: one lane per (contact, dof)
+__device__ inline void mc_contact_jac(const auto& m, const auto& L, const auto& X, const Team& T) {
+  const int nv = m.nv;
+  real* con = T.w + L.con;
+  int* coni = T.iw + L.coni;
+  real* jc = T.w + L.jc;
+  real* scom = T.w + L.scom;
+  real* cdof = T.w + L.cdof;
+  const int ncon = T.iw[L.ncon];
+  FOR_T(e, ncon * nv) {
+    int c = e / nv, k = e % nv;
+    const real* cc = con + CON_ND * c;
+    int b1 = m.geom_bodyid[coni[CON_NI * c + CONI_G1]], b2 = m.geom_bodyid[coni[CON_NI * c + CONI_G2]];
+    real pos[3] = {cc[CON_POS], cc[CON_POS + 1], cc[CON_POS + 2]}, a[3], b[3];
+    jac_col(m, X, scom, cdof, pos, b1, k, a);
+    jac_col(m, X, scom, cdof, pos, b2, k, b);
+    b[0] -= a[0]; b[1] -= a[1]; b[2] -= a[2];
+    for (int r = 0; r < 3; r++)
+      jc[(c * 3 + r) * nv + k] = cc[CON_FRAME + 3 * r] * b[0] + cc[CON_FRAME + 3 * r + 1] * b[1] +
+                                 cc[CON_FRAME + 3 * r + 2] * b[2];
+  }
+}
+
+// row allocation in the oracle's order (limits, then contacts).  When every
+// row fits (no njmax truncation) the offsets are prefix counts over ballots,
+// one lane per joint / contact; otherwise the oracle's loop on lane 0.
+// Returns whether the parallel branch ran (wave-uniform).
+__device__ inline bool mc_alloc(const auto& m, const auto& L, const auto& C, const Team& T) {
+  int* coni = T.iw + L.coni;
+  int* efc_type = T.iw + L.efc_type;
+  int* efc_id = T.iw + L.efc_id;
+  int* rsub = T.ci + C.rsub;
+  int* jcnt = T.ci + C.jcnt;
+  const int ncon = T.iw[L.ncon];
+  const int njmax = m.njmax < m.maxefc ? m.njmax : m.maxefc;
+  bool par = m.njnt <= TEAM_SIZE && ncon <= TEAM_SIZE;
+  if (par) {
+    const int t = T.tid;
+    const int jm = t < m.njnt ? jcnt[t] : 0;
+    const unsigned long long blo = __ballot(jm & 1), bhi = __ballot(jm & 2);
+    const int nlim = __popcll(blo) + __popcll(bhi);
+    const int dim = t < ncon ? coni[CON_NI * t + CONI_DIM] : 0;
+    const int nrow = t < ncon ? (dim == 1 ? 1 : 2 * (dim - 1)) : 0;
+    int before = 0, total = 0;  // contact rows of lanes below t, of all lanes
+    for (int b = 0; b < 5; b++) {
+      const unsigned long long bb = __ballot((nrow >> b) & 1);
+      before += (int)__builtin_amdgcn_mbcnt_hi((unsigned)(bb >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)bb, 0u)) << b;
+      total += __popcll(bb) << b;
+    }
+    par = nrow < 32 && __ballot(nrow >= 32) == 0ull && nlim + total <= njmax;
+    if (par) {
+      if (t < m.njnt && jm) {
+        const unsigned long long below = (1ull << t) - 1;
+        int r = __popcll(blo & below) + __popcll(bhi & below);
+        for (int side = -1; side <= 1; side += 2) {
+          if (!(jm & (side < 0 ? 1 : 2))) continue;
+          efc_type[r] = C_LIMIT;
+          efc_id[r] = t;
+          rsub[r] = side;
+          r++;
+        }
+      }
+      if (t < ncon) {
+        const int r0 = nlim + before;
+        coni[CON_NI * t + CONI_EFCADR] = r0;
+        for (int r = 0; r < nrow; r++) {
+          efc_type[r0 + r] = dim == 1 ? C_FRICTIONLESS : C_PYRAMIDAL;
+          efc_id[r0 + r] = t;
+          rsub[r0 + r] = r;
+        }
+      }
+      if (t == 0) T.iw[L.nefc] = nlim + total;
+    }
+  }
+  if (!par && T.tid == 0) {
+    int nefc = 0;
+    for (int j = 0; j < m.njnt; j++) {
+      int mask = jcnt[j];
+      for (int side = -1; side <= 1; side += 2) {
+        if (!(mask & (side < 0 ? 1 : 2))) continue;
+        if (nefc + 1 > njmax) break;
+        efc_type[nefc] = C_LIMIT;
+        efc_id[nefc] = j;
+        rsub[nefc] = side;
+        nefc++;
+      }
+    }
+    for (int c = 0; c < ncon; c++) {
+      int dim = coni[CON_NI * c + CONI_DIM];
+      int nrow = dim == 1 ? 1 : 2 * (dim - 1);
+      if (nefc + nrow > njmax) continue;
+      coni[CON_NI * c + CONI_EFCADR] = nefc;
+      for (int r = 0; r < nrow; r++) {
+        efc_type[nefc] = dim == 1 ? C_FRICTIONLESS : C_PYRAMIDAL;
+        efc_id[nefc] = c;
+        rsub[nefc] = r;
+        nefc++;
+      }
+    }
+    T.iw[L.nefc] = nefc;
+  }
+  return par;
+}
+
+// jacobian rows and row parameters (impedance, K/B, D) of rows [r0, r1)
+__device__ inline void mc_rows(const auto& m, const auto& L, const auto& C, const Team& T, int r0, int r1) {
+  const int nv = m.nv;
+  real* qpos = T.w + L.qpos;
+  real* con = T.w + L.con;
+  real* efcJ = T.w + L.efc_J;
+  real* efc_pos = T.w + L.efc_pos;
+  real* efc_margin = T.w + L.efc_margin;
+  real* efc_D = T.w + L.efc_D;
+  real* KBIP = T.w + L.efc_KBIP;
+  int* coni = T.iw + L.coni;
+  int* efc_type = T.iw + L.efc_type;
+  int* efc_id = T.iw + L.efc_id;
+  int* rsub = T.ci + C.rsub;
+  real* jc = T.w + L.jc;
+  FOR_T(e0, (r1 - r0) * nv) {
+    const int e = e0 + r0 * nv;
+    int i = e / nv, k = e % nv;
+    int type = efc_type[i], id = efc_id[i], sub = rsub[i];
+    real v;
+    if (type == C_LIMIT) {
+      v = (k == m.jnt_dofadr[id]) ? (real)(-sub) : 0.0;
+    } else if (type == C_FRICTIONLESS) {
+      v = jc[(id * 3 + 0) * nv + k];
+    } else {
+      int kk = sub / 2 + 1;
+      real f = con[CON_ND * id + CON_FRIC + kk - 1];
+      real j0 = jc[(id * 3 + 0) * nv + k], jk = jc[(id * 3 + kk) * nv + k];
+      v = (sub & 1) ? j0 + (-f) * jk : j0 + f * jk;
+    }
+    efcJ[i * nv + k] = v;
+  }
+  FOR_T(i0, r1 - r0) {
+    const int i = i0 + r0;
+    int type = efc_type[i], id = efc_id[i];
+    real solref[2], solimp[5], dA, imp, tc, dr, dmax, K, B, pos, mar;
+    if (type == C_LIMIT) {
+      real value = qpos[m.jnt_qposadr[id]];
+      int side = rsub[i];
+      pos = side * (m.jnt_range[2 * id + (side + 1) / 2] - value);
+      mar = m.jnt_margin[id];
+      ldm<2>(solref, m.jnt_solref + 2 * id);
+      ldm<5>(solimp, m.jnt_solimp + 5 * id);
+      dA = m.dof_invweight0[m.jnt_dofadr[id]];
+    } else {
+      const real* cc = con + CON_ND * id;
+      int b1 = m.geom_bodyid[coni[CON_NI * id + CONI_G1]], b2 = m.geom_bodyid[coni[CON_NI * id + CONI_G2]];
+      real tran = m.body_invweight0[2 * b1] + m.body_invweight0[2 * b2];
+      pos = cc[CON_DIST];
+      mar = cc[CON_INCLM];
+      ldm<2>(solref, cc + CON_SOLREF);
+      ldm<5>(solimp, cc + CON_SOLIMP);
+      if (type == C_FRICTIONLESS) {
+        dA = tran;
+      } else {
+        int k = (i - coni[CON_NI * id + CONI_EFCADR]) / 2;
+        real f = cc[CON_FRIC + k];
+        dA = tran + f * f * tran;
+      }
+    }
+    efc_pos[i] = pos;
+    efc_margin[i] = mar;
+    imp = get_impedance(solimp, pos, mar);
+    dmax = clipd(solimp[1], MINIMP, MAXIMP);
+    tc = solref[0];
+    dr = solref[1];
+    if (tc > 0) {
+      if (tc < 2 * m.opt_timestep) tc = 2 * m.opt_timestep;
+      K = 1 / (dmax * dmax * tc * tc * dr * dr);
+      B = 2 / (dmax * tc);
+    } else {
+      K = -tc / (dmax * dmax);
+      B = -dr / dmax;
+    }
+    KBIP[L.kstr * i] = K;
+    KBIP[L.kstr * i + 1] = B;
+    KBIP[L.kstr * i + 2] = imp;
+    real R = maxd(MINVAL, (1 - imp) * dA / imp);
+    efc_D[i] = 1 / R;
+  }
+}
+
+__device__ inline void make_constraint(const auto& m, const auto& L, const auto& C, const auto& X,
+                                       const Team& T) {
+  mc_limit_masks(m, L, C, T);
+  mc_contact_jac(m, L, X, T);
+  TSYNC();
+  (void)mc_alloc(m, L, C, T);
+  TSYNC();
+  mc_rows(m, L, C, T, 0, T.iw[L.nefc]);
+  TSYNC();
+}
+
+// The limit rows -- the first rows of the constraint arrays -- from qpos alone,
+// ahead of make_constraint (two-wave rollout, beside the kinematics): masks,
+// allocation and rows [0, nlim) exactly as make_constraint computes them.
+// Returns nlim (-1 when the limits alone exceed njmax: make_constraint then
+// takes its serial branch and computes every row).
+__device__ inline int limit_rows_pre(const auto& m, const auto& L, const auto& C, const Team& T) {
+  mc_limit_masks(m, L, C, T);
+  TSYNC();
+  if (m.njnt > TEAM_SIZE) return -1;
+  const int njmax = m.njmax < m.maxefc ? m.njmax : m.maxefc;
+  int* efc_type = T.iw + L.efc_type;
+  int* efc_id = T.iw + L.efc_id;
+  int* rsub = T.ci + C.rsub;
+  const int t = T.tid;
+  const int jm = t < m.njnt ? T.ci[C.jcnt + t] : 0;
+  const unsigned long long blo = __ballot(jm & 1), bhi = __ballot(jm & 2);
+  const int nlim = __popcll(blo) + __popcll(bhi);
+  if (nlim > njmax) return -1;
+  if (t < m.njnt && jm) {
+    const unsigned long long below = (1ull << t) - 1;
+    int r = __popcll(blo & below) + __popcll(bhi & below);
+    for (int side = -1; side <= 1; side += 2) {
+      if (!(jm & (side < 0 ? 1 : 2))) continue;
+      efc_type[r] = C_LIMIT;
+      efc_id[r] = t;
+      rsub[r] = side;
+      r++;
+    }
+  }
+  TSYNC();
+  mc_rows(m, L, C, T, 0, nlim);
+  TSYNC();
+  return nlim;
+}
+
+// transmission: actuator_moment (joint transmissions)
+__device__ inline void transmission(const auto& m, const auto& L, const Team& T) {
+  real* amom = T.w + L.amom;
+  FOR_T(e, m.nu * m.nv) {
+    int i = e / m.nv, k = e % m.nv;
+    int j = m.actuator_trnid[i];
+    amom[e] = (k == m.jnt_dofadr[j]) ? m.actuator_gear[i] : 0.0;
+  }
+}
+
+__device__ inline void fwd_position(const auto& m, const auto& L, const auto& C, const auto& X,
+                                    const Team& T) {
+  kinematics(m, L, C, T);
+  STAMP(14 - 14 + 0);
+  com_pos(m, L, T);
+  STAMP(1);
+  transmission(m, L, T);
+  crb(m, L, C, X, T);
+  STAMP(2);
+  factor_ld(m, X, T, T.w + L.qM, T.w + L.qLD, T.w + L.qLDinv, T.c + C.ftmp);
+  STAMP(3);
+  collision(m, L, C, X, T);
+  STAMP(4);
+  make_constraint(m, L, C, X, T);
+  STAMP(5);
+}
+
+// ------------------------------------------------------ velocity stage ---
+// part 0: the whole stage; 1: com velocities + RNE (primary wave of a
+// two-wave step); 2: passive forces + constraint reference (helper wave)
+// passive forces: one lane per dof (hinge/slide springs; ball/free rejected on the host)
+__device__ inline void passive_forces(const auto& m, const auto& L, const Team& T) {
+  real* qvel = T.w + L.qvel;
+  real* qpos = T.w + L.qpos;
+  real* qp = T.w + L.qfrc_passive;
+  FOR_T(i, m.nv) {
+    int j = m.dof_jntid[i];
+    real v = 0;
+    real k = m.jnt_stiffness[j];
+    if (k != 0) {
+      int pa = m.jnt_qposadr[j];
+      v = -k * (qpos[pa] - m.qpos_spring[pa]);
+    }
+    v -= m.dof_damping[i] * qvel[i];
+    qp[i] = v;
+  }
+}
+
+// constraint velocities and reference accelerations: one lane per row
+__device__ inline void constraint_ref(const auto& m, const auto& L, const Team& T) {
+  const int nv = m.nv;
+  real* qvel = T.w + L.qvel;
+  const int nefc = T.iw[L.nefc];
+  real* KBIP = T.w + L.efc_KBIP;
+  real* efc_vel = T.w + L.efc_vel;
+  real* aref = T.w + L.efc_aref;
+  real* J = T.w + L.efc_J;
+  real* pos = T.w + L.efc_pos;
+  real* mar = T.w + L.efc_margin;
+  FOR_T(i, nefc) {
+    real k0 = KBIP[L.kstr * i], k1 = KBIP[L.kstr * i + 1], k2 = KBIP[L.kstr * i + 2];
+    real v = tdot(J + i * nv, qvel, nv);
+    efc_vel[i] = v;
+    aref[i] = -k1 * v - k0 * k2 * (pos[i] - mar[i]);
+  }
+}
+
+// actuator forces and qfrc_actuator = moment' * force (the first part of the
+// acceleration stage; ctrl and the joint transmissions only)
+__device__ inline void actuator_force(const auto& m, const auto& L, const Team& T) {
+  const int nv = m.nv, nu = m.nu;
+  real* ctrl = T.w + L.ctrl;
+  real* af = T.w + L.afrc;
+  real* amom = T.w + L.amom;
+  real* qa = T.w + L.qfrc_act;
+  FOR_T(i, nu) {
+    real c = ctrl[i], f;
+    if (m.actuator_ctrllimited[i]) c = clipd(c, m.actuator_ctrlrange[2 * i], m.actuator_ctrlrange[2 * i + 1]);
+    f = m.actuator_gainprm[i] * c;
+    if (m.actuator_forcelimited[i]) f = clipd(f, m.actuator_forcerange[2 * i], m.actuator_forcerange[2 * i + 1]);
+    af[i] = f;
+  }
+  TSYNC();
+  FOR_T(j, nv) {
+    real s = 0;
+    for (int i = 0; i < nu; i++) s += amom[i * nv + j] * af[i];
+    qa[j] = s;
+  }
+}
+
+__device__ inline void fwd_velocity(const auto& m, const auto& L, const auto& C, const Team& T, int part = 0) {
+  const int nv = m.nv, nb = m.nbody;
+  real* cvelw = T.w + L.cvel;
+  real* cdof = T.w + L.cdof;
+  real* cdd = T.w + L.cdof_dot;
+  real* qvel = T.w + L.qvel;
+  real* qpos = T.w + L.qpos;
+  if (part != 2) {
+  // com velocities.  The recursion cvel_i = cvel_parent + sum_dof cdof*qvel is
+  // component-wise, so it runs as 6 parallel chains (lane k = component k);
+  // each dof's pre-update cvel is recorded (s_con) and the cdof_dot cross
+  // products, which mix components but feed nothing back, follow one lane per
+  // dof.  Per component the operations are the oracle's, in its order.
+  real* cvb = T.w + L.s_con;  // 6 x nv: cvel seen by each dof
+  FOR_T(k, 6) {
+    cvelw[k] = 0;
+    real cv = 0;
+    int prev = 0;
+    for (int i = 1; i < nb; i++) {
+      const int bda = m.body_dofadr[i], pid = m.body_parentid[i];
+      if (pid != prev) cv = cvelw[6 * pid + k];
+      for (int j = 0; j < m.body_dofnum[i]; j++) {
+        const int type = m.jnt_type[m.dof_jntid[bda + j]];
+        if (type == JNT_FREE) {
+          real t = 0;
+          for (int q = 0; q < 3; q++) t += cdof[6 * (bda + q) + k] * qvel[bda + q];
+          cv += t;
+          j += 3;
+        }
+        if (type == JNT_FREE || type == JNT_BALL) {
+          for (int q = 0; q < 3; q++) cvb[6 * (bda + j + q) + k] = cv;
+          real t = 0;
+          for (int q = 0; q < 3; q++) t += cdof[6 * (bda + j + q) + k] * qvel[bda + j + q];
+          cv += t;
+          j += 2;
+        } else {
+          cvb[6 * (bda + j) + k] = cv;
+          real t = 0;
+          t += cdof[6 * (bda + j) + k] * qvel[bda + j];
+          cv += t;
+        }
+      }
+      cvelw[6 * i + k] = cv;
+      prev = i;
+    }
+  }
+  TSYNC();
+  FOR_T(d, nv) {
+    const int jid = m.dof_jntid[d];
+    if (m.jnt_type[jid] == JNT_FREE && d < m.jnt_dofadr[jid] + 3) {
+      for (int q = 0; q < 6; q++) cdd[6 * d + q] = 0;
+    } else {
+      real cv[6], cd[6], r[6];
+      ldm<6>(cv, cvb + 6 * d);
+      ldm<6>(cd, cdof + 6 * d);
+      cross_motion(r, cv, cd);
+      for (int q = 0; q < 6; q++) cdd[6 * d + q] = r[q];
+    }
+  }
+  }
+  if (part != 1) {
+    passive_forces(m, L, T);
+    constraint_ref(m, L, T);
+  }
+  TSYNC();
+  if (part == 2) return;
+  // RNE: per (body, component) dof-velocity terms, then the chain per component
+  real* rt = T.c + C.rtmp;
+  real* cacc = T.w + L.s_rne;
+  real* cfrc = cacc + 6 * nb;
+  FOR_T(e, 6 * nb) {
+    int i = e / 6, k = e % 6;
+    if (i > 0) {
+      int bda = m.body_dofadr[i], nd = m.body_dofnum[i];
+      real sum = 0;
+      for (int j = 0; j < nd; j++) sum += cdd[6 * (bda + j) + k] * qvel[bda + j];
+      rt[e] = nd ? sum : 0;
+    }
+  }
+  TSYNC();
+  FOR_T(k, 6) {
+    cacc[k] = k < 3 ? 0.0 : (k == 3 ? -m.opt_gravity0 : (k == 4 ? -m.opt_gravity1 : -m.opt_gravity2));
+    for (int i = 1; i < nb; i++) cacc[6 * i + k] = cacc[6 * m.body_parentid[i] + k] + rt[6 * i + k];
+  }
+  TSYNC();
+  real* cinert = T.w + L.cinert;
+  FOR_T(i, nb) {
+    if (i == 0) {
+      for (int k = 0; k < 6; k++) cfrc[k] = 0;
+    } else {
+      real ci[10], a[6], f[6], cv[6], tmp[6], tmp1[6];
+      ldm<10>(ci, cinert + 10 * i);
+      ldm<6>(a, cacc + 6 * i);
+      ldm<6>(cv, cvelw + 6 * i);
+      mul_inert_vec(f, ci, a);
+      mul_inert_vec(tmp, ci, cv);
+      cross_force(tmp1, cv, tmp);
+      for (int k = 0; k < 6; k++) cfrc[6 * i + k] = f[k] + tmp1[k];
+    }
+  }
+  TSYNC();
+  FOR_T(k, 6) {
+    for (int i = nb - 1; i > 0; i--) {
+      int p = m.body_parentid[i];
+      if (p) cfrc[6 * p + k] += cfrc[6 * i + k];
+    }
+  }
+  TSYNC();
+  real* bias = T.w + L.qfrc_bias;
+  FOR_T(i, nv) bias[i] = tdot(cdof + 6 * i, cfrc + 6 * m.dof_bodyid[i], 6);
+  TSYNC();
+}
+
+// -------------------------------------------------- acceleration stage ---
+// act_pre: actuator_force() already ran (two-wave rollout: on the helper wave)
+__device__ inline void fwd_acceleration(const auto& m, const auto& L, const auto& X, const Team& T,
+                                        bool act_pre = false) {
+  const int nv = m.nv, nu = m.nu;
+  real* ctrl = T.w + L.ctrl;
+  real* af = T.w + L.afrc;
+  real* amom = T.w + L.amom;
+  real* qa = T.w + L.qfrc_act;
+  if (!act_pre) {
+    FOR_T(i, nu) {
+      real c = ctrl[i], f;
+      if (m.actuator_ctrllimited[i]) c = clipd(c, m.actuator_ctrlrange[2 * i], m.actuator_ctrlrange[2 * i + 1]);
+      f = m.actuator_gainprm[i] * c;
+      if (m.actuator_forcelimited[i]) f = clipd(f, m.actuator_forcerange[2 * i], m.actuator_forcerange[2 * i + 1]);
+      af[i] = f;
+    }
+    TSYNC();
+  }
+  real* sm = T.w + L.qfrc_smooth;
+  real* qp = T.w + L.qfrc_passive;
+  real* qb = T.w + L.qfrc_bias;
+  real* qap = T.w + L.qfrc_applied;
+  real* xf = T.w + L.xfrc_applied;
+  real* xipos = T.w + L.xipos;
+  real* scom = T.w + L.scom;
+  real* cdof = T.w + L.cdof;
+  real* qs = T.w + L.qacc_smooth;
+  // any nonzero xfrc_applied on a non-world body? (else the per-body loop below
+  // skips every body, so leaving it out changes nothing)
+  unsigned long long fmask = 0;
+  for (int i0 = 6; i0 < 6 * m.nbody; i0 += TEAM_SIZE) fmask |= __ballot(i0 + T.tid < 6 * m.nbody && xf[i0 + T.tid] != 0);
+  const bool anyf = fmask != 0ull;
+  FOR_T(j, nv) {
+    real s;
+    if (act_pre) {
+      s = qa[j];
+    } else {
+      s = 0;
+      for (int i = 0; i < nu; i++) s += amom[i * nv + j] * af[i];
+      qa[j] = s;
+    }
+    real v = qp[j] - qb[j];
+    v += qap[j];
+    v += s;
+    // xfrc_applied: jac columns of dof j at each loaded body's COM
+    for (int b = 1; anyf && b < m.nbody; b++) {
+      real f[6];
+      ldm<6>(f, xf + 6 * b);
+      if (f[0] == 0 && f[1] == 0 && f[2] == 0 && f[3] == 0 && f[4] == 0 && f[5] == 0) continue;
+      real p[3] = {xipos[3 * b], xipos[3 * b + 1], xipos[3 * b + 2]}, jp[3], jr[3] = {0, 0, 0};
+      jac_col(m, X, scom, cdof, p, b, j, jp);
+      int bb = b;
+      while (bb && !m.body_dofnum[bb]) bb = m.body_parentid[bb];
+      if (bb && X.isanc[(m.body_dofadr[bb] + m.body_dofnum[bb] - 1) * nv + j]) {
+        jr[0] = cdof[6 * j]; jr[1] = cdof[6 * j + 1]; jr[2] = cdof[6 * j + 2];
+      }
+      real t1 = jp[0] * f[0] + jp[1] * f[1] + jp[2] * f[2];
+      real t2 = jr[0] * f[3] + jr[1] * f[4] + jr[2] * f[5];
+      v += t1 + t2;
+    }
+    sm[j] = v;
+    qs[j] = v;
+  }
+  TSYNC();
+  solve_ld(m, X, T, T.w + L.qLD, T.w + L.qLDinv, qs);
+}
+
+// constraint cost of residuals `jar`; force/state per row, qfrc_constraint per dof
+__device__ inline real constraint_update(const auto& m, const auto& L, const auto& C, const Team& T,
+                                           const real* jar) {
+  const int nv = m.nv, ne = T.iw[L.nefc];
+  real* D = T.w + L.efc_D;
+  real* force = T.w + L.efc_force;
+  real* J = T.w + L.efc_J;
+  real* qc = T.w + L.qfrc_con;
+  int* state = T.iw + L.efc_state;
+  real* term = T.c + C.cterm;
+  FOR_T(i, ne) {
+    real jr = jar[i];
+    if (jr < 0) {
+      real Di = D[i];
+      force[i] = -Di * jr;
+      state[i] = 1;
+      term[i] = 0.5 * Di * jr * jr;
+    } else {
+      force[i] = 0;
+      state[i] = 0;
+    }
+  }
+  TSYNC();
+  FOR_T(j, nv) {
+    real s = 0;
+    for (int i = 0; i < ne; i++) s += J[i * nv + j] * force[i];
+    qc[j] = s;
+  }
+  if (T.tid == 0) {
+    real cost = 0;
+    for (int i = 0; i < ne; i++)
+      if (state[i]) cost += term[i];
+    T.c[C.bc] = cost;
+  }
+  TSYNC();
+  return T.c[C.bc];
+}
+
+__device__ inline void hessian_factor(const auto& m, const auto& L, const auto& C, const Team& T,
+                                      real* H) {
+  const int nv = m.nv, ne = T.iw[L.nefc];
+  real* J = T.w + L.efc_J;
+  real* D = T.w + L.efc_D;
+  real* qM = T.w + L.qM;
+  int* state = T.iw + L.efc_state;
+  FOR_T(e, nv * nv) {
+    int r = e / nv, c = e % nv;
+    if (c <= r) {
+      real h = 0;
+      for (int i = 0; i < ne; i++)
+        if (state[i]) h += J[i * nv + r] * D[i] * J[i * nv + c];
+      H[e] = qM[e] + h;
+    }
+  }
+  TSYNC();
+  if (nv <= RMAX) {
+    cholesky_rows(nv, T.tid, H);
+    return;
+  }
+  if (nv <= SERIAL_NV) {
+    if (T.tid == 0) {
+      for (int j = 0; j < nv; j++) {
+        real t = H[j * nv + j];
+        if (j) t -= tdot(H + j * nv, H + j * nv, j);
+        if (t < MINVAL) t = MINVAL;
+        H[j * nv + j] = sqrt(t);
+        t = 1 / H[j * nv + j];
+        for (int i = j + 1; i < nv; i++) H[i * nv + j] = (H[i * nv + j] - tdot(H + i * nv, H + j * nv, j)) * t;
+      }
+    }
+    TSYNC();
+    return;
+  }
+  for (int j = 0; j < nv; j++) {
+    if (T.tid == 0) {
+      real t = H[j * nv + j];
+      if (j) t -= tdot(H + j * nv, H + j * nv, j);
+      if (t < MINVAL) t = MINVAL;
+      H[j * nv + j] = sqrt(t);
+      T.c[C.bc + 1] = 1 / H[j * nv + j];
+    }
+    TSYNC();
+    const real tinv = T.c[C.bc + 1];
+    FOR_T(i, nv) {
+      if (i > j) H[i * nv + j] = (H[i * nv + j] - tdot(H + i * nv, H + j * nv, j)) * tinv;
+    }
+    TSYNC();
+  }
+}
+
+__device__ inline void solver_newton(const auto& m, const auto& L, const auto& C, const Team& T,
+                                     int maxiter, real tol) {
+  const int nv = m.nv, ne = T.iw[L.nefc];
+  const real scale = 1 / (m.stat_meaninertia * (nv > 1 ? nv : 1));
+  real* s = T.w + L.s_newton;
+  real *Ma = s, *grad = s + nv, *search = s + 2 * nv, *Mv = s + 3 * nv, *H = s + 4 * nv;
+  real* jar = s + 4 * nv + nv * nv;
+  real* Jv = jar + ne;
+  real* qM = T.w + L.qM;
+  real* qacc = T.w + L.qacc;
+  real* J = T.w + L.efc_J;
+  real* aref = T.w + L.efc_aref;
+  real* qfs = T.w + L.qfrc_smooth;
+  real* qas = T.w + L.qacc_smooth;
+  real* qc = T.w + L.qfrc_con;
+  real* Dv = T.w + L.efc_D;
+  real* bc = T.c + C.bc;
+  FOR_T(i, nv) Ma[i] = tdot(qM + i * nv, qacc, nv);
+  FOR_T(i, ne) jar[i] = tdot(J + i * nv, qacc, nv) - aref[i];
+  TSYNC();
+  real ccost = constraint_update(m, L, C, T, jar);
+  if (T.tid == 0) {
+    real g = 0;
+    for (int j = 0; j < nv; j++) g += (Ma[j] - qfs[j]) * (qacc[j] - qas[j]);
+    bc[2] = 0.5 * g + ccost;
+  }
+  FOR_T(j, nv) grad[j] = (Ma[j] - qfs[j]) - qc[j];
+  TSYNC();
+  real cost = bc[2];
+  hessian_factor(m, L, C, T, H);
+  int iter = 0;
+#ifdef ILQG_STAMPS
+  if (T.tid == 0) atomicAdd(&g_newton_calls, 1ull);
+#endif
+  while (iter < maxiter) {
+    // search = -H^-1 grad ; line search ; all on lane 0 except the parallel products
+    if (nv <= RMAX) {
+      chol_solve_rows(nv, T.tid, H, grad, search);
+    } else {
+      if (T.tid == 0) {
+        for (int i = 0; i < nv; i++) search[i] = grad[i];
+        for (int i = 0; i < nv; i++) {
+          if (i) search[i] -= tdot(H + i * nv, search, i);
+          search[i] /= H[i * nv + i];
+        }
+        for (int i = nv - 1; i >= 0; i--) {
+          for (int j = i + 1; j < nv; j++) search[i] -= H[j * nv + i] * search[j];
+          search[i] /= H[i * nv + i];
+        }
+        for (int j = 0; j < nv; j++) search[j] = -search[j];
+      }
+      TSYNC();
+    }
+    STAMP(14);
+    FOR_T(i, nv) Mv[i] = tdot(qM + i * nv, search, nv);
+    FOR_T(i, ne) Jv[i] = tdot(J + i * nv, search, nv);
+    TSYNC();
+    STAMP(15);
+    if (T.tid == 0) {
+      real alpha = 0;
+      real snorm = sqrt(tdot(search, search, nv));
+      if (!(snorm < MINVAL)) {
+        real g1 = 0, g2 = 0, d1, d2, lo = 0, hi = -1;
+        for (int j = 0; j < nv; j++) g1 += search[j] * (Ma[j] - qfs[j]);
+        for (int j = 0; j < nv; j++) g2 += search[j] * Mv[j];
+        auto eval = [&](real a) {
+          d1 = g1 + g2 * a;
+          d2 = g2;
+          for (int i = 0; i < ne; i++) {
+            real jv = Jv[i];
+            real x = jar[i] + a * jv;
+            if (x < 0) {
+              real Di = Dv[i];
+              d1 += Di * x * jv;
+              d2 += Di * jv * jv;
+            }
+          }
+        };
+        eval(0.0);
+        if (!(d1 >= 0)) {  // oracle: return 0 iff d1 >= 0 (a NaN proceeds)
+          real gtol = LS_TOL * fabs(d1);
+          for (int it = 0; it < LS_ITER; it++) {
+            real anew = alpha - d1 / d2;
+            if (hi >= 0 && !(anew > lo && anew < hi)) anew = 0.5 * (lo + hi);
+            alpha = anew;
+            eval(alpha);
+            if (fabs(d1) < gtol) break;
+            if (d1 < 0) lo = alpha; else hi = alpha;
+          }
+        }
+      }
+      bc[3] = alpha;
+    }
+    TSYNC();
+    STAMP(16);
+    const real alpha = bc[3];
+    if (alpha == 0) break;
+    FOR_T(j, nv) {
+      qacc[j] += alpha * search[j];
+      Ma[j] += alpha * Mv[j];
+    }
+    FOR_T(i, ne) jar[i] += alpha * Jv[i];
+    TSYNC();
+    iter++;
+#ifdef ILQG_STAMPS
+    if (T.tid == 0) atomicAdd(&g_newton_iters, 1ull);
+#endif
+    STAMP(17);
+    real oldcost = cost;
+    ccost = constraint_update(m, L, C, T, jar);
+    FOR_T(j, nv) grad[j] = (Ma[j] - qfs[j]) - qc[j];
+    TSYNC();
+    if (T.tid == 0) {
+      real g = 0;
+      for (int j = 0; j < nv; j++) g += (Ma[j] - qfs[j]) * (qacc[j] - qas[j]);
+      real c2 = 0.5 * g + ccost;
+      real improvement = scale * (oldcost - c2);
+      real gradient = scale * sqrt(tdot(grad, grad, nv));
+      bc[2] = c2;
+      bc[4] = (improvement < tol || gradient < tol) ? 1.0 : 0.0;
+    }
+    TSYNC();
+    STAMP(18);
+    cost = bc[2];
+    if (bc[4] != 0) break;
+    hessian_factor(m, L, C, T, H);
+    STAMP(19);
+  }
+}
+
+
+// ---------------------------------------------------------------------------
+// Newton solver, wave-parallel form for nefc <= 64 (one constraint row per
+// lane).  Every ordered reduction over rows (constraint cost, line-search
+// derivatives) keeps the oracle's row order: each lane forms its row's term,
+// then the terms are added in lane order through v_readlane.  A row that the
+// oracle skips contributes -0.0, the exact identity of IEEE addition.  The
+// Hessian factor is reused while the active set is unchanged: it is a
+// function of (qM, J, D, active set) only, so the reused factor is the one
+// the oracle recomputes, bit for bit.
+
+// s0 + v[lane 0] + v[lane 1] + ... + v[lane n-1], in that order
+__device__ __forceinline__ real lane_sum(real s0, real v, int n) {
+  for (int i = 0; i < n; i++) s0 += bcast(v, i);
+  return s0;
+}
+// the same ordered sum over the lanes of a (wave-uniform) mask only: lanes
+// outside it hold -0.0, and x + (-0.0) == x for every x, so skipping them is exact
+__device__ __forceinline__ real lane_sum_mask(real s0, real v, unsigned long long mask) {
+  for (unsigned long long mm = mask; mm; mm &= mm - 1) s0 += bcast(v, __builtin_ctzll(mm));
+  return s0;
+}
+
+// constraint_update for row registers: returns the cost (uniform) and the
+// active-row mask; with `full` also force/state and qfrc_constraint = J' force
+__device__ inline real cu_fast(const auto& m, const auto& L, const Team& T, real jr, real Di, bool full,
+                                 unsigned long long& mask, bool want_cost = true) {
+  const int nv = m.nv, ne = T.iw[L.nefc];
+  const int r = T.tid;
+  const bool row = r < ne;
+  const bool act = row && jr < 0;
+  if (full) {
+    real* force = T.w + L.efc_force;
+    int* state = T.iw + L.efc_state;
+    if (row) {
+      force[r] = act ? -Di * jr : 0.0;
+      state[r] = act ? 1 : 0;
+    }
+    TSYNC();
+    real* J = T.w + L.efc_J;
+    real* qc = T.w + L.qfrc_con;
+    // rows with zero force add J * 0 = +-0 to a sum that is never -0 (it starts
+    // at +0): skipping them is exact
+    const unsigned long long am = __ballot(act);
+    FOR_T(j, nv) {
+      real s = 0;
+      for (unsigned long long mm = am; mm; mm &= mm - 1) {
+        const int i = __builtin_ctzll(mm);
+        s += J[i * nv + j] * force[i];
+      }
+      qc[j] = s;
+    }
+    TSYNC();
+  }
+  mask = __ballot(act);
+  if (!want_cost) return 0.0;
+  const real tv = act ? 0.5 * Di * jr * jr : -0.0;
+  return lane_sum_mask(0.0, tv, mask);
+}
+
+// 0.5 * sum_j (Ma_j - qfs_j)(qacc_j - qas_j), every lane (uniform)
+__device__ inline real gauss_u(int nv, const real* Ma, const real* qfs, const real* qacc, const real* qas) {
+  real g = 0;
+  for (int j = 0; j < nv; j++) g += (Ma[j] - qfs[j]) * (qacc[j] - qas[j]);
+  return 0.5 * g;
+}
+
+// amask: the active rows (efc_state != 0) as a ballot, walked in ascending order
+__device__ inline void hessian_build_fast(const auto& m, const auto& L, const Team& T, real* H,
+                                          unsigned long long amask) {
+  const int nv = m.nv;
+  real* J = T.w + L.efc_J;
+  real* D = T.w + L.efc_D;
+  real* qM = T.w + L.qM;
+  FOR_T(e, nv * nv) {
+    int r = e / nv, c = e % nv;
+    if (c <= r) {
+      real h = 0;
+      for (unsigned long long mm = amask; mm; mm &= mm - 1) {
+        const int i = __builtin_ctzll(mm);
+        h += J[i * nv + r] * D[i] * J[i * nv + c];
+      }
+      H[e] = qM[e] + h;
+    }
+  }
+  TSYNC();
+}
+
+// The helper wave of a two-wave rollout team, beside the primary's
+// acceleration stage: everything of the Newton start that depends only on the
+// warm start -- jar and M*warm, its constraint cost, the full constraint update
+// (forces, states, qfrc_constraint) and the Hessian factor of its active set.
+// The primary then needs only the smooth start's cost to choose; from the warm
+// start (the common case) it goes straight to the first iteration.  Same
+// expressions as fwd_constraint_fast, on the other wave.
+__device__ inline void newton_warm_prep(const auto& m, const auto& L, const auto& C, const Team& T) {
+  const int nv = m.nv, ne = T.iw[L.nefc];
+  real* s = T.w + L.s_newton;
+  real *Ma = s, *H = s + 4 * nv;
+  real* jar = s + 4 * nv + nv * nv;
+  real* qM = T.w + L.qM;
+  real* warm = T.w + L.warm;
+  real* J = T.w + L.efc_J;
+  real* aref = T.w + L.efc_aref;
+  const int r = T.tid;
+  const bool row = r < ne;
+  const real Di = row ? T.w[L.efc_D + r] : 0.0;
+  const real jw = row ? tdot(J + r * nv, warm, nv) - aref[r] : 0.0;
+  if (row) jar[r] = jw;
+  FOR_T(i, nv) Ma[i] = tdot(qM + i * nv, warm, nv);
+  TSYNC();
+  unsigned long long mw;
+  const real cu_w = cu_fast(m, L, T, jw, Di, true, mw);
+  hessian_build_fast(m, L, T, H, mw);
+  cholesky_rows(nv, T.tid, H);
+  if (T.tid == 0) {
+    T.c[C.bc + 4] = cu_w;
+    T.c[C.bc + 5] = __longlong_as_double((long long)mw);
+  }
+  TSYNC();
+}
+
+// dual: the primary wave of a two-wave team whose helper runs newton_warm_prep
+// concurrently; exactly one __syncthreads (after the smooth start's cost)
+__device__ inline void fwd_constraint_fast(const auto& m, const auto& L, const auto& C, const auto& X,
+                                           const Team& T, int maxiter, real tol, bool dual = false) {
+  const int nv = m.nv, ne = T.iw[L.nefc];
+  const real scale = 1 / (m.stat_meaninertia * (nv > 1 ? nv : 1));
+  real* s = T.w + L.s_newton;
+  real *Ma = s, *grad = s + nv, *search = s + 2 * nv, *Mv = s + 3 * nv, *H = s + 4 * nv;
+  real* jar = s + 4 * nv + nv * nv;
+  real* Jv = jar + ne;
+  real* qM = T.w + L.qM;
+  real* qacc = T.w + L.qacc;
+  real* warm = T.w + L.warm;
+  real* J = T.w + L.efc_J;
+  real* aref = T.w + L.efc_aref;
+  real* b = T.w + L.efc_b;
+  real* qfs = T.w + L.qfrc_smooth;
+  real* qas = T.w + L.qacc_smooth;
+  real* qc = T.w + L.qfrc_con;
+  const int r = T.tid;
+  const bool row = r < ne;
+  const real Di = row ? T.w[L.efc_D + r] : 0.0;
+  unsigned long long mask, hmask;
+  // warm-start selection (oracle fwd_constraint): smooth vs warmstart cost
+  real jb = 0, jw = 0, cost_warm, cost_smooth;
+  unsigned long long mask_w = 0;
+  if (dual) {
+    if (row) {
+      jb = tdot(J + r * nv, qas, nv) - aref[r];
+      b[r] = jb;
+    }
+    cost_smooth = cu_fast(m, L, T, jb, Di, false, mask);
+    __syncthreads();  // the helper's warm-start part (newton_warm_prep) is in LDS
+    if (row) jw = jar[r];
+    mask_w = (unsigned long long)__double_as_longlong(T.c[C.bc + 5]);
+    cost_warm = gauss_u(nv, Ma, qfs, warm, qas) + T.c[C.bc + 4];
+  } else {
+    if (row) {
+      jb = tdot(J + r * nv, qas, nv) - aref[r];
+      jw = tdot(J + r * nv, warm, nv) - aref[r];
+      b[r] = jb;
+    }
+    FOR_T(i, nv) Ma[i] = tdot(qM + i * nv, warm, nv);
+    TSYNC();
+    cost_smooth = cu_fast(m, L, T, jb, Di, false, mask);
+    cost_warm = gauss_u(nv, Ma, qfs, warm, qas) + cu_fast(m, L, T, jw, Di, false, mask);
+  }
+  const bool use_smooth = cost_warm > cost_smooth;
+  // solver start (oracle solver_newton): Ma, jar at qacc, full constraint update
+  real jr = use_smooth ? jb : jw;
+  FOR_T(i, nv) qacc[i] = use_smooth ? qas[i] : warm[i];
+  TSYNC();
+  if (use_smooth) {
+    FOR_T(i, nv) Ma[i] = tdot(qM + i * nv, qacc, nv);
+    TSYNC();
+  }
+  // from the warm start the full update's cost is cost_warm's expression on the
+  // same values: only its side effects (force, state, qfrc_constraint) are new
+  real cost;
+  if (use_smooth) {
+    cost = gauss_u(nv, Ma, qfs, qacc, qas) + cu_fast(m, L, T, jr, Di, true, mask);
+  } else if (dual) {
+    mask = mask_w;  // forces, states, qfrc_constraint and the factor: the helper's
+    cost = cost_warm;
+  } else {
+    (void)cu_fast(m, L, T, jr, Di, true, mask, false);
+    cost = cost_warm;
+  }
+  FOR_T(j, nv) grad[j] = (Ma[j] - qfs[j]) - qc[j];
+  if (use_smooth || !dual) {
+    hessian_build_fast(m, L, T, H, mask);
+    cholesky_rows(nv, T.tid, H);
+  } else {
+    TSYNC();
+  }
+  hmask = mask;
+  int iter = 0;
+#ifdef ILQG_STAMPS
+  if (T.tid == 0) atomicAdd(&g_newton_calls, 1ull);
+#endif
+  while (iter < maxiter) {
+    chol_solve_rows(nv, T.tid, H, grad, search);
+    STAMP(14);
+    FOR_T(i, nv) Mv[i] = tdot(qM + i * nv, search, nv);
+    const real jv = row ? tdot(J + r * nv, search, nv) : 0.0;
+    TSYNC();
+    STAMP(15);
+    // exact line search (oracle linesearch), uniform on every lane
+    real alpha = 0;
+    {
+      real snorm = sqrt(tdot(search, search, nv));
+      if (!(snorm < MINVAL)) {
+        real g1 = 0, g2 = 0, d1, d2, lo = 0, hi = -1;
+        for (int j = 0; j < nv; j++) g1 += search[j] * (Ma[j] - qfs[j]);
+        for (int j = 0; j < nv; j++) g2 += search[j] * Mv[j];
+        // active rows only (the others add -0.0); d2 depends on the active set
+        // alone, so it is summed again only when the set changes
+        unsigned long long pmask = 0;
+        bool have = false;
+        real d2c = 0, rd2 = 0;
+        const real c2 = Di * jv * jv;
+        auto eval = [&](real a) {
+          const real x = jr + a * jv;
+          const bool on = row && x < 0;
+          const real c1 = Di * x * jv;
+          const unsigned long long am = __ballot(on);
+          d1 = lane_sum_mask(g1 + g2 * a, c1, am);
+          if (!have || am != pmask) {
+            d2c = lane_sum_mask(g2, c2, am);
+            rd2 = rcp_ref(d2c);  // d1 / d2 below: the divisor's part, once per active set
+            pmask = am;
+            have = true;
+          }
+          d2 = d2c;
+        };
+        eval(0.0);
+        if (!(d1 >= 0)) {
+          real gtol = LS_TOL * fabs(d1);
+          for (int it = 0; it < LS_ITER; it++) {
+            real anew = alpha - div_ref_lane<0>(d1, d2, rd2);
+            if (hi >= 0 && !(anew > lo && anew < hi)) anew = 0.5 * (lo + hi);
+            alpha = anew;
+            eval(alpha);
+            if (fabs(d1) < gtol) break;
+            if (d1 < 0) lo = alpha; else hi = alpha;
+          }
+        }
+      }
+    }
+    STAMP(16);
+    if (alpha == 0) break;
+    FOR_T(j, nv) {
+      qacc[j] += alpha * search[j];
+      Ma[j] += alpha * Mv[j];
+    }
+    jr += alpha * jv;
+    TSYNC();
+    iter++;
+#ifdef ILQG_STAMPS
+    if (T.tid == 0) atomicAdd(&g_newton_iters, 1ull);
+#endif
+    STAMP(17);
+    const real oldcost = cost;
+    cost = gauss_u(nv, Ma, qfs, qacc, qas) + cu_fast(m, L, T, jr, Di, true, mask);
+    FOR_T(j, nv) grad[j] = (Ma[j] - qfs[j]) - qc[j];
+    TSYNC();
+    const real improvement = scale * (oldcost - cost);
+    const real gradient = scale * sqrt(tdot(grad, grad, nv));
+    STAMP(18);
+    if (improvement < tol || gradient < tol) break;
+    if (mask != hmask) {
+      hessian_build_fast(m, L, T, H, mask);
+      cholesky_rows(nv, T.tid, H);
+      hmask = mask;
+    }
+    STAMP(19);
+  }
+  if (row) jar[r] = jr;
+  FOR_T(i, nv) warm[i] = qacc[i];
+  TSYNC();
+}
+
+__device__ inline void fwd_constraint(const auto& m, const auto& L, const auto& C, const auto& X, const Team& T,
+                                      int maxiter, real tol) {
+  const int nv = m.nv, ne = T.iw[L.nefc];
+  real* qacc = T.w + L.qacc;
+  real* warm = T.w + L.warm;
+  real* qas = T.w + L.qacc_smooth;
+  real* qc = T.w + L.qfrc_con;
+  if (!ne) {
+    FOR_T(i, nv) { real v = qas[i]; qacc[i] = v; warm[i] = v; qc[i] = 0; }
+    TSYNC();
+    return;
+  }
+  if (ne <= TEAM_SIZE && nv <= RMAX) {
+    fwd_constraint_fast(m, L, C, X, T, maxiter, tol);
+    return;
+  }
+  {
+    real* s = T.w + L.s_newton;
+    real* Ma = s;
+    real* jar = s + 4 * nv + nv * nv;
+    real* J = T.w + L.efc_J;
+    real* aref = T.w + L.efc_aref;
+    real* b = T.w + L.efc_b;
+    real* qM = T.w + L.qM;
+    real* qfs = T.w + L.qfrc_smooth;
+    FOR_T(i, ne) {
+      b[i] = tdot(J + i * nv, qas, nv) - aref[i];
+      jar[i] = tdot(J + i * nv, warm, nv) - aref[i];
+    }
+    FOR_T(i, nv) Ma[i] = tdot(qM + i * nv, warm, nv);
+    TSYNC();
+    real cost_smooth = constraint_update(m, L, C, T, b);
+    real cw = constraint_update(m, L, C, T, jar);
+    if (T.tid == 0) {
+      real g = 0;
+      for (int j = 0; j < nv; j++) g += (Ma[j] - qfs[j]) * (warm[j] - qas[j]);
+      real cost_warm = 0.5 * g + cw;
+      T.ci[C.ibc] = cost_warm > cost_smooth ? 1 : 0;
+    }
+    TSYNC();
+    const int use_smooth = T.ci[C.ibc];
+    FOR_T(i, nv) qacc[i] = use_smooth ? qas[i] : warm[i];
+    TSYNC();
+  }
+  solver_newton(m, L, C, T, maxiter, tol);
+  FOR_T(i, nv) warm[i] = qacc[i];
+  TSYNC();
+}
+
+__device__ inline void forward_skip(const auto& m, const auto& L, const auto& C, const auto& X,
+                                    const Team& T, int skipstage, int maxiter, real tol) {
+  STAMP(-1);
+  TSYNC();
+  STAMP(20);
+  TSYNC();
+  STAMP(21);
+  if (skipstage < STAGE_POS) fwd_position(m, L, C, X, T);
+  if (skipstage < STAGE_VEL) fwd_velocity(m, L, C, T);
+  STAMP(6);
+  fwd_acceleration(m, L, X, T);
+  STAMP(7);
+  fwd_constraint(m, L, C, X, T, maxiter, tol);
+  STAMP(8);
+}
+
+// forward_skip split at the warm start: the position and velocity stages never
+// read qacc_warmstart, the acceleration stage's constraint solve does
+__device__ inline void forward_posvel(const auto& m, const auto& L, const auto& C, const auto& X, const Team& T,
+                                      int skipstage) {
+  STAMP(-1);
+  TSYNC();
+  if (skipstage < STAGE_POS) fwd_position(m, L, C, X, T);
+  if (skipstage < STAGE_VEL) fwd_velocity(m, L, C, T);
+  STAMP(6);
+}
+__device__ inline void forward_acc(const auto& m, const auto& L, const auto& C, const auto& X, const Team& T,
+                                   int maxiter, real tol) {
+  STAMP(-1);
+  fwd_acceleration(m, L, X, T);
+  STAMP(7);
+  fwd_constraint(m, L, C, X, T, maxiter, tol);
+  STAMP(8);
+}
+
+__device__ inline void integrate_pos(const auto& m, const Team& T, real* qpos, const real* qvel, real dt) {
+  FOR_T(j, m.njnt) {
+    int pa = m.jnt_qposadr[j], va = m.jnt_dofadr[j];
+    int type = m.jnt_type[j];
+    if (type == JNT_FREE || type == JNT_BALL) {
+      if (type == JNT_FREE) {
+        for (int i = 0; i < 3; i++) qpos[pa + i] += dt * qvel[va + i];
+        pa += 3;
+        va += 3;
+      }
+      real q[4], v[3];
+      ldm<4>(q, qpos + pa);
+      ldm<3>(v, qvel + va);
+      quat_integrate(q, v, dt);
+      for (int k = 0; k < 4; k++) qpos[pa + k] = q[k];
+    } else {
+      qpos[pa] += dt * qvel[va];
+    }
+  }
+  TSYNC();
+}
+
+__device__ inline void reset_data(const auto& m, const auto& L, const Team& T) {
+  real* qpos = T.w + L.qpos;
+  FOR_T(i, m.nq) qpos[i] = m.qpos0[i];
+  FOR_T(i, m.nv) {
+    T.w[L.qvel + i] = 0;
+    T.w[L.warm + i] = 0;
+    T.w[L.qfrc_applied + i] = 0;
+  }
+  FOR_T(i, m.nu) T.w[L.ctrl + i] = 0;
+  FOR_T(i, 6 * m.nbody) T.w[L.xfrc_applied + i] = 0;
+  if (T.tid == 0) T.w[L.time] = 0;
+  TSYNC();
+}
+
+// mj_checkPos/Vel/Acc test: any NaN/huge entry (a wave ballot, no serial scan)
+__device__ inline int any_bad(const Team& T, const auto& C, const real* x, int n) {
+  unsigned long long bad = 0;
+  for (int i0 = 0; i0 < n; i0 += TEAM_SIZE) {
+    const int i = i0 + T.tid;
+    bad |= __ballot(i < n && is_bad(x[i]));
+  }
+  return bad != 0ull;
+}
+
+// Euler with implicit joint damping (MuJoCo mj_Euler): qacc_e = (M + h D)^-1 M qacc.
+// Split so a helper wave can factor M + h D (a function of qM only) while the
+// primary wave is still in the velocity stage; the factor is the same numbers.
+__device__ inline bool euler_damped(const auto& m, const Team& T) {
+  const int nv = m.nv;
+  unsigned long long dmask = 0;
+  for (int i0 = 0; i0 < nv; i0 += TEAM_SIZE) dmask |= __ballot(i0 + T.tid < nv && m.dof_damping[i0 + T.tid] > 0);
+  return dmask != 0ull;
+}
+__device__ inline void euler_prefactor(const auto& m, const auto& L, const auto& C, const auto& X, const Team& T) {
+  const int nv = m.nv;
+  real* s = T.w + L.s_euler;
+  real *qH = s + nv, *qHLD = s + nv + nv * nv, *qHinv = s + nv + 2 * nv * nv;
+  real* qM = T.w + L.qM;
+  if (!euler_damped(m, T)) return;
+  FOR_T(e, nv * nv) {
+    int i = e / nv, j = e % nv;
+    real v = qM[e];
+    if (i == j) v += m.opt_timestep * m.dof_damping[i];
+    qH[e] = v;
+  }
+  TSYNC();
+  factor_ld(m, X, T, qH, qHLD, qHinv, T.c + C.ftmp);
+}
+__device__ inline void euler_finish(const auto& m, const auto& L, const auto& C, const auto& X, const Team& T,
+                                    bool factored) {
+  const int nv = m.nv;
+  real* s = T.w + L.s_euler;
+  real *qacc = s, *qHLD = s + nv + nv * nv, *qHinv = s + nv + 2 * nv * nv;
+  real* qM = T.w + L.qM;
+  real* dq = T.w + L.qacc;
+  real* qvel = T.w + L.qvel;
+  if (!euler_damped(m, T)) {
+    FOR_T(i, nv) qacc[i] = dq[i];
+    TSYNC();
+  } else {
+    FOR_T(i, nv) qacc[i] = tdot(qM + i * nv, dq, nv);
+    TSYNC();
+    if (!factored) euler_prefactor(m, L, C, X, T);
+    solve_ld(m, X, T, qHLD, qHinv, qacc);
+  }
+  const real h = m.opt_timestep;
+  FOR_T(i, nv) qvel[i] += qacc[i] * h;
+  TSYNC();
+  integrate_pos(m, T, T.w + L.qpos, qvel, h);
+  if (T.tid == 0) T.w[L.time] += h;
+  TSYNC();
+}
+__device__ inline void euler(const auto& m, const auto& L, const auto& C, const auto& X, const Team& T) {
+  euler_finish(m, L, C, X, T, false);
+}
+
+__device__ inline void rk4(const auto& m, const auto& L, const auto& C, const auto& X, const Team& T,
+                           int maxiter, real tol) {
+  const real A[9] = {0.5, 0, 0, 0, 0.5, 0, 0, 0, 1};
+  const real Bw[4] = {1.0 / 6, 1.0 / 3, 1.0 / 3, 1.0 / 6};
+  const int nv = m.nv, nq = m.nq, N = 4;
+  const real h = m.opt_timestep;
+  real* qpos = T.w + L.qpos;
+  real* qvel = T.w + L.qvel;
+  real* qaccw = T.w + L.qacc;
+  const real time = T.w[L.time];
+  real Cc[3], Tt[3];
+  real* s = T.w + L.s_rk4;
+  real *dX = s, *X0 = s + 2 * nv, *F = s + 2 * nv + 4 * (nq + nv);
+  for (int i = 1; i < N; i++) {
+    Cc[i - 1] = 0;
+    for (int j = 0; j < i; j++) Cc[i - 1] += A[(i - 1) * (N - 1) + j];
+    Tt[i - 1] = time + Cc[i - 1] * h;
+  }
+  FOR_T(k, nq) X0[k] = qpos[k];
+  FOR_T(k, nv) { X0[nq + k] = qvel[k]; F[k] = qaccw[k]; }
+  TSYNC();
+  for (int i = 1; i < N; i++) {
+    real* Xi = X0 + i * (nq + nv);
+    FOR_T(k, nv) {
+      real a0 = 0, a1 = 0;
+      for (int j = 0; j < i; j++) {
+        real a = A[(i - 1) * (N - 1) + j];
+        a0 += X0[j * (nq + nv) + nq + k] * a;
+        a1 += F[j * nv + k] * a;
+      }
+      dX[k] = a0;
+      dX[nv + k] = a1;
+    }
+    FOR_T(k, nq + nv) Xi[k] = X0[k];
+    TSYNC();
+    integrate_pos(m, T, Xi, dX, h);
+    FOR_T(k, nv) Xi[nq + k] += dX[nv + k] * h;
+    TSYNC();
+    FOR_T(k, nq) qpos[k] = Xi[k];
+    FOR_T(k, nv) qvel[k] = Xi[nq + k];
+    if (T.tid == 0) T.w[L.time] = Tt[i - 1];
+    TSYNC();
+    forward_skip(m, L, C, X, T, STAGE_NONE, maxiter, tol);
+    FOR_T(k, nv) F[i * nv + k] = qaccw[k];
+    TSYNC();
+  }
+  FOR_T(k, nv) {
+    real a0 = 0, a1 = 0;
+    for (int j = 0; j < N; j++) {
+      a0 += X0[j * (nq + nv) + nq + k] * Bw[j];
+      a1 += F[j * nv + k] * Bw[j];
+    }
+    dX[k] = a0;
+    dX[nv + k] = a1;
+  }
+  TSYNC();
+  FOR_T(k, nq) qpos[k] = X0[k];
+  FOR_T(k, nv) qvel[k] = X0[nq + k] + dX[nv + k] * h;
+  if (T.tid == 0) T.w[L.time] = time;
+  TSYNC();
+  integrate_pos(m, T, qpos, dX, h);
+  if (T.tid == 0) T.w[L.time] += h;
+  TSYNC();
+}
+
+// mj_step with the model's own solver settings
+__device__ inline void step(const auto& m, const auto& L, const auto& C, const auto& X,
+                            const Team& T) {
+  if (any_bad(T, C, T.w + L.qpos, m.nq)) reset_data(m, L, T);
+  if (any_bad(T, C, T.w + L.qvel, m.nv)) reset_data(m, L, T);
+  forward_skip(m, L, C, X, T, STAGE_NONE, m.opt_iterations, m.opt_tolerance);
+  if (any_bad(T, C, T.w + L.qacc, m.nv)) {
+    reset_data(m, L, T);
+    forward_skip(m, L, C, X, T, STAGE_NONE, m.opt_iterations, m.opt_tolerance);
+  }
+  STAMP(-1);
+  if (m.opt_integrator == 1)
+    rk4(m, L, C, X, T, m.opt_iterations, m.opt_tolerance);
+  else
+    euler(m, L, C, X, T);
+  STAMP(9);
+}
+
+// the L'DL factor of M and, for Euler with damping, the factor of M + h D
+// (euler_prefactor's matrix) in one pass of the register-row factorization:
+// lanes 0..31 factor M, lanes 32..63 factor M + h D.  Same numbers as
+// factor_ld() followed by euler_prefactor().
+__device__ inline void factor_m_and_euler(const auto& m, const auto& L, const auto& C, const auto& X,
+                                          const Team& T, bool eul) {
+  const int nv = m.nv;
+  real* qM = T.w + L.qM;
+  if (!(eul && euler_damped(m, T))) {
+    factor_ld(m, X, T, qM, T.w + L.qLD, T.w + L.qLDinv, T.c + C.ftmp);
+    return;
+  }
+  if (!(nv <= RMAX && X.pmask)) {
+    factor_ld(m, X, T, qM, T.w + L.qLD, T.w + L.qLDinv, T.c + C.ftmp);
+    euler_prefactor(m, L, C, X, T);
+    return;
+  }
+  real* s = T.w + L.s_euler;
+  real *qH = s + nv, *qHLD = s + nv + nv * nv, *qHinv = s + nv + 2 * nv * nv;
+  FOR_T(e, nv * nv) {
+    int i = e / nv, j = e % nv;
+    real v = qM[e];
+    if (i == j) v += m.opt_timestep * m.dof_damping[i];
+    qH[e] = v;
+  }
+  TSYNC();
+  factor_ld_rows2(nv, X.pmask, T.tid, qM, T.w + L.qLD, T.w + L.qLDinv, qH, qHLD, qHinv);
+}
+
+// step_dual for the split layout (L.split: RNE / com-velocity / Euler scratch
+// outside the union) and register-row models, on a THREE-wave team (wave 0
+// the dependency chain, waves 1 and 2 helpers).  Work moves to where a helper
+// has slack, without changing any value:
+//   phase 1 (beside the kinematics), wave 1: control law + record, the limit
+//     rows of make_constraint (qpos only), passive forces, transmission and
+//     actuator forces (ctrl only);
+//   phase 2 (beside com_pos), wave 1: collision;
+//   phase 3 (beside crb), wave 1: contact jacobians and row allocation;
+//   phase 4 (beside com velocities + RNE), wave 1: the contact rows'
+//     jacobians and parameters, constraint reference accelerations and the
+//     warm-start half of the Newton start; wave 2: the factors of M and of
+//     M + h D in one register-row pass;
+//   phase 5: the primary's acceleration stage and constraint solve find the
+//     Newton warm start ready.
+__device__ inline void step_dual_split(const auto& m, const auto& L, const auto& C, const auto& X, const Team& T,
+                                       int wave, int sid, auto&& pre) {
+  const bool A = wave == 0, B = wave == 1;
+  int* fq = T.ci + C.ibc + 6;  // quaternions final (primary -> frames helper)
+  int* ff = T.ci + C.ibc + 7;  // frame rotations final (helper -> primary)
+  const bool eul = m.opt_integrator != 1;
+  STAMP(-1);
+  STAMPB(-1);
+  const bool bad = any_bad(T, C, T.w + L.qpos, m.nq) || any_bad(T, C, T.w + L.qvel, m.nv);
+  if (bad) {
+    if (B) pre();
+    __syncthreads();
+    if (A) reset_data(m, L, T);
+    __syncthreads();  // the helpers' phase-1 work reads the reset state
+  }
+  int* nlim_sh = T.ci + C.ibc + 5;  // the limit rows' count, from wave 2 to wave 1
+  constexpr bool ksplit = kin_split_ok<std::remove_cvref_t<decltype(m)>>();
+  if (A) {
+    if constexpr (ksplit) kinematics_primary(m, L, C, T, fq, ff, sid);
+    else kinematics(m, L, C, T);
+    STAMP(0);
+  } else if (!B) {
+    // wave 2: the qpos/qvel-only rows and forces, then the frame rotations
+    const int nl = limit_rows_pre(m, L, C, T);
+    if (T.tid == 0) *nlim_sh = nl;
+    passive_forces(m, L, T);
+    if constexpr (ksplit) kinematics_frames(m, L, T, fq, ff, sid);
+  } else {
+    if (!bad) pre();
+    STAMPB(41);
+    transmission(m, L, T);
+    TSYNC();
+    actuator_force(m, L, T);
+    STAMPB(42);
+  }
+  __syncthreads();
+  const int nlim = *nlim_sh;
+  STAMP(24);
+  STAMPB(32);
+  if (A) {
+    com_pos(m, L, T);
+    STAMP(1);
+  } else if (B) {
+    collision(m, L, C, X, T);
+    STAMPB(33);
+  }
+  __syncthreads();
+  STAMP(25);
+  STAMPB(34);
+  bool rows_done = false;
+  if (A) {
+    crb(m, L, C, X, T);
+    STAMP(2);
+  } else if (B) {
+    mc_contact_jac(m, L, X, T);
+    TSYNC();
+    const bool par = mc_alloc(m, L, C, T);
+    TSYNC();
+    if (!par || nlim < 0) {
+      // the serial allocation (njmax truncation): every row here, as make_constraint
+      mc_rows(m, L, C, T, 0, T.iw[L.nefc]);
+      TSYNC();
+      rows_done = true;
+    }
+    STAMPB(35);
+  }
+  __syncthreads();
+  STAMP(26);
+  STAMPB(36);
+  const int ne5 = T.iw[L.nefc];
+  const bool spec = ne5 > 0 && ne5 <= TEAM_SIZE && m.nv <= RMAX;
+  if (A) {
+    fwd_velocity(m, L, C, T, 1);
+    STAMP(6);
+  } else if (B) {
+    if (!rows_done) {
+      mc_rows(m, L, C, T, nlim, T.iw[L.nefc]);
+      TSYNC();
+    }
+    constraint_ref(m, L, T);
+    TSYNC();
+    STAMPB(37);
+    if (spec) newton_warm_prep(m, L, C, T);
+    STAMPB(30);
+  } else {
+    factor_m_and_euler(m, L, C, X, T, eul);
+  }
+  __syncthreads();
+  STAMP(27);
+  STAMPB(39);
+  if (A) {
+    fwd_acceleration(m, L, X, T, true);
+    STAMP(7);
+    if (spec) {
+      fwd_constraint_fast(m, L, C, X, T, m.opt_iterations, m.opt_tolerance, true);
+    } else {
+      __syncthreads();
+      fwd_constraint(m, L, C, X, T, m.opt_iterations, m.opt_tolerance);
+    }
+    STAMP(8);
+  } else {
+    __syncthreads();  // the primary's barrier inside its Newton start
+    STAMPB(38);
+  }
+  __syncthreads();
+  STAMP(29);
+  STAMPB(43);
+  if (A) {
+    bool reset = false;
+    if (any_bad(T, C, T.w + L.qacc, m.nv)) {
+      reset = true;
+      reset_data(m, L, T);
+      forward_skip(m, L, C, X, T, STAGE_NONE, m.opt_iterations, m.opt_tolerance);
+    }
+    if (!eul) rk4(m, L, C, X, T, m.opt_iterations, m.opt_tolerance);
+    else euler_finish(m, L, C, X, T, !reset);
+    STAMP(9);
+  }
+  __syncthreads();
+  STAMP(28);
+  STAMPB(40);
+}
+
+// mj_step by a two-wave team (rollout kernels): wave 0 runs the dependency
+// chain, wave 1 takes the branches off it -- collision beside com_pos,
+// make_constraint beside crb + factor_ld(M), passive forces + constraint
+// reference + the Euler factor of M + h D beside com velocities + RNE.  Every
+// quantity is still computed by the same code, so results are unchanged;
+// both waves pass the same __syncthreads sequence.
+__device__ inline void step_dual(const auto& m, const auto& L, const auto& C, const auto& X, const Team& T,
+                                 int wave, auto&& pre) {
+  const bool A = wave == 0;
+  const bool eul = m.opt_integrator != 1;
+  STAMP(-1);
+  STAMPB(-1);
+  // `pre` (the caller's per-step work that reads the state before the step:
+  // control law, trajectory record) runs on the helper wave beside the
+  // kinematics.  mj_checkPos/Vel resets the state, so on a bad state it runs
+  // first, as in the one-wave order; both waves test the same LDS state.
+  const bool bad = any_bad(T, C, T.w + L.qpos, m.nq) || any_bad(T, C, T.w + L.qvel, m.nv);
+  if (bad) {
+    if (!A) pre();
+    __syncthreads();
+    if (A) reset_data(m, L, T);
+  }
+  if (A) {
+    kinematics(m, L, C, T);
+    STAMP(0);
+  } else if (!bad) {
+    pre();
+    STAMPB(41);
+  }
+  __syncthreads();
+  STAMP(24);
+  STAMPB(32);
+  if (A) {
+    com_pos(m, L, T);
+    STAMP(1);
+  } else {
+    collision(m, L, C, X, T);
+    STAMPB(33);
+  }
+  __syncthreads();
+  STAMP(25);
+  STAMPB(34);
+  if (A) {
+    transmission(m, L, T);
+    crb(m, L, C, X, T);
+    STAMP(2);
+  } else {
+    make_constraint(m, L, C, X, T);
+    STAMPB(35);
+  }
+  __syncthreads();
+  STAMP(26);
+  STAMPB(36);
+  // the L'DL factor of M runs on the helper beside the com velocities and RNE
+  // (nothing on the primary reads it before the acceleration stage)
+  if (A) {
+    fwd_velocity(m, L, C, T, 1);
+    STAMP(6);
+  } else {
+    fwd_velocity(m, L, C, T, 2);
+    STAMPB(37);
+    factor_ld(m, X, T, T.w + L.qM, T.w + L.qLD, T.w + L.qLDinv, T.c + C.ftmp);
+    STAMPB(42);
+  }
+  __syncthreads();
+  STAMP(27);
+  STAMPB(39);
+  // the Euler factor of M + h D on the helper beside the constraint solve
+  // ... and the warm-start half of the Newton start before it (one extra
+  // barrier inside the phase, on both waves)
+  const int ne5 = T.iw[L.nefc];
+  const bool spec = ne5 > 0 && ne5 <= TEAM_SIZE && m.nv <= RMAX;
+  if (A) {
+    fwd_acceleration(m, L, X, T);
+    STAMP(7);
+    if (spec) {
+      fwd_constraint_fast(m, L, C, X, T, m.opt_iterations, m.opt_tolerance, true);
+    } else {
+      __syncthreads();
+      fwd_constraint(m, L, C, X, T, m.opt_iterations, m.opt_tolerance);
+    }
+    STAMP(8);
+  } else {
+    if (spec) newton_warm_prep(m, L, C, T);
+    STAMPB(30);
+    __syncthreads();
+    if (eul) euler_prefactor(m, L, C, X, T);
+    STAMPB(38);
+  }
+  __syncthreads();
+  STAMP(29);
+  STAMPB(43);
+  if (A) {
+    // (after the barrier: a reset recomputes the forward pass on this wave
+    // alone, and its factorisations share scratch with the helper's)
+    bool reset = false;
+    if (any_bad(T, C, T.w + L.qacc, m.nv)) {
+      reset = true;
+      reset_data(m, L, T);
+      forward_skip(m, L, C, X, T, STAGE_NONE, m.opt_iterations, m.opt_tolerance);
+    }
+    if (!eul) rk4(m, L, C, X, T, m.opt_iterations, m.opt_tolerance);
+    else euler_finish(m, L, C, X, T, !reset);
+    STAMP(9);
+  }
+  __syncthreads();
+  STAMP(28);
+  STAMPB(40);
+}
+

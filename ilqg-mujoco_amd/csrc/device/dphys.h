@@ -12,6 +12,8 @@
 
 #include <hip/hip_runtime.h>
 
+#include <type_traits>
+
 #include "dmodel.h"
 
 namespace ilqg {
@@ -88,37 +90,42 @@ __device__ inline double det_cos(double x) {
   }
 }
 
-__device__ __forceinline__ double dot3(const double* a, const double* b) { return a[0] * b[0] + a[1] * b[1] + a[2] * b[2]; }
-__device__ __forceinline__ void cross3(double* r, const double* a, const double* b) {
-  double t0 = a[1] * b[2] - a[2] * b[1];
-  double t1 = a[2] * b[0] - a[0] * b[2];
-  double t2 = a[0] * b[1] - a[1] * b[0];
+template <class A, class B>
+__device__ __forceinline__ auto dot3(const A* a, const B* b) { return a[0] * b[0] + a[1] * b[1] + a[2] * b[2]; }
+template <class R, class A, class B>
+__device__ __forceinline__ void cross3(R* r, const A* a, const B* b) {
+  R t0 = a[1] * b[2] - a[2] * b[1];
+  R t1 = a[2] * b[0] - a[0] * b[2];
+  R t2 = a[0] * b[1] - a[1] * b[0];
   r[0] = t0; r[1] = t1; r[2] = t2;
 }
-__device__ inline double normalize3(double* v) {
-  double norm = sqrt(v[0] * v[0] + v[1] * v[1] + v[2] * v[2]);
+template <class R>
+__device__ inline R normalize3(R* v) {
+  R norm = sqrt(v[0] * v[0] + v[1] * v[1] + v[2] * v[2]);
   if (norm < MINVAL) {
     v[0] = 1; v[1] = 0; v[2] = 0;
   } else {
-    double inv = 1 / norm;
+    R inv = 1 / norm;
     v[0] *= inv; v[1] *= inv; v[2] *= inv;
   }
   return norm;
 }
-__device__ inline void normalize4(double* q) {
-  double norm = sqrt(q[0] * q[0] + q[1] * q[1] + q[2] * q[2] + q[3] * q[3]);
+template <class R>
+__device__ inline void normalize4(R* q) {
+  R norm = sqrt(q[0] * q[0] + q[1] * q[1] + q[2] * q[2] + q[3] * q[3]);
   if (norm < MINVAL) {
     q[0] = 1; q[1] = 0; q[2] = 0; q[3] = 0;
   } else if (fabs(norm - 1) > MINVAL) {
-    double inv = 1 / norm;
+    R inv = 1 / norm;
     q[0] *= inv; q[1] *= inv; q[2] *= inv; q[3] *= inv;
   }
 }
-__device__ __forceinline__ void quat_mul(double* r, const double* a, const double* b) {
-  double t0 = a[0] * b[0] - a[1] * b[1] - a[2] * b[2] - a[3] * b[3];
-  double t1 = a[0] * b[1] + a[1] * b[0] + a[2] * b[3] - a[3] * b[2];
-  double t2 = a[0] * b[2] - a[1] * b[3] + a[2] * b[0] + a[3] * b[1];
-  double t3 = a[0] * b[3] + a[1] * b[2] - a[2] * b[1] + a[3] * b[0];
+template <class R, class A, class B>
+__device__ __forceinline__ void quat_mul(R* r, const A* a, const B* b) {
+  R t0 = a[0] * b[0] - a[1] * b[1] - a[2] * b[2] - a[3] * b[3];
+  R t1 = a[0] * b[1] + a[1] * b[0] + a[2] * b[3] - a[3] * b[2];
+  R t2 = a[0] * b[2] - a[1] * b[3] + a[2] * b[0] + a[3] * b[1];
+  R t3 = a[0] * b[3] + a[1] * b[2] - a[2] * b[1] + a[3] * b[0];
   r[0] = t0; r[1] = t1; r[2] = t2; r[3] = t3;
 }
 // dof j of x_a (-) x_b (oracle ora_state_diff): plain difference for
@@ -126,40 +133,43 @@ __device__ __forceinline__ void quat_mul(double* r, const double* a, const doubl
 // first-order log map 2 sign(w) v of conj(q_b) q_a.  For models without
 // ball/free joints this is exactly qpos_a[j] - qpos_b[j].
 template <class M, class PA, class PB>
-__device__ inline double state_diff_dof(const M& m, int j, const PA& qa, const PB& qb) {
+__device__ inline auto state_diff_dof(const M& m, int j, const PA& qa, const PB& qb) {
+  using R = std::remove_cvref_t<decltype(qa[0])>;
   const int jid = m.dof_jntid[j], t = m.jnt_type[jid], qadr = m.jnt_qposadr[jid], dadr = m.jnt_dofadr[jid];
   if ((t == JNT_FREE && j >= dadr + 3) || t == JNT_BALL) {
     const int qo = qadr + (t == JNT_FREE ? 3 : 0), k = j - dadr - (t == JNT_FREE ? 3 : 0);
-    const double c[4] = {qb[qo], -qb[qo + 1], -qb[qo + 2], -qb[qo + 3]};
-    const double a[4] = {qa[qo], qa[qo + 1], qa[qo + 2], qa[qo + 3]};
-    double q[4];
+    const R c[4] = {qb[qo], -qb[qo + 1], -qb[qo + 2], -qb[qo + 3]};
+    const R a[4] = {qa[qo], qa[qo + 1], qa[qo + 2], qa[qo + 3]};
+    R q[4];
     quat_mul(q, c, a);
-    const double sg = q[0] < 0 ? -2.0 : 2.0;
-    return sg * q[1 + k];
+    const R sg = q[0] < 0 ? -2.0 : 2.0;
+    return (R)(sg * q[1 + k]);
   }
-  return qa[qadr + j - dadr] - qb[qadr + j - dadr];
+  return (R)(qa[qadr + j - dadr] - qb[qadr + j - dadr]);
 }
-__device__ inline void rot_vec_quat(double* r, const double* v, const double* q) {
+template <class R, class V, class Q>
+__device__ inline void rot_vec_quat(R* r, const V* v, const Q* q) {
   if (v[0] == 0 && v[1] == 0 && v[2] == 0) {
     r[0] = r[1] = r[2] = 0;
   } else if (q[0] == 1 && q[1] == 0 && q[2] == 0 && q[3] == 0) {
     r[0] = v[0]; r[1] = v[1]; r[2] = v[2];
   } else {
-    double t0 = q[0] * v[0] + q[2] * v[2] - q[3] * v[1];
-    double t1 = q[0] * v[1] + q[3] * v[0] - q[1] * v[2];
-    double t2 = q[0] * v[2] + q[1] * v[1] - q[2] * v[0];
-    double r0 = v[0] + 2 * (q[2] * t2 - q[3] * t1);
-    double r1 = v[1] + 2 * (q[3] * t0 - q[1] * t2);
-    double r2 = v[2] + 2 * (q[1] * t1 - q[2] * t0);
+    R t0 = q[0] * v[0] + q[2] * v[2] - q[3] * v[1];
+    R t1 = q[0] * v[1] + q[3] * v[0] - q[1] * v[2];
+    R t2 = q[0] * v[2] + q[1] * v[1] - q[2] * v[0];
+    R r0 = v[0] + 2 * (q[2] * t2 - q[3] * t1);
+    R r1 = v[1] + 2 * (q[3] * t0 - q[1] * t2);
+    R r2 = v[2] + 2 * (q[1] * t1 - q[2] * t0);
     r[0] = r0; r[1] = r1; r[2] = r2;
   }
 }
-__device__ inline void quat2mat(double* r, const double* q) {
+template <class R, class Q>
+__device__ inline void quat2mat(R* r, const Q* q) {
   // MuJoCo's identity shortcut is omitted: for q == (1,0,0,0) the general
   // formula yields exactly the same doubles, and the branch forced r to scratch.
-  double q00 = q[0] * q[0], q01 = q[0] * q[1], q02 = q[0] * q[2], q03 = q[0] * q[3];
-  double q11 = q[1] * q[1], q12 = q[1] * q[2], q13 = q[1] * q[3];
-  double q22 = q[2] * q[2], q23 = q[2] * q[3], q33 = q[3] * q[3];
+  R q00 = q[0] * q[0], q01 = q[0] * q[1], q02 = q[0] * q[2], q03 = q[0] * q[3];
+  R q11 = q[1] * q[1], q12 = q[1] * q[2], q13 = q[1] * q[3];
+  R q22 = q[2] * q[2], q23 = q[2] * q[3], q33 = q[3] * q[3];
   r[0] = q00 + q11 - q22 - q33;
   r[4] = q00 - q11 + q22 - q33;
   r[8] = q00 - q11 - q22 + q33;
@@ -170,30 +180,34 @@ __device__ inline void quat2mat(double* r, const double* q) {
   r[6] = 2 * (q13 - q02);
   r[7] = 2 * (q23 + q01);
 }
-__device__ inline void axis_angle2quat(double* r, const double* axis, double angle) {
+template <class R, class A, class G>
+__device__ inline void axis_angle2quat(R* r, const A* axis, G angle) {
   if (angle == 0) {
     r[0] = 1; r[1] = 0; r[2] = 0; r[3] = 0;
   } else {
-    double s = det_sin(angle * 0.5);
+    R s = det_sin(angle * 0.5);
     r[0] = det_cos(angle * 0.5);
     r[1] = axis[0] * s; r[2] = axis[1] * s; r[3] = axis[2] * s;
   }
 }
-__device__ __forceinline__ void rot_vec_mat(double* r, const double* v, const double* m) {
-  double r0 = m[0] * v[0] + m[1] * v[1] + m[2] * v[2];
-  double r1 = m[3] * v[0] + m[4] * v[1] + m[5] * v[2];
-  double r2 = m[6] * v[0] + m[7] * v[1] + m[8] * v[2];
+template <class R, class V, class X>
+__device__ __forceinline__ void rot_vec_mat(R* r, const V* v, const X* m) {
+  R r0 = m[0] * v[0] + m[1] * v[1] + m[2] * v[2];
+  R r1 = m[3] * v[0] + m[4] * v[1] + m[5] * v[2];
+  R r2 = m[6] * v[0] + m[7] * v[1] + m[8] * v[2];
   r[0] = r0; r[1] = r1; r[2] = r2;
 }
-__device__ inline void quat_integrate(double* quat, const double* vel, double scale) {
-  double tmp[3] = {vel[0], vel[1], vel[2]}, qrot[4];
-  double angle = scale * normalize3(tmp);
+template <class R, class V, class G>
+__device__ inline void quat_integrate(R* quat, const V* vel, G scale) {
+  R tmp[3] = {vel[0], vel[1], vel[2]}, qrot[4];
+  R angle = scale * normalize3(tmp);
   axis_angle2quat(qrot, tmp, angle);
   normalize4(quat);
   quat_mul(quat, quat, qrot);
 }
-__device__ inline void make_frame(double* f) {
-  double tmp[3], d;
+template <class R>
+__device__ inline void make_frame(R* f) {
+  R tmp[3], d;
   normalize3(f);
   f[3] = f[4] = f[5] = 0;
   if (fabs(f[1]) < 0.5) f[4] = 1; else f[5] = 1;
@@ -203,8 +217,9 @@ __device__ inline void make_frame(double* f) {
   normalize3(f + 3);
   cross3(f + 6, f, f + 3);
 }
-__device__ inline void inert_com(double* res, const double* in, const double* mat, const double* dif, double mass) {
-  double tmp[9] = {mat[0] * in[0], mat[3] * in[0], mat[6] * in[0],
+template <class R, class I, class X, class D, class G>
+__device__ inline void inert_com(R* res, const I* in, const X* mat, const D* dif, G mass) {
+  R tmp[9] = {mat[0] * in[0], mat[3] * in[0], mat[6] * in[0],
                    mat[1] * in[1], mat[4] * in[1], mat[7] * in[1],
                    mat[2] * in[2], mat[5] * in[2], mat[8] * in[2]};
   res[0] = mat[0] * tmp[0] + mat[1] * tmp[3] + mat[2] * tmp[6];
@@ -224,7 +239,8 @@ __device__ inline void inert_com(double* res, const double* in, const double* ma
   res[8] = mass * dif[2];
   res[9] = mass;
 }
-__device__ inline void mul_inert_vec(double* r, const double* i, const double* v) {
+template <class R, class I, class V>
+__device__ inline void mul_inert_vec(R* r, const I* i, const V* v) {
   r[0] = i[0] * v[0] + i[3] * v[1] + i[4] * v[2] - i[8] * v[4] + i[7] * v[5];
   r[1] = i[3] * v[0] + i[1] * v[1] + i[5] * v[2] + i[8] * v[3] - i[6] * v[5];
   r[2] = i[4] * v[0] + i[5] * v[1] + i[2] * v[2] - i[7] * v[3] + i[6] * v[4];
@@ -232,7 +248,8 @@ __device__ inline void mul_inert_vec(double* r, const double* i, const double* v
   r[4] = i[6] * v[2] - i[8] * v[0] + i[9] * v[4];
   r[5] = i[7] * v[0] - i[6] * v[1] + i[9] * v[5];
 }
-__device__ inline void cross_motion(double* r, const double* vel, const double* v) {
+template <class R, class A, class V>
+__device__ inline void cross_motion(R* r, const A* vel, const V* v) {
   r[0] = -vel[2] * v[1] + vel[1] * v[2];
   r[1] = vel[2] * v[0] - vel[0] * v[2];
   r[2] = -vel[1] * v[0] + vel[0] * v[1];
@@ -243,7 +260,8 @@ __device__ inline void cross_motion(double* r, const double* vel, const double* 
   r[4] += vel[5] * v[0] - vel[3] * v[2];
   r[5] += -vel[4] * v[0] + vel[3] * v[1];
 }
-__device__ inline void cross_force(double* r, const double* vel, const double* f) {
+template <class R, class A, class V>
+__device__ inline void cross_force(R* r, const A* vel, const V* f) {
   r[0] = -vel[2] * f[1] + vel[1] * f[2];
   r[1] = vel[2] * f[0] - vel[0] * f[2];
   r[2] = -vel[1] * f[0] + vel[0] * f[1];
@@ -256,52 +274,58 @@ __device__ inline void cross_force(double* r, const double* vel, const double* f
 }
 
 // load a small vector into registers
-template <int N>
-__device__ __forceinline__ void ldm(double* r, const double* a) {
+template <int N, class R, class A>
+__device__ __forceinline__ void ldm(R* r, const A* a) {
 #pragma unroll
   for (int k = 0; k < N; k++) r[k] = a[k];
 }
 
-struct LdsConSink {
-  double* rec;  // contact k at rec + 7k: dist, pos[3], n[3]
-  __device__ __forceinline__ void put(int k, double d, const double* p, const double* n) const {
-    double* r = rec + 7 * k;
+template <class R>
+struct LdsConSinkT {
+  R* rec;  // contact k at rec + 7k: dist, pos[3], n[3]
+  template <class P, class N>
+  __device__ __forceinline__ void put(int k, R d, const P* p, const N* n) const {
+    R* r = rec + 7 * k;
     r[0] = d;
     r[1] = p[0]; r[2] = p[1]; r[3] = p[2];
     r[4] = n[0]; r[5] = n[1]; r[6] = n[2];
   }
 };
+using LdsConSink = LdsConSinkT<double>;
 template <class S>
-__device__ __forceinline__ int sphere_sphere(const S& out, int k, double margin, const double* p1, double r1,
-                                             const double* p2, double r2) {
-  double axis[3] = {p2[0] - p1[0], p2[1] - p1[1], p2[2] - p1[2]};
-  double dist = normalize3(axis) - r1 - r2;
+__device__ __forceinline__ int sphere_sphere(const S& out, int k, double margin, const auto* p1, double r1,
+                                             const auto* p2, double r2) {
+  using R = std::remove_cvref_t<decltype(*out.rec)>;
+  R axis[3] = {p2[0] - p1[0], p2[1] - p1[1], p2[2] - p1[2]};
+  R dist = normalize3(axis) - r1 - r2;
   if (dist > margin) return 0;
-  const double s = r1 + dist / 2;
-  const double pos[3] = {p1[0] + axis[0] * s, p1[1] + axis[1] * s, p1[2] + axis[2] * s};
+  const R s = r1 + dist / 2;
+  const R pos[3] = {p1[0] + axis[0] * s, p1[1] + axis[1] * s, p1[2] + axis[2] * s};
   out.put(k, dist, pos, axis);
   return 1;
 }
 template <class S>
-__device__ __forceinline__ int plane_sphere(const S& out, int k, double margin, const double* pos1,
-                                            const double* mat1, const double* p2, double r2) {
-  double n[3] = {mat1[2], mat1[5], mat1[8]};
-  double tmp[3] = {p2[0] - pos1[0], p2[1] - pos1[1], p2[2] - pos1[2]};
-  double cdist = dot3(tmp, n);
+__device__ __forceinline__ int plane_sphere(const S& out, int k, double margin, const auto* pos1,
+                                            const auto* mat1, const auto* p2, double r2) {
+  using R = std::remove_cvref_t<decltype(*out.rec)>;
+  R n[3] = {mat1[2], mat1[5], mat1[8]};
+  R tmp[3] = {p2[0] - pos1[0], p2[1] - pos1[1], p2[2] - pos1[2]};
+  R cdist = dot3(tmp, n);
   if (cdist > margin + r2) return 0;
-  const double dist = cdist - r2;
-  const double s = -dist / 2 - r2;
-  const double pos[3] = {p2[0] + n[0] * s, p2[1] + n[1] * s, p2[2] + n[2] * s};
+  const R dist = cdist - r2;
+  const R s = -dist / 2 - r2;
+  const R pos[3] = {p2[0] + n[0] * s, p2[1] + n[1] * s, p2[2] + n[2] * s};
   out.put(k, dist, pos, n);
   return 1;
 }
 template <class M, class S>
-__device__ __forceinline__ int narrow(const M& m, int t1, int t2, const double* pos1, const double* mat1,
-                                      const double* sz1, const double* pos2, const double* mat2, const double* sz2,
+__device__ __forceinline__ int narrow(const M& m, int t1, int t2, const auto* pos1, const auto* mat1,
+                                      const auto* sz1, const auto* pos2, const auto* mat2, const auto* sz2,
                                       double margin, const S& out) {
+  using R = std::remove_cvref_t<decltype(*out.rec)>;
   if (t1 == GEOM_PLANE && t2 == GEOM_SPHERE) return plane_sphere(out, 0, margin, pos1, mat1, pos2, sz2[0]);
   if (t1 == GEOM_PLANE && t2 == GEOM_CAPSULE) {
-    double seg[3] = {mat2[2] * sz2[1], mat2[5] * sz2[1], mat2[8] * sz2[1]}, p[3];
+    R seg[3] = {mat2[2] * sz2[1], mat2[5] * sz2[1], mat2[8] * sz2[1]}, p[3];
     int n1, n2;
     p[0] = pos2[0] + seg[0]; p[1] = pos2[1] + seg[1]; p[2] = pos2[2] + seg[2];
     n1 = plane_sphere(out, 0, margin, pos1, mat1, p, sz2[0]);
@@ -311,20 +335,20 @@ __device__ __forceinline__ int narrow(const M& m, int t1, int t2, const double* 
   }
   if (t1 == GEOM_SPHERE && t2 == GEOM_SPHERE) return sphere_sphere(out, 0, margin, pos1, sz1[0], pos2, sz2[0]);
   if (t1 == GEOM_SPHERE && t2 == GEOM_CAPSULE) {
-    double ax[3] = {mat2[2], mat2[5], mat2[8]}, dif[3], p[3], x;
+    R ax[3] = {mat2[2], mat2[5], mat2[8]}, dif[3], p[3], x;
     dif[0] = pos1[0] - pos2[0]; dif[1] = pos1[1] - pos2[1]; dif[2] = pos1[2] - pos2[2];
     x = clipd(dot3(ax, dif), -sz2[1], sz2[1]);
     p[0] = pos2[0] + ax[0] * x; p[1] = pos2[1] + ax[1] * x; p[2] = pos2[2] + ax[2] * x;
     return sphere_sphere(out, 0, margin, pos1, sz1[0], p, sz2[0]);
   }
   if (t1 == GEOM_CAPSULE && t2 == GEOM_CAPSULE) {
-    double a1[3] = {mat1[2] * sz1[1], mat1[5] * sz1[1], mat1[8] * sz1[1]};
-    double a2[3] = {mat2[2] * sz2[1], mat2[5] * sz2[1], mat2[8] * sz2[1]};
-    double dif[3] = {pos1[0] - pos2[0], pos1[1] - pos2[1], pos1[2] - pos2[2]};
-    double ma = dot3(a1, a1), mb = -dot3(a1, a2), mc = dot3(a2, a2);
-    double u = -dot3(a1, dif), v = dot3(a2, dif);
-    double det = ma * mc - mb * mb;
-    double v1[3], v2[3], x1, x2;
+    R a1[3] = {mat1[2] * sz1[1], mat1[5] * sz1[1], mat1[8] * sz1[1]};
+    R a2[3] = {mat2[2] * sz2[1], mat2[5] * sz2[1], mat2[8] * sz2[1]};
+    R dif[3] = {pos1[0] - pos2[0], pos1[1] - pos2[1], pos1[2] - pos2[2]};
+    R ma = dot3(a1, a1), mb = -dot3(a1, a2), mc = dot3(a2, a2);
+    R u = -dot3(a1, dif), v = dot3(a2, dif);
+    R det = ma * mc - mb * mb;
+    R v1[3], v2[3], x1, x2;
     if (fabs(det) >= MINVAL) {
       x1 = (mc * u - mb * v) / det;
       x2 = (ma * v - mb * u) / det;
@@ -351,7 +375,8 @@ __device__ __forceinline__ int narrow(const M& m, int t1, int t2, const double* 
   return 0;
 }
 
-__device__ inline double get_impedance(const double* solimp, double pos, double margin) {
+template <class S>
+__device__ inline double get_impedance(const S* solimp, double pos, double margin) {
   double dmin = clipd(solimp[0], MINIMP, MAXIMP), dmax = clipd(solimp[1], MINIMP, MAXIMP);
   double width = solimp[2], mid = solimp[3], power = solimp[4], x, y, imp;
   if (dmin == dmax || width <= MINVAL) return 0.5 * (dmin + dmax);

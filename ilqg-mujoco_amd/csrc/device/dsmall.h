@@ -110,10 +110,22 @@ __device__ __forceinline__ double div_ref_lane(double a, double b, double r) {
   return q;
 }
 
+// fp32 physics (coopf, the fp32 FD sweep): plain IEEE division
+__device__ __forceinline__ float rcp_ref(float) { return 0.f; }
+template <int K>
+__device__ __forceinline__ float div_ref_lane(float a, float b, float) {
+  return a / b;
+}
+// v_readlane of a float
+__device__ __forceinline__ float bcast(float x, int lane) {
+  return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(x), lane));
+}
+
 // r[idx] for a per-lane index: select chain over constant indices (written
 // with sfor so SROA sees constant subscripts and keeps r in registers)
-__device__ __forceinline__ double rsel(const double (&r)[RMAX], int idx) {
-  double v = r[0];
+template <class R>
+__device__ __forceinline__ R rsel(const R (&r)[RMAX], int idx) {
+  R v = r[0];
   sfor<1, RMAX>(SLAM(jj) { v = (idx == SK(jj)) ? r[SK(jj)] : v; });
   return v;
 }
@@ -121,9 +133,9 @@ __device__ __forceinline__ double rsel(const double (&r)[RMAX], int idx) {
 // Tree L'DL factorization of the lower triangle of `mat` (nv x nv, row-major)
 // into LD (full nv x nv, zero upper) and diaginv.  pmask[i]: proper ancestors
 // of dof i.  Mirrors coop::factor_ld's serial loop entry by entry.
-__device__ inline void factor_ld_rows(int nv, const auto& pmask, int tid, const double* mat, double* LD,
-                                      double* diaginv) {
-  double r[RMAX];
+template <class R>
+__device__ inline void factor_ld_rows(int nv, const auto& pmask, int tid, const R* mat, R* LD, R* diaginv) {
+  R r[RMAX];
   unsigned long long pm[RMAX];  // wave-uniform ancestor masks, loaded up front
   const bool own = tid < nv;
   sfor<0, RMAX>(SLAM(jj) {
@@ -137,15 +149,15 @@ __device__ inline void factor_ld_rows(int nv, const auto& pmask, int tid, const 
     constexpr int k = RMAX - 1 - SK(kk);
     if (k >= nv) return;
     const unsigned long long ak = pm[k];
-    double dk = bcast(r[k], k);
+    R dk = bcast(r[k], k);
     if (dk < MINVAL) dk = MINVAL;
-    double rk[RMAX];
+    R rk[RMAX];
     sfor<0, RMAX>(SLAM(jj) {
       constexpr int j = SK(jj);
       rk[j] = (j <= k) ? bcast(r[j], k) : 0.0;
     });
     // lanes i in anc(k): tmp_i = LD[k][i] / LD[k][k]; row i -= tmp_i * row k
-    double tmp = 0;
+    R tmp = 0;
     if (own && ((ak >> tid) & 1)) {
       tmp = rsel(rk, tid) / dk;
       sfor<0, k>(SLAM(jj) {
@@ -157,7 +169,7 @@ __device__ inline void factor_ld_rows(int nv, const auto& pmask, int tid, const 
     sfor<0, k>(SLAM(ii) {
       constexpr int i = SK(ii);
       if ((ak >> i) & 1) {
-        const double ti = bcast(tmp, i);
+        const R ti = bcast(tmp, i);
         if (tid == k) r[i] = ti;
       }
     });
@@ -178,20 +190,21 @@ __device__ inline void factor_ld_rows(int nv, const auto& pmask, int tid, const 
 // factor receives exactly the operations of factor_ld_rows.  The matrices and
 // factors are addressed as offsets from mat0 / LD0 / dinv0 (no pointer
 // selects).  nv <= RMAX <= 32.
-__device__ inline void factor_ld_rows2(int nv, const auto& pmask, int tid, const double* mat0, double* LD0,
-                                       double* diaginv0, const double* mat1, double* LD1, double* diaginv1) {
+template <class R>
+__device__ inline void factor_ld_rows2(int nv, const auto& pmask, int tid, const R* mat0, R* LD0, R* diaginv0,
+                                       const R* mat1, R* LD1, R* diaginv1) {
   const bool hi = tid >= 32;
   const int t = tid & 31;
   const int om = hi ? (int)(mat1 - mat0) : 0, ol = hi ? (int)(LD1 - LD0) : 0,
             od = hi ? (int)(diaginv1 - diaginv0) : 0;
-  const double* mat = mat0 + om;
-  double* LD = LD0 + ol;
-  double* diaginv = diaginv0 + od;
-  auto bc = [&](double x, int k) __attribute__((always_inline)) {
-    const double a = bcast(x, k), b = bcast(x, 32 + k);
+  const R* mat = mat0 + om;
+  R* LD = LD0 + ol;
+  R* diaginv = diaginv0 + od;
+  auto bc = [&](R x, int k) __attribute__((always_inline)) {
+    const R a = bcast(x, k), b = bcast(x, 32 + k);
     return hi ? b : a;
   };
-  double r[RMAX];
+  R r[RMAX];
   unsigned long long pm[RMAX];
   const bool own = t < nv;
   sfor<0, RMAX>(SLAM(jj) {
@@ -205,14 +218,14 @@ __device__ inline void factor_ld_rows2(int nv, const auto& pmask, int tid, const
     constexpr int k = RMAX - 1 - SK(kk);
     if (k >= nv) return;
     const unsigned long long ak = pm[k];
-    double dk = bc(r[k], k);
+    R dk = bc(r[k], k);
     if (dk < MINVAL) dk = MINVAL;
-    double rk[RMAX];
+    R rk[RMAX];
     sfor<0, RMAX>(SLAM(jj) {
       constexpr int j = SK(jj);
       rk[j] = (j <= k) ? bc(r[j], k) : 0.0;
     });
-    double tmp = 0;
+    R tmp = 0;
     if (own && ((ak >> t) & 1)) {
       tmp = rsel(rk, t) / dk;
       sfor<0, k>(SLAM(jj) {
@@ -223,7 +236,7 @@ __device__ inline void factor_ld_rows2(int nv, const auto& pmask, int tid, const
     sfor<0, k>(SLAM(ii) {
       constexpr int i = SK(ii);
       if ((ak >> i) & 1) {
-        const double ti = bc(tmp, i);
+        const R ti = bc(tmp, i);
         if (t == k) r[i] = ti;
       }
     });
@@ -239,10 +252,10 @@ __device__ inline void factor_ld_rows2(int nv, const auto& pmask, int tid, const
 }
 
 // x <- (L'DL)^-1 x for the factor above; mirrors coop::solve_ld.
-__device__ inline void solve_ld_rows(int nv, const auto& pmask, int tid, const double* LD,
-                                     const double* diaginv, double* x) {
+template <class R>
+__device__ inline void solve_ld_rows(int nv, const auto& pmask, int tid, const R* LD, const R* diaginv, R* x) {
   const bool own = tid < nv;
-  double row[RMAX], col[RMAX], xt = 0, dinv = 0;
+  R row[RMAX], col[RMAX], xt = 0, dinv = 0;
   unsigned long long anc = 0;
   sfor<0, RMAX>(SLAM(jj) {
     constexpr int j = SK(jj);
@@ -258,12 +271,12 @@ __device__ inline void solve_ld_rows(int nv, const auto& pmask, int tid, const d
   sfor<0, RMAX>(SLAM(ii) {
     constexpr int i = RMAX - 1 - SK(ii);
     if (i >= nv) return;
-    const double xi = bcast(xt, i);
+    const R xi = bcast(xt, i);
     if (xi != 0 && own && ((pmask[i] >> tid) & 1)) xt -= col[i] * xi;
   });
   xt *= dinv;
   // x[i] -= LD[i][j] * x[j] for j in anc(i) descending, i ascending
-  double xf[RMAX];
+  R xf[RMAX];
   sfor<0, RMAX>(SLAM(ii) {
     constexpr int i = SK(ii);
     if (i >= nv) {
@@ -285,9 +298,10 @@ __device__ inline void solve_ld_rows(int nv, const auto& pmask, int tid, const d
 
 // In-place dense Cholesky of the lower triangle of H (row-major nv x nv);
 // mirrors coop::hessian_factor's serial loop.
-__device__ inline void cholesky_rows(int nv, int tid, double* H) {
+template <class R>
+__device__ inline void cholesky_rows(int nv, int tid, R* H) {
   const bool own = tid < nv;
-  double r[RMAX];
+  R r[RMAX];
   sfor<0, RMAX>(SLAM(jj) {
     constexpr int j = SK(jj);
     r[j] = (own && j < nv && j <= tid) ? H[tid * nv + j] : 0.0;
@@ -295,20 +309,20 @@ __device__ inline void cholesky_rows(int nv, int tid, double* H) {
   sfor<0, RMAX>(SLAM(jc) {
     constexpr int j = SK(jc);
     if (j >= nv) return;
-    double rj[RMAX];  // row j, entries 0..j-1 final
+    R rj[RMAX];  // row j, entries 0..j-1 final
     sfor<0, j>(SLAM(qq) { rj[SK(qq)] = bcast(r[SK(qq)], j); });
-    double t = bcast(r[j], j);
+    R t = bcast(r[j], j);
     if (j) {
-      double s = 0;
+      R s = 0;
       sfor<0, j>(SLAM(qq) { s += rj[SK(qq)] * rj[SK(qq)]; });
       t -= s;
     }
     if (t < MINVAL) t = MINVAL;
-    const double d = sqrt(t);
-    const double tinv = 1 / d;
+    const R d = sqrt(t);
+    const R tinv = 1 / d;
     if (tid == j) r[j] = d;
     if (own && tid > j) {
-      double s = 0;
+      R s = 0;
       sfor<0, j>(SLAM(qq) { s += r[SK(qq)] * rj[SK(qq)]; });
       r[j] = (r[j] - s) * tinv;
     }
@@ -324,29 +338,30 @@ __device__ inline void cholesky_rows(int nv, int tid, double* H) {
 
 // search = -(H H')^-1 grad with the Cholesky factor in H's lower triangle;
 // mirrors the lane-0 substitution in coop::solver_newton.
-__device__ inline void chol_solve_rows(int nv, int tid, const double* H, const double* grad, double* search) {
+template <class R>
+__device__ inline void chol_solve_rows(int nv, int tid, const R* H, const R* grad, R* search) {
   const bool own = tid < nv;
-  double row[RMAX], col[RMAX], g = 0;
+  R row[RMAX], col[RMAX], g = 0;
   sfor<0, RMAX>(SLAM(jj) {
     constexpr int j = SK(jj);
     row[j] = (own && j < nv) ? H[tid * nv + j] : 0.0;
     col[j] = (own && j < nv) ? H[j * nv + tid] : 0.0;
   });
   if (own) g = grad[tid];
-  const double dg = own ? rsel(row, tid) : 1.0;
-  const double rg = rcp_ref(dg);
+  const R dg = own ? rsel(row, tid) : (R)1.0;
+  const R rg = rcp_ref(dg);
   // forward: s[i] = (s[i] - sum_{j<i} H[i][j] s[j]) / H[i][i].  Every lane
   // accumulates its dot product as the s[j] arrive (ascending j, from +0: the
   // oracle's dotn), so step i is one subtraction and the division's tail; no
   // lane-divergent branches
-  double sf[RMAX], acc = 0, gf = 0;
+  R sf[RMAX], acc = 0, gf = 0;
   sfor<0, RMAX>(SLAM(ii) {
     constexpr int i = SK(ii);
     if (i >= nv) {
       sf[i] = 0;
       return;
     }
-    const double q = div_ref_lane<i>(i ? g - acc : g, dg, rg);
+    const R q = div_ref_lane<i>(i ? g - acc : g, dg, rg);
     sf[i] = bcast(q, i);
     acc += row[i] * sf[i];
     gf = tid == i ? sf[i] : gf;
@@ -354,7 +369,7 @@ __device__ inline void chol_solve_rows(int nv, int tid, const double* H, const d
   g = gf;
   // backward: s[i] -= H[j][i] s[j] for j = i+1.. ascending, then / H[i][i];
   // the products are formed as the s[j] arrive
-  double sb[RMAX], pr[RMAX];
+  R sb[RMAX], pr[RMAX];
   sfor<0, RMAX>(SLAM(ii) {
     constexpr int i = RMAX - 1 - SK(ii);
     if (i >= nv) {
@@ -362,7 +377,7 @@ __device__ inline void chol_solve_rows(int nv, int tid, const double* H, const d
       pr[i] = 0;
       return;
     }
-    double t = g;
+    R t = g;
     sfor<i + 1, RMAX>(SLAM(jj) {
       constexpr int j = SK(jj);
       if (j < nv) t -= pr[j];

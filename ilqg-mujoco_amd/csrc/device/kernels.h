@@ -70,6 +70,13 @@ hipError_t launch_fd_cols_coop(const DevModel& m, const WsLayout& L, const coop:
                                const coop::CoopAux& X, TrajDev tr, int npts, int P, const double* qfrc_applied,
                                const double* xfrc_applied, CostDev cost, const double* warm_c, const double* cost_c,
                                double* deriv, int Ds, hipStream_t st);
+// fp32 FD sweep (kernels_fd32.hip; BASELINE.json configs[4]): centre + column
+// kernels on the fp32 physics, fp64 records; eps is the FD step (1e-3)
+size_t coop_lds_bytes_f32(const WsLayout& L, const coop::CoopLayout& C);
+hipError_t launch_fd_sweep_f32(const DevModel& m, const WsLayout& L, const coop::CoopLayout& C,
+                               const coop::CoopAux& X, TrajDev tr, int npts, int P, const double* qfrc_applied,
+                               const double* xfrc_applied, CostDev cost, double* warm_c, double* cost_c,
+                               double* deriv, int Ds, double eps, hipStream_t st);
 hipError_t launch_fd_fused_coop(const DevModel& m, const WsLayout& L, const coop::CoopLayout& C,
                                 const coop::CoopAux& X, const FdFused& a, hipStream_t st);
 hipError_t launch_rollout_coop(const DevModel& m, const WsLayout& L, const coop::CoopLayout& C,

@@ -63,7 +63,7 @@ EXPORTS = [
     "ilqg_solver_stream", "ilqg_solver_device_costs", "ilqg_solver_set_stream", "ilqg_solver_set_timing",
     "ilqg_solver_get_timing",
     "ilqg_solver_debug_set_fault", "ilqg_solver_device_traj", "ilqg_solver_set_groups", "ilqg_solver_get_groups",
-    "ilqg_solver_set_riccati", "ilqg_selftest_div",
+    "ilqg_solver_set_riccati", "ilqg_selftest_div", "ilqg_solver_set_fd_precision",
 ]
 KERNELS = ("rollout", "select", "fd_centre", "fd_cols", "backward", "fd_backward")
 
@@ -408,6 +408,12 @@ class ILQR:
         """'exact' (bit-identical to the oracle, default) or 'mfma' (matrix-core
         products, fp64; agrees to rounding): ilqg_solver_set_riccati"""
         _check(lib().ilqg_solver_set_riccati(self._h, {"exact": 0, "mfma": 1}[mode]), "set_riccati")
+
+    def set_fd_precision(self, prec: str):
+        """'f64' (the reference's arithmetic, eps 1e-6, bit-exact; default) or
+        'f32' (BASELINE.json cfg 5: fp32 FD physics, eps 1e-3, fp64 records):
+        ilqg_solver_set_fd_precision"""
+        _check(lib().ilqg_solver_set_fd_precision(self._h, {"f64": 0, "f32": 1}[prec]), "set_fd_precision")
 
     def groups(self):
         """(ngroups, roll_cus) in effect"""

@@ -174,6 +174,18 @@ int ilqg_solver_set_groups(ilqg_solver* s, int ngroups, int roll_cus);
 #define ILQG_RICCATI_MFMA 1
 int ilqg_solver_set_riccati(ilqg_solver* s, int mode);
 int ilqg_solver_get_groups(ilqg_solver* s, int* ngroups, int* roll_cus);
+/* FD sweep precision (calcMJDerivatives, src/mjderivative.cpp:212-255).  F64
+   (default): the reference's fp64 arithmetic and eps = 1e-6, bit-identical to
+   the oracle.  F32: BASELINE.json configs[4]'s "fp32 FD with fp64 Riccati" --
+   the physics of every FD evaluation in fp32 (workspace, state and arithmetic;
+   the model stays fp64), eps = ILQG_FD32_EPS (1e-6 is below fp32 resolution,
+   SURVEY.md §7(g)), fp64 records for the fp64 (exact or MFMA) recursion.
+   Agrees with the fp64 oracle at the same eps to the tolerance stated in
+   tests/test_gpu_parity.py (fp32 rounding amplified by 1/(2 eps)). */
+#define ILQG_FD_F64 0
+#define ILQG_FD_F32 1
+#define ILQG_FD32_EPS 1e-3
+int ilqg_solver_set_fd_precision(ilqg_solver* s, int prec);
 /* device pointer to the per-seed selected-candidate cost (nseed doubles), for
    an in-stream collective (RCCL all-gather) without a host round trip */
 int ilqg_solver_device_costs(ilqg_solver* s, double** dptr);

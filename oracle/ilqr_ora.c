@@ -33,7 +33,8 @@
 static int g_nthread_override = 0;
 static const int ora_niter = 30;
 static const int ora_nwarmup = 3;
-static const double ora_eps = 1e-6;
+static double ora_eps = 1e-6; /* mjderivative.cpp:39; ora_set_fd_eps for the fp32-FD tolerance tests */
+void ora_set_fd_eps(double eps) { ora_eps = eps; }
 
 void ora_set_nthread(int n) { g_nthread_override = n; }
 

@@ -33,6 +33,7 @@ typedef struct {
 } ora_ilqr;
 
 void ora_set_nthread(int n);
+void ora_set_fd_eps(double eps); /* FD step (default 1e-6, mjderivative.cpp:39) */
 int ora_get_nthread(void);
 void ora_cpMjData(const mjModel* m, mjData* dst, const mjData* src);
 mjtNum ora_cost_pendulum(const mjData* d);

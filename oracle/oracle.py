@@ -70,6 +70,7 @@ class Lib:
         L.ora_calcMJDerivatives_tuned.argtypes = [ctypes.c_void_p, ctypes.c_void_p, _dp, ctypes.c_void_p,
                                                   ctypes.POINTER(ctypes.c_void_p), ctypes.c_int]
         L.ora_set_nthread.argtypes = [ctypes.c_int]
+        L.ora_set_fd_eps.argtypes = [ctypes.c_double]
         L.ora_set_cost_desc.argtypes = [ctypes.POINTER(CostDesc)]
         L.ora_ilqr_create.restype = ctypes.c_void_p
         L.ora_ilqr_create.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p,

@@ -331,16 +331,23 @@ def test_humanoid_iterate_tangent_space(ia, ora):
     exact(v[0], oa["v"], "v")
 
 
-def _humanoid_cfg5(ia, ora, H, iters, riccati):
+def _humanoid_cfg5(ia, ora, H, iters, riccati, fdprec="f64"):
     """BASELINE.json configs[4] state: humanoid qpos0 standing at z = 1.4
     (humanoid.xml:49-50), qvel = 0, ctrl = 0; the GPU solver and the oracle
-    iterate from it"""
+    iterate from it (fdprec "f32": the GPU's fp32 FD sweep at eps 1e-3, the
+    oracle's fp64 FD at the same eps)"""
     m, om = setup(ia, ora, "humanoid", ia.HUMANOID_COST)
     st = m.reset_state(1)
     st.qpos[0, 2] = 1.4
-    il = _oracle_ilqr(ora, om, _state_dict(st, 0), H, "ora_cost_desc_fn", iters)
+    if fdprec == "f32":
+        om.lib.L.ora_set_fd_eps(FD32_EPS)
+    try:
+        il = _oracle_ilqr(ora, om, _state_dict(st, 0), H, "ora_cost_desc_fn", iters)
+    finally:
+        om.lib.L.ora_set_fd_eps(1e-6)
     g = ia.ILQR(m, st, H, ia.HUMANOID_COST)
     g.set_riccati(riccati)
+    g.set_fd_precision(fdprec)
     for _ in range(iters):
         g.iterate()
     g.synchronize()
@@ -611,3 +618,66 @@ def test_split_division_is_ieee(ia):
         assert np.array_equal(np.isnan(got), nan)
         bad = np.flatnonzero(got[~nan].view(np.int64) != want[~nan].view(np.int64))
         assert bad.size == 0, (bad.size, a[~nan][bad[:4]], b[~nan][bad[:4]], got[~nan][bad[:4]])
+
+
+# fp32 FD (BASELINE.json configs[4]: "fp32 FD with fp64 Riccati").  The FD step
+# is 1e-3; the oracle runs the same central differences in
+# fp64 at the same step, so the difference is fp32 rounding of qacc (~6e-8
+# relative) amplified by 1/(2 eps) = 500 and by the conditioning of the
+# constrained dynamics -- and, at the few evaluations where a perturbed fp32
+# state sits on the other side of a contact or limit activation than the fp64
+# one, by the jump of the dynamics there (isolated entries of order 1-10).
+# Stated tolerances on e = |d - d_ref| / (1 + |d_ref|) over every record entry
+# (measured on MI355X):
+FD32_EPS = 1e-3
+FD32_MEDIAN = 1e-3     # median e (measured 2.2e-4 humanoid)
+FD32_P99 = 0.1         # 99th percentile of e (measured 4.2e-2)
+FD32_FRAC_BIG = 5e-3   # fraction of entries with e > 0.1
+FD32_GAIN_RTOL = 0.1   # K, k, v after the H = 200 recursion, relative to each array's max
+FD32_V_RTOL = 1e-3     # V (measured 6.8e-5)
+
+
+def _fd32_stats(what, d, dref):
+    assert np.all(np.isfinite(d))
+    e = np.abs(d - dref) / (1 + np.abs(dref))
+    st = dict(median=float(np.median(e)), p99=float(np.quantile(e, 0.99)), frac_big=float(np.mean(e > 0.1)),
+              max=float(e.max()))
+    print(f"{what} fp32 FD vs fp64 oracle (eps 1e-3): {st}")
+    assert st["median"] <= FD32_MEDIAN and st["p99"] <= FD32_P99 and st["frac_big"] <= FD32_FRAC_BIG, st
+    return st
+
+
+def test_humanoid_cfg5_fp32_fd(ia, ora):
+    """cfg 5 with fp32 FD and the fp64 MFMA Riccati engine (one iteration,
+    H = 200): the rollout is the fp64 one (bit-exact); the FD records and the
+    gains agree with the fp64 oracle at eps = 1e-3 to the stated tolerances"""
+    g, il = _humanoid_cfg5(ia, ora, 200, 1, "mfma", "f32")
+    oa, ot, gt = il.arrays(), il.traj(), g.traj()
+    exact(gt.qpos.reshape(ot["qpos"].shape), ot["qpos"], "traj.qpos")
+    _fd32_stats("humanoid H=200", g.deriv()[0], oa["deriv"])
+    K, k = g.gains()
+    V, v = g.value()
+    errs = {n: _rel(a, b) for n, a, b in (("K", K[0], oa["K"]), ("k", k[0], oa["k"]), ("V", V[0], oa["V"]),
+                                          ("v", v[0], oa["v"]))}
+    print("cfg5 fp32 FD gains, max relative deviation:", errs)
+    assert errs["V"] <= FD32_V_RTOL and all(errs[n] <= FD32_GAIN_RTOL for n in ("K", "k", "v")), errs
+
+
+def test_fp32_fd_hopper_contacts(ia, ora):
+    """The fp32 FD sweep on a contact-rich model (hopper after 500 passive
+    steps, cfg 3's state; the generic kernels): records within the stated
+    tolerances of the fp64 oracle at eps = 1e-3"""
+    m, om = setup(ia, ora, "hopper", ia.HOPPER_COST)
+    st = m.reset_state(1)
+    st.ctrl[:] = -0.1
+    m.step(st, 500)
+    om.lib.L.ora_set_fd_eps(FD32_EPS)
+    try:
+        il = _oracle_ilqr(ora, om, _state_dict(st, 0), 40, "ora_cost_desc_fn", 1)
+    finally:
+        om.lib.L.ora_set_fd_eps(1e-6)
+    g = ia.ILQR(m, st, 40, ia.HOPPER_COST)
+    g.set_fd_precision("f32")
+    g.iterate()
+    g.synchronize()
+    _fd32_stats("hopper H=40", g.deriv()[0], il.arrays()["deriv"])
