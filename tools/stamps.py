@@ -19,8 +19,13 @@ NAMES = {0: "kinematics", 1: "com_pos", 2: "trn+crb", 3: "factor_ld(M)", 4: "col
 L = ia.lib()
 acc = (ctypes.c_ulonglong * 48)(); cnt = (ctypes.c_ulonglong * 48)()
 m = ia.Model.load(workloads.model_file(sys.argv[1] if len(sys.argv) > 1 else "hopper"))
-dmain = workloads.hopper_dmain(m, 1) if m.nv == 6 else workloads.pendulum_dmain(m, 1)
-g = ia.ILQR(m, dmain, 500 if m.nv == 6 else 200, ia.HOPPER_COST if m.nv == 6 else ia.PENDULUM_COST)
+if m.nq != m.nv:  # humanoid, cfg 5's state (tools/cfg5_probe.py)
+    dmain = m.reset_state(1)
+    dmain.qpos[0, 2] = 1.4
+    g = ia.ILQR(m, dmain, 200, ia.HUMANOID_COST)
+else:
+    dmain = workloads.hopper_dmain(m, 1) if m.nv == 6 else workloads.pendulum_dmain(m, 1)
+    g = ia.ILQR(m, dmain, 500 if m.nv == 6 else 200, ia.HOPPER_COST if m.nv == 6 else ia.PENDULUM_COST)
 g.iterate(); g.synchronize()
 g.set_timing(True)
 for what, fn, rd in (("rollout (1 seed)", g.forward_pass, L.ilqg_debug_stamps),
