@@ -761,6 +761,44 @@ __device__ inline void factor_ld(const auto& m, const auto& X, const Team& T, co
     LD[e] = (j <= i) ? mat[e] : 0;
   }
   TSYNC();
+  if (nv > SERIAL_NV && nv <= TEAM_SIZE && X.pmask && T.nt == TEAM_SIZE) {
+    // lane i owns row i.  For each k (descending) every proper ancestor i of k
+    // at once: tmp = LD[k][i] / LD[k][k], LD[i][j] -= tmp * LD[k][j] over j in
+    // {i} u anc(i) (descending, as the oracle), then LD[k][i] = tmp.  Within
+    // one k the oracle reads LD[k][j] only for j not yet rescaled (the walk
+    // goes up the tree and j lies above i), and each LD[i][j] is updated once,
+    // so the rows are independent: the same operations on the same operands.
+    const int i = T.tid;
+    const unsigned long long pm = i < nv ? X.pmask[i] : 0ull;  // one load; broadcast per k
+    const unsigned long long self = i < nv ? (pm | (1ull << i)) : 0ull;
+    for (int k = nv - 1; k >= 0; k--) {
+      const unsigned long long ak = bcast_u64(pm, k);
+      if (!ak) continue;  // a root dof: nothing to eliminate (the clamp below still runs)
+      real dk = LD[k * nv + k];
+      if (dk < MINVAL) dk = MINVAL;
+      TSYNC();
+      if (i == k) LD[k * nv + k] = dk;
+      const bool act = i < nv && ((ak >> i) & 1);
+      real tmp = 0;
+      if (act) {
+        tmp = LD[k * nv + i] / dk;
+        for (unsigned long long mj = self; mj;) {
+          const int j = 63 - __builtin_clzll(mj);
+          mj &= ~(1ull << j);
+          LD[i * nv + j] -= tmp * LD[k * nv + j];
+        }
+      }
+      TSYNC();
+      if (act) LD[k * nv + i] = tmp;
+      TSYNC();
+    }
+    // the clamp of root dofs (no ancestors), as the oracle's loop does for every k
+    if (i < nv && !pm && LD[i * nv + i] < MINVAL) LD[i * nv + i] = MINVAL;
+    TSYNC();
+    FOR_T(r, nv) diaginv[r] = 1 / LD[r * nv + r];
+    TSYNC();
+    return;
+  }
   if (nv <= SERIAL_NV) {
     // small trees: the oracle's loop on lane 0 beats 4 LDS round trips per k
     if (T.tid == 0) {
@@ -824,6 +862,37 @@ __device__ inline void solve_ld(const auto& m, const auto& X, const Team& T, con
   const int nv = m.nv;
   if (nv <= RMAX && X.pmask) {
     solve_ld_rows(nv, X.pmask, T.tid, LD, diaginv, x);
+    return;
+  }
+  if (nv > SERIAL_NV && nv <= TEAM_SIZE && X.pmask && T.nt == TEAM_SIZE) {
+    // lane j owns x[j]; the products LD[i][j] * x[.] are formed by the lane
+    // holding the operand (one coalesced row read per step) and applied in the
+    // oracle's order: the same operations on the same operands
+    const int j = T.tid;
+    const bool own = j < nv;
+    const unsigned long long anc = own ? X.pmask[j] : 0ull;
+    real xj = own ? x[j] : (real)0;
+    TSYNC();  // every lane has read x before it is overwritten
+    for (int i = nv - 1; i >= 0; i--) {  // x[j] -= LD[i][j] * x[i], j in anc(i)
+      const real tmp = bcast(xj, i);
+      const real lij = own ? LD[i * nv + j] : (real)0;
+      if (tmp != 0 && own && ((bcast_u64(anc, i) >> j) & 1)) xj -= lij * tmp;
+    }
+    if (own) xj *= diaginv[j];
+    for (int i = 0; i < nv; i++) {  // x[i] -= LD[i][j] * x[j], j in anc(i) descending
+      const unsigned long long ai = bcast_u64(anc, i);
+      if (!ai) continue;
+      const real pr = own ? LD[i * nv + j] * xj : (real)0;
+      real xi = bcast(xj, i);
+      for (unsigned long long mj = ai; mj;) {
+        const int q = 63 - __builtin_clzll(mj);
+        mj &= ~(1ull << q);
+        xi -= bcast(pr, q);
+      }
+      xj = j == i ? xi : xj;
+    }
+    if (own) x[j] = xj;
+    TSYNC();
     return;
   }
   if (T.tid == 0) {
@@ -1510,9 +1579,11 @@ __device__ inline void fwd_acceleration(const auto& m, const auto& L, const auto
   solve_ld(m, X, T, T.w + L.qLD, T.w + L.qLDinv, qs);
 }
 
-// constraint cost of residuals `jar`; force/state per row, qfrc_constraint per dof
+// constraint cost of residuals `jar`; force/state per row, qfrc_constraint per dof.
+// With `chg`: *chg (uniform) = some row's state differs from the one it held
+// on entry (one-wave teams; wider teams report a change unconditionally)
 __device__ inline real constraint_update(const auto& m, const auto& L, const auto& C, const Team& T,
-                                           const real* jar) {
+                                           const real* jar, int* chg = nullptr) {
   const int nv = m.nv, ne = T.iw[L.nefc];
   real* D = T.w + L.efc_D;
   real* force = T.w + L.efc_force;
@@ -1520,8 +1591,10 @@ __device__ inline real constraint_update(const auto& m, const auto& L, const aut
   real* qc = T.w + L.qfrc_con;
   int* state = T.iw + L.efc_state;
   real* term = T.c + C.cterm;
+  bool ch = false;
   FOR_T(i, ne) {
     real jr = jar[i];
+    if (chg) ch |= state[i] != (jr < 0 ? 1 : 0);
     if (jr < 0) {
       real Di = D[i];
       force[i] = -Di * jr;
@@ -1532,6 +1605,7 @@ __device__ inline real constraint_update(const auto& m, const auto& L, const aut
       state[i] = 0;
     }
   }
+  if (chg) *chg = T.nt <= 64 ? (__ballot(ch) != 0ull) : 1;
   TSYNC();
   FOR_T(j, nv) {
     real s = 0;
@@ -1555,14 +1629,28 @@ __device__ inline void hessian_factor(const auto& m, const auto& L, const auto& 
   real* D = T.w + L.efc_D;
   real* qM = T.w + L.qM;
   int* state = T.iw + L.efc_state;
-  FOR_T(e, nv * nv) {
-    int r = e / nv, c = e % nv;
-    if (c <= r) {
-      real h = 0;
+  // one lane per lower-triangle entry (r, c); the active rows walked in
+  // ascending order (as a ballot when nefc <= 64), inactive rows skipped as
+  // the oracle skips them
+  const int ntri = nv * (nv + 1) / 2;
+  const bool bal = ne <= 64 && T.nt == 64;
+  const unsigned long long am = bal ? __ballot(T.tid < ne && state[T.tid] != 0) : 0ull;
+  FOR_T(e, ntri) {
+    int r = (int)((sqrtf(8.0f * (float)e + 1.0f) - 1.0f) * 0.5f);
+    while (r * (r + 1) / 2 > e) r--;
+    while ((r + 1) * (r + 2) / 2 <= e) r++;
+    const int c = e - r * (r + 1) / 2;
+    real h = 0;
+    if (bal) {
+      for (unsigned long long mm = am; mm; mm &= mm - 1) {
+        const int i = __builtin_ctzll(mm);
+        h += J[i * nv + r] * D[i] * J[i * nv + c];
+      }
+    } else {
       for (int i = 0; i < ne; i++)
         if (state[i]) h += J[i * nv + r] * D[i] * J[i * nv + c];
-      H[e] = qM[e] + h;
     }
+    H[r * nv + c] = qM[r * nv + c] + h;
   }
   TSYNC();
   if (nv <= RMAX) {
@@ -1581,6 +1669,29 @@ __device__ inline void hessian_factor(const auto& m, const auto& L, const auto& 
       }
     }
     TSYNC();
+    return;
+  }
+  if (nv <= TEAM_SIZE && T.nt == TEAM_SIZE) {
+    // lane i owns row i: per column j every row's dot product with row j at
+    // once (the diagonal's is lane j's), the pivot broadcast from lane j
+    const int i = T.tid;
+    const bool own = i < nv;
+    for (int j = 0; j < nv; j++) {
+      const bool part = own && i >= j;
+      const real s = part ? tdot(H + i * nv, H + j * nv, j) : (real)0;
+      real t = 0;
+      if (i == j) {
+        t = H[j * nv + j];
+        if (j) t -= s;
+        if (t < MINVAL) t = MINVAL;
+        t = sqrt(t);
+      }
+      const real d = bcast(t, j);
+      const real tinv = 1 / d;
+      if (i == j) H[j * nv + j] = d;
+      if (part && i > j) H[i * nv + j] = (H[i * nv + j] - s) * tinv;
+      TSYNC();
+    }
     return;
   }
   for (int j = 0; j < nv; j++) {
@@ -1638,6 +1749,8 @@ __device__ inline void solver_newton(const auto& m, const auto& L, const auto& C
     // search = -H^-1 grad ; line search ; all on lane 0 except the parallel products
     if (nv <= RMAX) {
       chol_solve_rows(nv, T.tid, H, grad, search);
+    } else if (nv <= TEAM_SIZE) {
+      chol_solve_wave(nv, T.tid, H, grad, search);
     } else {
       if (T.tid == 0) {
         for (int i = 0; i < nv; i++) search[i] = grad[i];
@@ -1709,7 +1822,8 @@ __device__ inline void solver_newton(const auto& m, const auto& L, const auto& C
 #endif
     STAMP(17);
     real oldcost = cost;
-    ccost = constraint_update(m, L, C, T, jar);
+    int chg = 1;
+    ccost = constraint_update(m, L, C, T, jar, &chg);
     FOR_T(j, nv) grad[j] = (Ma[j] - qfs[j]) - qc[j];
     TSYNC();
     if (T.tid == 0) {
@@ -1725,7 +1839,9 @@ __device__ inline void solver_newton(const auto& m, const auto& L, const auto& C
     STAMP(18);
     cost = bc[2];
     if (bc[4] != 0) break;
-    hessian_factor(m, L, C, T, H);
+    // the factor is a function of (qM, J, D, efc_state) alone: rebuilt only
+    // when some row's state changed since it was computed (the same bits)
+    if (chg) hessian_factor(m, L, C, T, H);
     STAMP(19);
   }
 }

@@ -59,6 +59,12 @@ __device__ __forceinline__ double bcast(double x, int lane) {
   return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
 }
 
+__device__ __forceinline__ unsigned long long bcast_u64(unsigned long long x, int lane) {
+  const unsigned lo = __builtin_amdgcn_readlane((int)(x & 0xffffffffull), lane);
+  const unsigned hi = __builtin_amdgcn_readlane((int)(x >> 32), lane);
+  return ((unsigned long long)hi << 32) | lo;
+}
+
 // ---- fp64 division with the divisor's refined reciprocal computed early ----
 // The compiler's f64 division is ten dependent operations: v_div_scale of the
 // divisor, v_rcp, four fma refining that reciprocal, v_div_scale of the
@@ -387,6 +393,56 @@ __device__ inline void chol_solve_rows(int nv, int tid, const R* H, const R* gra
     gf = tid == i ? sb[i] : gf;
   });
   if (own) search[tid] = -gf;
+  team_sync();
+}
+
+// a / b where only lane k's quotient is used, k wave-uniform at run time
+__device__ __forceinline__ double div_ref_lane_rt(double a, double b, double r, int k) {
+  bool ok;
+  double q = div_tail(a, b, r, ok);
+  if (__builtin_expect((__ballot(!ok) >> k) & 1, 0)) q = div_slow(a, b);
+  return q;
+}
+__device__ __forceinline__ float div_ref_lane_rt(float a, float b, float, int) { return a / b; }
+
+// The same substitution for RMAX < nv <= TEAM_SIZE (the humanoid, nv = 27),
+// with run-time loops: lane t holds row t's running dot product (forward) and
+// its final entry; nothing but the matrix entries goes through LDS.  Mirrors the
+// lane-0 loops of coop::solver_newton entry by entry:
+//   forward  s[i] = (g[i] - sum_{j<i} H[i][j] s[j]) / H[i][i], the sum ascending
+//            from +0 (tdot) -- lane t adds H[t][i] s[i] as s[i] is broadcast;
+//   backward s[i] -= H[j][i] s[j] for j = i+1 .. nv-1 ascending, then / H[i][i]
+//            -- lane j forms its product H[j][i] s[j] (the oracle's product),
+//            and the subtractions run in the oracle's order on broadcasts.
+template <class R>
+__device__ inline void chol_solve_wave(int nv, int tid, const R* H, const R* grad, R* search) {
+  const bool own = tid < nv;
+  const R dg = own ? H[tid * nv + tid] : (R)1.0;
+  const R rg = rcp_ref(dg);
+  const R g = own ? grad[tid] : (R)0.0;
+  R acc = 0, sv = 0;
+  R h = own ? H[tid * nv] : (R)0.0;  // column 0 of lane tid's row
+  for (int i = 0; i < nv; i++) {
+    const R hn = (own && i + 1 < nv) ? H[tid * nv + i + 1] : (R)0.0;  // next column, off the chain
+    const R q = div_ref_lane_rt(i ? g - acc : g, dg, rg, i);
+    const R si = bcast(q, i);
+    sv = tid == i ? si : sv;
+    acc += h * si;
+    h = hn;
+  }
+  R sb = 0;
+  R hc = own ? H[tid * nv + nv - 1] : (R)0.0;  // H[tid][i] for i = nv-1
+  for (int i = nv - 1; i >= 0; i--) {
+    const R hcn = (own && i > 0) ? H[tid * nv + i - 1] : (R)0.0;
+    R t = bcast(sv, i);
+    const R pr = (own && tid > i) ? hc * sb : (R)0.0;
+    for (int j = i + 1; j < nv; j++) t -= bcast(pr, j);
+    const R q = div_ref_lane_rt(t, bcast(dg, i), bcast(rg, i), 0);
+    sb = tid == i ? q : sb;
+    hc = hcn;
+  }
+  team_sync();
+  if (own) search[tid] = -sb;
   team_sync();
 }
 
