@@ -78,6 +78,25 @@ __device__ __forceinline__ real tdot(const real* a, const real* b, int n) {
   for (int i = 0; i < n; i++) r += a[i] * b[i];
   return r;
 }
+// the same sum for run-time n over LDS operands: the loads of eight terms are
+// issued together (one LDS latency per eight terms instead of per term), the
+// additions stay in ascending order from +0
+__device__ __forceinline__ real tdotw(const real* a, const real* b, int n) {
+  real r = 0;
+  int i = 0;
+  for (; i + 8 <= n; i += 8) {
+    real x[8], y[8];
+#pragma unroll
+    for (int k = 0; k < 8; k++) {
+      x[k] = a[i + k];
+      y[k] = b[i + k];
+    }
+#pragma unroll
+    for (int k = 0; k < 8; k++) r += x[k] * y[k];
+  }
+  for (; i < n; i++) r += a[i] * b[i];
+  return r;
+}
 
 // ------------------------------------------------------ position stage ---
 // model traits with compile-time sizes and tables (static_models.h)
@@ -404,10 +423,9 @@ __device__ inline void kinematics(const auto& m, const auto& L, const auto& C, c
       kin_chain_par(m, T, qpos, qloc, xpos, xquat, xanchor, xaxis, T.w + L.con, []() {});
     else if (T.tid == 0)
       kin_chain_static(m, qpos, qloc, xpos, xquat, xanchor, xaxis);
-  } else if (T.tid == 0) {
-    xpos[0] = xpos[1] = xpos[2] = 0;
-    xquat[0] = 1; xquat[1] = xquat[2] = xquat[3] = 0;
-    for (int i = 1; i < m.nbody; i++) {
+  } else {
+    // body i from its parent's frame (the oracle's loop body)
+    auto walk_body = [&](int i) {
       int pid = m.body_parentid[i];
       real xp[3], xq[4], tmp[3], pq[4], bp[3], bq[4];
       ldm<4>(pq, xquat + 4 * pid);
@@ -452,6 +470,28 @@ __device__ inline void kinematics(const auto& m, const auto& L, const auto& C, c
       normalize4(xq);
       for (int k = 0; k < 3; k++) xpos[3 * i + k] = xp[k];
       for (int k = 0; k < 4; k++) xquat[4 * i + k] = xq[k];
+    };
+    const int nb = m.nbody;
+    if (nb <= TEAM_SIZE && T.nt == TEAM_SIZE) {
+      // level by level: every body at depth d at once (its parent, at depth
+      // d - 1, is final); each body's operations are the oracle's
+      const int i = T.tid;
+      int dep = 0;
+      if (i < nb)
+        for (int p = i; p > 0; p = m.body_parentid[p]) dep++;
+      if (i == 0) {
+        xpos[0] = xpos[1] = xpos[2] = 0;
+        xquat[0] = 1; xquat[1] = xquat[2] = xquat[3] = 0;
+      }
+      TSYNC();
+      for (int d = 1; __ballot(i < nb && dep >= d); d++) {
+        if (i < nb && dep == d) walk_body(i);
+        TSYNC();
+      }
+    } else if (T.tid == 0) {
+      xpos[0] = xpos[1] = xpos[2] = 0;
+      xquat[0] = 1; xquat[1] = xquat[2] = xquat[3] = 0;
+      for (int i = 1; i < nb; i++) walk_body(i);
     }
   }
   TSYNC();
@@ -1579,6 +1619,18 @@ __device__ inline void fwd_acceleration(const auto& m, const auto& L, const auto
   solve_ld(m, X, T, T.w + L.qLD, T.w + L.qLDinv, qs);
 }
 
+// s0 + v[lane 0] + v[lane 1] + ... + v[lane n-1], in that order
+__device__ __forceinline__ real lane_sum(real s0, real v, int n) {
+  for (int i = 0; i < n; i++) s0 += bcast(v, i);
+  return s0;
+}
+// the same ordered sum over the lanes of a (wave-uniform) mask only: lanes
+// outside it hold -0.0, and x + (-0.0) == x for every x, so skipping them is exact
+__device__ __forceinline__ real lane_sum_mask(real s0, real v, unsigned long long mask) {
+  for (unsigned long long mm = mask; mm; mm &= mm - 1) s0 += bcast(v, __builtin_ctzll(mm));
+  return s0;
+}
+
 // constraint cost of residuals `jar`; force/state per row, qfrc_constraint per dof.
 // With `chg`: *chg (uniform) = some row's state differs from the one it held
 // on entry (one-wave teams; wider teams report a change unconditionally)
@@ -1611,6 +1663,16 @@ __device__ inline real constraint_update(const auto& m, const auto& L, const aut
     real s = 0;
     for (int i = 0; i < ne; i++) s += J[i * nv + j] * force[i];
     qc[j] = s;
+  }
+  if (ne <= TEAM_SIZE && T.nt == TEAM_SIZE) {
+    // the active rows' terms added in row order on broadcasts (uniform)
+    const int r = T.tid;
+    const real jr = r < ne ? jar[r] : (real)0;
+    const bool act = r < ne && jr < 0;
+    const real tv = act ? 0.5 * D[r] * jr * jr : -0.0;
+    const real cost = lane_sum_mask(0.0, tv, __ballot(act));
+    TSYNC();
+    return cost;
   }
   if (T.tid == 0) {
     real cost = 0;
@@ -1678,7 +1740,7 @@ __device__ inline void hessian_factor(const auto& m, const auto& L, const auto& 
     const bool own = i < nv;
     for (int j = 0; j < nv; j++) {
       const bool part = own && i >= j;
-      const real s = part ? tdot(H + i * nv, H + j * nv, j) : (real)0;
+      const real s = part ? tdotw(H + i * nv, H + j * nv, j) : (real)0;
       real t = 0;
       if (i == j) {
         t = H[j * nv + j];
@@ -1741,6 +1803,7 @@ __device__ inline void solver_newton(const auto& m, const auto& L, const auto& C
   TSYNC();
   real cost = bc[2];
   hessian_factor(m, L, C, T, H);
+  STAMP(19);
   int iter = 0;
 #ifdef ILQG_STAMPS
   if (T.tid == 0) atomicAdd(&g_newton_calls, 1ull);
@@ -1767,11 +1830,55 @@ __device__ inline void solver_newton(const auto& m, const auto& L, const auto& C
       TSYNC();
     }
     STAMP(14);
-    FOR_T(i, nv) Mv[i] = tdot(qM + i * nv, search, nv);
-    FOR_T(i, ne) Jv[i] = tdot(J + i * nv, search, nv);
+    FOR_T(i, nv) Mv[i] = tdotw(qM + i * nv, search, nv);
+    FOR_T(i, ne) Jv[i] = tdotw(J + i * nv, search, nv);
     TSYNC();
     STAMP(15);
-    if (T.tid == 0) {
+    if (ne <= TEAM_SIZE && T.nt == TEAM_SIZE) {
+      // the same exact line search on every lane (uniform), the row sums in row
+      // order over the active rows' lanes (fwd_constraint_fast's form)
+      real alpha = 0;
+      const real snorm = sqrt(tdot(search, search, nv));
+      if (!(snorm < MINVAL)) {
+        const int r = T.tid;
+        const bool row = r < ne;
+        const real jr = row ? jar[r] : (real)0, jv = row ? Jv[r] : (real)0, Di = row ? Dv[r] : (real)0;
+        real g1 = 0, g2 = 0, d1, d2, lo = 0, hi = -1;
+        for (int j = 0; j < nv; j++) g1 += search[j] * (Ma[j] - qfs[j]);
+        for (int j = 0; j < nv; j++) g2 += search[j] * Mv[j];
+        unsigned long long pmask = 0;
+        bool have = false;
+        real d2c = 0, rd2 = 0;
+        const real c2 = Di * jv * jv;
+        auto eval = [&](real a) {
+          const real x = jr + a * jv;
+          const bool on = row && x < 0;
+          const real c1 = Di * x * jv;
+          const unsigned long long am = __ballot(on);
+          d1 = lane_sum_mask(g1 + g2 * a, c1, am);
+          if (!have || am != pmask) {
+            d2c = lane_sum_mask(g2, c2, am);
+            rd2 = rcp_ref(d2c);
+            pmask = am;
+            have = true;
+          }
+          d2 = d2c;
+        };
+        eval(0.0);
+        if (!(d1 >= 0)) {
+          const real gtol = LS_TOL * fabs(d1);
+          for (int it = 0; it < LS_ITER; it++) {
+            real anew = alpha - div_ref_lane<0>(d1, d2, rd2);
+            if (hi >= 0 && !(anew > lo && anew < hi)) anew = 0.5 * (lo + hi);
+            alpha = anew;
+            eval(alpha);
+            if (fabs(d1) < gtol) break;
+            if (d1 < 0) lo = alpha; else hi = alpha;
+          }
+        }
+      }
+      if (T.tid == 0) bc[3] = alpha;
+    } else if (T.tid == 0) {
       real alpha = 0;
       real snorm = sqrt(tdot(search, search, nv));
       if (!(snorm < MINVAL)) {
@@ -1856,18 +1963,6 @@ __device__ inline void solver_newton(const auto& m, const auto& L, const auto& C
 // Hessian factor is reused while the active set is unchanged: it is a
 // function of (qM, J, D, active set) only, so the reused factor is the one
 // the oracle recomputes, bit for bit.
-
-// s0 + v[lane 0] + v[lane 1] + ... + v[lane n-1], in that order
-__device__ __forceinline__ real lane_sum(real s0, real v, int n) {
-  for (int i = 0; i < n; i++) s0 += bcast(v, i);
-  return s0;
-}
-// the same ordered sum over the lanes of a (wave-uniform) mask only: lanes
-// outside it hold -0.0, and x + (-0.0) == x for every x, so skipping them is exact
-__device__ __forceinline__ real lane_sum_mask(real s0, real v, unsigned long long mask) {
-  for (unsigned long long mm = mask; mm; mm &= mm - 1) s0 += bcast(v, __builtin_ctzll(mm));
-  return s0;
-}
 
 // constraint_update for row registers: returns the cost (uniform) and the
 // active-row mask; with `full` also force/state and qfrc_constraint = J' force
