@@ -42,10 +42,13 @@ __device__ inline void rollout_body(const auto& m, const auto& L, const auto& C,
     if (t < nu * nx) return K[pn * nu * nx + t];
     return k[pn * nu + t - nu * nx];
   };
-  constexpr int PFR = 4;  // registers per lane: R <= 4 * 64
+  // registers per lane: R <= PFR * 64.  The run-time (generic) models take
+  // records up to 20 * 64 doubles (the humanoid's is 1231: K alone is
+  // nu x 2nv = 1134) in flight a step ahead as well
+  using MT = std::remove_cvref_t<decltype(m)>;
+  constexpr int PFR = StaticModel<MT> ? 4 : 20;
   double pf[PFR];
-  // larger records (humanoid: K alone is nu x 2nv = 1134 doubles) are not
-  // prefetched: park() copies them from global memory directly
+  // larger records are not prefetched: park() copies them from global memory directly
   const bool pfok = R <= PFR * TEAM_SIZE;
   if (!passive) {
     FOR_T(t, R) rec[t] = fetch((size_t)s * P + (P - 1), t);
@@ -74,7 +77,21 @@ __device__ inline void rollout_body(const auto& m, const auto& L, const auto& C,
       TSYNC();
       FOR_T(i, nu) {
         double t = 0;
-        for (int j = 0; j < nx; j++) t += rK[i + j * nu] * dx[j];
+        int j = 0;
+        if constexpr (!StaticModel<MT>) {
+          // run-time nx: eight terms' loads in flight at once, additions in order
+          for (; j + 8 <= nx; j += 8) {
+            double kk[8], xx[8];
+#pragma unroll
+            for (int q = 0; q < 8; q++) {
+              kk[q] = rK[i + (j + q) * nu];
+              xx[q] = dx[j + q];
+            }
+#pragma unroll
+            for (int q = 0; q < 8; q++) t += kk[q] * xx[q];
+          }
+        }
+        for (; j < nx; j++) t += rK[i + j * nu] * dx[j];
         ctrl[i] = (t + alpha * rk[i]) + ru[i];
       }
       TSYNC();
