@@ -78,6 +78,23 @@ __device__ __forceinline__ real tdot(const real* a, const real* b, int n) {
   for (int i = 0; i < n; i++) r += a[i] * b[i];
   return r;
 }
+// sum_j (Ma_j - qfs_j)(qa_j - qas_j) in ascending order, four terms' loads in flight
+__device__ __forceinline__ real gauss_w(const real* Ma, const real* qfs, const real* qa, const real* qas, int n) {
+  real g = 0;
+  int j = 0;
+  for (; j + 4 <= n; j += 4) {
+    real a[4], b[4];
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+      a[k] = Ma[j + k] - qfs[j + k];
+      b[k] = qa[j + k] - qas[j + k];
+    }
+#pragma unroll
+    for (int k = 0; k < 4; k++) g += a[k] * b[k];
+  }
+  for (; j < n; j++) g += (Ma[j] - qfs[j]) * (qa[j] - qas[j]);
+  return g;
+}
 // the same sum for run-time n over LDS operands: the loads of eight terms are
 // issued together (one LDS latency per eight terms instead of per term), the
 // additions stay in ascending order from +0
@@ -1933,19 +1950,13 @@ __device__ inline void solver_newton(const auto& m, const auto& L, const auto& C
     ccost = constraint_update(m, L, C, T, jar, &chg);
     FOR_T(j, nv) grad[j] = (Ma[j] - qfs[j]) - qc[j];
     TSYNC();
-    if (T.tid == 0) {
-      real g = 0;
-      for (int j = 0; j < nv; j++) g += (Ma[j] - qfs[j]) * (qacc[j] - qas[j]);
-      real c2 = 0.5 * g + ccost;
-      real improvement = scale * (oldcost - c2);
-      real gradient = scale * sqrt(tdot(grad, grad, nv));
-      bc[2] = c2;
-      bc[4] = (improvement < tol || gradient < tol) ? 1.0 : 0.0;
-    }
-    TSYNC();
+    // the same scalars on every lane (uniform): no LDS round trip
+    const real c2 = 0.5 * gauss_w(Ma, qfs, qacc, qas, nv) + ccost;
+    const real improvement = scale * (oldcost - c2);
+    const real gradient = scale * sqrt(tdotw(grad, grad, nv));
     STAMP(18);
-    cost = bc[2];
-    if (bc[4] != 0) break;
+    cost = c2;
+    if (improvement < tol || gradient < tol) break;
     // the factor is a function of (qM, J, D, efc_state) alone: rebuilt only
     // when some row's state changed since it was computed (the same bits)
     if (chg) hessian_factor(m, L, C, T, H);

@@ -436,6 +436,7 @@ __device__ inline void chol_solve_wave(int nv, int tid, const R* H, const R* gra
     const R hcn = (own && i > 0) ? H[tid * nv + i - 1] : (R)0.0;
     R t = bcast(sv, i);
     const R pr = (own && tid > i) ? hc * sb : (R)0.0;
+#pragma unroll 4
     for (int j = i + 1; j < nv; j++) t -= bcast(pr, j);
     const R q = div_ref_lane_rt(t, bcast(dg, i), bcast(rg, i), 0);
     sb = tid == i ? q : sb;
