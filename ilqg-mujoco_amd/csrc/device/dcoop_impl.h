@@ -1678,7 +1678,18 @@ __device__ inline real constraint_update(const auto& m, const auto& L, const aut
   TSYNC();
   FOR_T(j, nv) {
     real s = 0;
-    for (int i = 0; i < ne; i++) s += J[i * nv + j] * force[i];
+    int i = 0;
+    for (; i + 8 <= ne; i += 8) {  // eight rows' loads in flight, additions in row order
+      real jj[8], ff[8];
+#pragma unroll
+      for (int q = 0; q < 8; q++) {
+        jj[q] = J[(i + q) * nv + j];
+        ff[q] = force[i + q];
+      }
+#pragma unroll
+      for (int q = 0; q < 8; q++) s += jj[q] * ff[q];
+    }
+    for (; i < ne; i++) s += J[i * nv + j] * force[i];
     qc[j] = s;
   }
   if (ne <= TEAM_SIZE && T.nt == TEAM_SIZE) {
@@ -1807,8 +1818,8 @@ __device__ inline void solver_newton(const auto& m, const auto& L, const auto& C
   real* qc = T.w + L.qfrc_con;
   real* Dv = T.w + L.efc_D;
   real* bc = T.c + C.bc;
-  FOR_T(i, nv) Ma[i] = tdot(qM + i * nv, qacc, nv);
-  FOR_T(i, ne) jar[i] = tdot(J + i * nv, qacc, nv) - aref[i];
+  FOR_T(i, nv) Ma[i] = tdotw(qM + i * nv, qacc, nv);
+  FOR_T(i, ne) jar[i] = tdotw(J + i * nv, qacc, nv) - aref[i];
   TSYNC();
   real ccost = constraint_update(m, L, C, T, jar);
   if (T.tid == 0) {
@@ -2262,10 +2273,10 @@ __device__ inline void fwd_constraint(const auto& m, const auto& L, const auto& 
     real* qM = T.w + L.qM;
     real* qfs = T.w + L.qfrc_smooth;
     FOR_T(i, ne) {
-      b[i] = tdot(J + i * nv, qas, nv) - aref[i];
-      jar[i] = tdot(J + i * nv, warm, nv) - aref[i];
+      b[i] = tdotw(J + i * nv, qas, nv) - aref[i];
+      jar[i] = tdotw(J + i * nv, warm, nv) - aref[i];
     }
-    FOR_T(i, nv) Ma[i] = tdot(qM + i * nv, warm, nv);
+    FOR_T(i, nv) Ma[i] = tdotw(qM + i * nv, warm, nv);
     TSYNC();
     real cost_smooth = constraint_update(m, L, C, T, b);
     real cw = constraint_update(m, L, C, T, jar);
