@@ -1732,9 +1732,25 @@ __device__ inline void hessian_factor(const auto& m, const auto& L, const auto& 
     const int c = e - r * (r + 1) / 2;
     real h = 0;
     if (bal) {
-      for (unsigned long long mm = am; mm; mm &= mm - 1) {
-        const int i = __builtin_ctzll(mm);
-        h += J[i * nv + r] * D[i] * J[i * nv + c];
+      // four active rows' loads in flight at once, the terms added in row order
+      for (unsigned long long mm = am; mm;) {
+        int id[4];
+        real a[4], d[4], b[4];
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+          id[q] = mm ? __builtin_ctzll(mm) : -1;
+          mm &= mm - 1;
+        }
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+          const int i = id[q] < 0 ? id[0] : id[q];
+          a[q] = J[i * nv + r];
+          d[q] = D[i];
+          b[q] = J[i * nv + c];
+        }
+#pragma unroll
+        for (int q = 0; q < 4; q++)
+          if (id[q] >= 0) h += a[q] * d[q] * b[q];
       }
     } else {
       for (int i = 0; i < ne; i++)
