@@ -127,6 +127,70 @@ def cpu_baseline(budget_s, horizon, threads, nalpha):
     }
 
 
+def _free_port():
+    import socket
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_ranks(n, argv):
+    """`bench.py --gpus N` without a launcher: start N ranks of this script as
+    child processes (RANK / LOCAL_RANK / WORLD_SIZE / MASTER_* set, the same
+    environment torchrun gives) and return the worst child exit code.  Runs
+    before anything touches the GPU (the parent never initialises HIP); if one
+    rank fails the others are stopped rather than left waiting in a collective."""
+    env0 = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT=str(_free_port()), WORLD_SIZE=str(n),
+                LOCAL_WORLD_SIZE=str(n))
+    procs = [subprocess.Popen([sys.executable, os.path.abspath(__file__)] + argv,
+                              env=dict(env0, RANK=str(r), LOCAL_RANK=str(r))) for r in range(n)]
+    rcs = [None] * n
+    while any(rc is None for rc in rcs):
+        for i, p in enumerate(procs):
+            if rcs[i] is None:
+                rcs[i] = p.poll()
+        if any(rc not in (None, 0) for rc in rcs):
+            for i, p in enumerate(procs):
+                if rcs[i] is None:
+                    p.terminate()
+                    try:
+                        rcs[i] = p.wait(timeout=30)
+                    except subprocess.TimeoutExpired:
+                        p.kill()
+                        rcs[i] = p.wait()
+            break
+        time.sleep(0.05)
+    bad = [rc for rc in rcs if rc != 0]
+    return (bad[0] if bad[0] > 0 else 1) if bad else 0
+
+
+class DrySolver:
+    """`--dry-run`: the bench's host side (rank launch, process group, cost
+    exchange, max-over-ranks timing, rank-0 printing) on CPU with gloo and no
+    GPU.  Stands in for ilqg_amd.ILQR's iterate()/costs only; its per-seed
+    costs are a deterministic function of (global seed, iteration).  Never a
+    measurement: the line it prints carries "dry_run": true and no roofline."""
+
+    def __init__(self, S, rank):
+        self.S, self.rank, self.it = S, rank, 0
+        self.costs = torch.zeros(S, dtype=torch.float64)
+        self.stream = 0
+
+    def iterate(self):
+        self.it += 1
+        g = np.arange(seed_offset(self.rank, self.S), seed_offset(self.rank, self.S) + self.S)
+        self.costs.copy_(torch.from_numpy(np.abs(np.sin(1.0 + g * 0.37 + self.it)) * (1.0 + g)))
+
+    def synchronize(self):
+        pass
+
+    def set_timing(self, on):
+        pass
+
+    def timing(self):
+        return {}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -142,49 +206,77 @@ def main():
     # rollouts on --roll-cus CUs and the FD sweeps on the rest
     ap.add_argument("--groups", type=int, default=1)
     ap.add_argument("--roll-cus", type=int, default=128)
-    args = ap.parse_args()
+    # host-side rehearsal of the multi-rank path on CPU (gloo, no GPU, no measurement)
+    ap.add_argument("--dry-run", action="store_true")
+    argv = sys.argv[1:]
+    args = ap.parse_args(argv)
 
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        if not args.dry_run and torch.cuda.device_count() < args.gpus:  # counting does not initialise HIP
+            sys.exit(f"bench.py: --gpus {args.gpus} but {torch.cuda.device_count()} GPUs visible")
+        sys.exit(launch_ranks(args.gpus, argv))
     world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world != args.gpus:
+        sys.exit(f"bench.py: WORLD_SIZE={world} but --gpus {args.gpus}; refusing to print a mislabelled line")
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    torch.cuda.set_device(local_rank)
-    if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+    print(f"bench.py: rank {rank}/{world} started", file=sys.stderr, flush=True)
+    if args.dry_run:
+        dev = "cpu"
+        if world > 1:
+            dist.init_process_group("gloo", rank=rank, world_size=world)
+    else:
+        dev = "cuda"
+        torch.cuda.set_device(local_rank)
+        if world > 1:
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
 
     S, A, H = args.seeds_per_gpu, args.alphas, args.horizon
     P = H + 1
     alphas = tuple(2.0 ** -i for i in range(A))
     m = ia.Model.load(workloads.model_file("hopper"))
-    dmain = workloads.hopper_dmain(m, S, sigma=0.01, seed_offset=seed_offset(rank, S))
-    solver = ia.ILQR(m, dmain, H, ia.HOPPER_COST, alphas=alphas, select="min_cost", device=local_rank)
-    # one explicit stream for the solver's launches and the cost exchange: the
-    # all-gather (RCCL waits on torch's current stream) is then ordered after
-    # the iteration that produced the costs (torch's default stream is the
-    # legacy null stream, which does not order against the solver's own)
-    stream = torch.cuda.Stream()
-    solver.set_stream(stream.cuda_stream)
-    if args.groups > 1:
-        solver.set_groups(args.groups, args.roll_cus)
-    exchange = CostExchange(device_view(solver.device_costs_ptr(), S), world, solver=solver)
+    if args.dry_run:
+        solver = DrySolver(S, rank)
+        exchange = CostExchange(solver.costs, world)
+        stream = None
+    else:
+        dmain = workloads.hopper_dmain(m, S, sigma=0.01, seed_offset=seed_offset(rank, S))
+        solver = ia.ILQR(m, dmain, H, ia.HOPPER_COST, alphas=alphas, select="min_cost", device=local_rank)
+        # one explicit stream for the solver's launches and the cost exchange: the
+        # all-gather (RCCL waits on torch's current stream) is then ordered after
+        # the iteration that produced the costs (torch's default stream is the
+        # legacy null stream, which does not order against the solver's own)
+        stream = torch.cuda.Stream()
+        solver.set_stream(stream.cuda_stream)
+        if args.groups > 1:
+            solver.set_groups(args.groups, args.roll_cus)
+        exchange = CostExchange(device_view(solver.device_costs_ptr(), S), world, solver=solver)
 
     def one_step():
+        if stream is None:
+            solver.iterate()
+            return exchange()
         with torch.cuda.stream(stream):
             solver.iterate()
             return exchange()
 
+    def device_sync():
+        if not args.dry_run:
+            torch.cuda.synchronize()
+
     for _ in range(args.warmup):
         one_step()
-    torch.cuda.synchronize()
+    device_sync()
     solver.synchronize()  # raises if a fused sweep's hand-off wait timed out
     if world > 1:
         dist.barrier()
     solver.set_timing(True)
     solver.timing()  # reset
-    torch.cuda.synchronize()
+    device_sync()
     t0 = time.perf_counter()
     for _ in range(args.steps):
         best = one_step()
-    torch.cuda.synchronize()
+    device_sync()
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
@@ -192,10 +284,20 @@ def main():
     # garbage gains and costs and must not print a bench line (raises)
     solver.synchronize()
     ktime = solver.timing()
-    elapsed = max_over_ranks(elapsed, world, "cuda")
+    elapsed = max_over_ranks(elapsed, world, dev)
     best_seed = int(best.item())
+    gathered = exchange.gather()
 
     value = world * S * args.steps / elapsed
+    if args.dry_run:
+        if rank == 0:
+            print(json.dumps({"metric": METRIC, "dry_run": True, "value": None, "n_gpus": world,
+                              "steps": args.steps, "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3,
+                              "exchange": {"costs_gathered": int(gathered.numel()), "best_seed": best_seed,
+                                           "costs": gathered.tolist()}}), flush=True)
+        if world > 1:
+            dist.destroy_process_group()
+        return
     # roofline of the dominant kernel (largest device time in the timed region)
     abytes = algorithmic_bytes(m, S, A, P)
     per_kernel = {k: {"ms_total": v[0], "launches": v[1], "avg_ms": (v[0] / v[1] if v[1] else 0.0)}
@@ -246,6 +348,7 @@ def main():
                               "flops_source": "tests/fixtures/flops.json (instrumented oracle)", "kernels": valu}},
         "kernels": per_kernel,
         "best_seed": best_seed,
+        "exchange": {"costs_gathered": int(gathered.numel()), "best_seed": best_seed},
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cb = cpu_baseline(args.cpu_budget, H, args.cpu_threads, A)

@@ -191,13 +191,9 @@ struct ilqg_model {
     static_id = match_static_model(key);
   }
 
-  int upload(int device) {
-    if (dev == device && buf.p) return ILQG_OK;
-    HIPCHK(hipSetDevice(device));
+  // the cooperative LDS layouts (host-side: model scalars only)
+  void layouts() {
     const HostModel& h = host;
-    HIPCHK(buf.alloc(img.size()));
-    HIPCHK(hipMemcpy(buf.p, img.data(), img.size(), hipMemcpyHostToDevice));
-    for (auto& f : fix) *f.second = static_cast<unsigned char*>(buf.p) + f.first;
 #define ILQG_SC_I(nm) dm.nm = h.nm;
 #define ILQG_SC_F(nm) dm.nm = h.nm;
     ILQG_MODEL_I32_SCALARS(ILQG_SC_I)
@@ -206,19 +202,29 @@ struct ilqg_model {
 #undef ILQG_SC_F
     dm.maxcon = h.maxcon;
     dm.maxefc = h.maxefc;
-    dm.img = static_cast<const unsigned char*>(buf.p);
     dm.img_bytes = (int)img.size();
     dm.static_id = use_static() ? static_id : 0;
     Lc = make_layout(dm, npair);
+    C = coop::make_coop_layout(dm, npair);
+    // no LDS left for the model image (humanoid): the kernels read it from its
+    // global copy (stage_model with C.imgd == 0)
+    if (coop_lds_bytes(Lc, C) > kMaxLds) C.imgd = 0;
+  }
+
+  int upload(int device) {
+    if (dev == device && buf.p) return ILQG_OK;
+    HIPCHK(hipSetDevice(device));
+    const HostModel& h = host;
+    HIPCHK(buf.alloc(img.size()));
+    HIPCHK(hipMemcpy(buf.p, img.data(), img.size(), hipMemcpyHostToDevice));
+    for (auto& f : fix) *f.second = static_cast<unsigned char*>(buf.p) + f.first;
+    layouts();
+    dm.img = static_cast<const unsigned char*>(buf.p);
     X.isanc = reinterpret_cast<const int*>(static_cast<unsigned char*>(buf.p) + isanc_at);
     X.pair = reinterpret_cast<const int*>(static_cast<unsigned char*>(buf.p) + pair_at);
     X.npair = npair;
     X.pmask = h.nv <= 64 ? reinterpret_cast<const unsigned long long*>(static_cast<unsigned char*>(buf.p) + pmask_at)
                          : nullptr;
-    C = coop::make_coop_layout(dm, npair);
-    // no LDS left for the model image (humanoid): the kernels read it from its
-    // global copy (stage_model with C.imgd == 0)
-    if (coop_lds_bytes(Lc, C) > kMaxLds) C.imgd = 0;
     if (getenv("ILQG_VERBOSE"))
       fprintf(stderr, "ilqg: model nq=%d nv=%d static_id=%d lds/team=%zu B (ws %d + coop %d + image %d doubles, %d ints)\n",
               h.nq, h.nv, dm.static_id, coop_lds_bytes(Lc, C), Lc.nd, C.nd, C.imgd, Lc.ni + C.ni);
@@ -374,6 +380,16 @@ int ilqg_device_count(int* count) {
 static int finish_model(ilqg_model* m, ilqg_model** out) {
   m->blob = write_blob(m->host);
   m->prepare();
+  // every device path runs one physics evaluation per workgroup with its
+  // workspace in LDS: a model whose workspace exceeds one CU's 160 KB is
+  // refused here, at load, rather than at the first launch
+  m->layouts();
+  if (coop_lds_bytes(m->Lc, m->C) > kMaxLds) {
+    const size_t b = coop_lds_bytes(m->Lc, m->C);
+    delete m;
+    return fail(ILQG_ERR_UNSUPPORTED, "model workspace (" + std::to_string(b) +
+                                          " B of LDS per physics evaluation) exceeds one CU's LDS (160 KB)");
+  }
   *out = m;
   return ILQG_OK;
 }
@@ -1050,9 +1066,8 @@ int ilqg_solver_set_riccati(ilqg_solver* s, int mode) {
   if (!s || (mode != ILQG_RICCATI_EXACT && mode != ILQG_RICCATI_MFMA)) return fail(ILQG_ERR_ARG, "bad argument");
   const HostModel& h = s->model->host;
   if (mode == ILQG_RICCATI_MFMA) {
-    const int D = h.nv * (2 * h.nv + h.nu) + 2 * h.nv + h.nu;
-    if (h.nu > 32 || D > 4096 || backward_mfma_lds_bytes(h.nv, h.nu) > kMaxLds)
-      return fail(ILQG_ERR_UNSUPPORTED, "MFMA Riccati: nu <= 32, FD record <= 4096 doubles, LDS <= 160 KB");
+    if (!backward_mfma_supported(h.nv, h.nu))
+      return fail(ILQG_ERR_UNSUPPORTED, "MFMA Riccati: nu <= 32, 2 nv + 1 <= 256, FD record <= 4096 doubles, LDS <= 160 KB");
     if (!s->groups.empty()) return fail(ILQG_ERR_UNSUPPORTED, "MFMA Riccati with seed groups");
   }
   HIPCHK(s->sync_all());

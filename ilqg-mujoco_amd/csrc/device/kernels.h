@@ -36,6 +36,7 @@ size_t backward_lds_bytes(int nv, int nu);
 hipError_t launch_backward_mfma(const DevModel& m, int S, int P, double mu, const double* deriv, int Ds, TrajDev tr,
                                 double* K, double* k, double* V, double* v, hipStream_t st);
 size_t backward_mfma_lds_bytes(int nv, int nu);
+bool backward_mfma_supported(int nv, int nu);
 
 // fused FD sweep + streamed backward pass (kernels_coop.hip)
 struct FdFused {

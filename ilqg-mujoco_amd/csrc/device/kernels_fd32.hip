@@ -106,10 +106,6 @@ __global__ __launch_bounds__(TEAM32) void k_fd_cols32(DevModel m, WsLayout L, co
   float* qacc = T.w + L.qacc;
   float* temp = T.w + L.s_fd;
   load_state32(m, L, T, tr, pt, pt / P, qfrc_applied, xfrc_applied);
-  // the unperturbed fp32 state, kept for the minus side of a qpos column
-  const float q0 = T.tid < m.nq ? qpos[T.tid] : 0.f;
-  const float u0 = T.tid < nu ? ctrl[T.tid] : 0.f;
-  const float v0 = T.tid < nv ? qvel[T.tid] : 0.f;
   int kind, i, skip_minus;
   if (col < nctrl) { kind = 0; i = col; skip_minus = STAGE_VEL; }
   else if (col < nctrl + nv) { kind = 1; i = col - nctrl; skip_minus = STAGE_POS; }
@@ -124,7 +120,9 @@ __global__ __launch_bounds__(TEAM32) void k_fd_cols32(DevModel m, WsLayout L, co
       dofpos = i - m.jnt_dofadr[jid] - 3;
     }
   }
-  const float ui = __shfl(u0, i < nu ? i : 0), vi = __shfl(v0, i);
+  // the unperturbed fp32 values, re-read from the trajectory point (any nq, nv, nu)
+  const float ui = kind == 0 ? (float)tr.ctrl[(size_t)pt * nu + i] : 0.f;
+  const float vi = kind == 1 ? (float)tr.qvel[(size_t)pt * nv + i] : 0.f;
   auto perturb = [&](float h) {
     if (kind == 0) ctrl[i] = ui + h;
     else if (kind == 1) qvel[i] = vi + h;
@@ -150,7 +148,8 @@ __global__ __launch_bounds__(TEAM32) void k_fd_cols32(DevModel m, WsLayout L, co
   TSYNC();
   forward_skip(m, L, C, X, T, STAGE_NONE, FD32_NITER, 0.0);
   FOR_T(j, nv) temp[j] = qacc[j];
-  if (kind == 2 && T.tid < m.nq) qpos[T.tid] = q0;
+  // qpos undo before the minus side (mjderivative.cpp:184): the fp32 centre state
+  if (kind == 2) FOR_T(k, m.nq) qpos[k] = (float)tr.qpos[(size_t)pt * m.nq + k];
   TSYNC();
   // - side
   if (T.tid == 0) {

@@ -79,14 +79,21 @@ size_t backward_lds_bytes(int nv, int nu) {
   return nd * sizeof(double) + 2 * (size_t)nu * sizeof(int) + 16;  // + transp, perm
 }
 
-size_t backward_mfma_lds_bytes(int nv, int nu) { return rmfma::lds_doubles(nv, nu) * sizeof(double); }
+// dynamic + static LDS of k_backward_mfma (the limit check counts both)
+size_t backward_mfma_lds_bytes(int nv, int nu) {
+  return rmfma::lds_doubles(nv, nu) * sizeof(double) + rmfma::STATIC_LDS_BYTES;
+}
+bool backward_mfma_supported(int nv, int nu) {
+  const int D = nv * (2 * nv + nu) + 2 * nv + nu;
+  // stage 5 solves one right-hand side per thread: nx + 1 <= THREADS
+  return nu <= rmfma::NU_MAX && D <= rmfma::MPF * rmfma::THREADS && 2 * nv + 1 <= rmfma::THREADS &&
+         backward_mfma_lds_bytes(nv, nu) <= 160 * 1024;
+}
 
 hipError_t launch_backward_mfma(const DevModel& m, int S, int P, double mu, const double* deriv, int Ds, TrajDev tr,
                                 double* K, double* k, double* V, double* v, hipStream_t st) {
-  const int D = m.nv * (2 * m.nv + m.nu) + 2 * m.nv + m.nu;
-  if (m.nu > 32 || D > rmfma::MPF * rmfma::THREADS) return hipErrorInvalidValue;
-  const size_t lds = backward_mfma_lds_bytes(m.nv, m.nu);
-  if (lds > 160 * 1024) return hipErrorInvalidValue;
+  if (!backward_mfma_supported(m.nv, m.nu)) return hipErrorInvalidValue;
+  const size_t lds = rmfma::lds_doubles(m.nv, m.nu) * sizeof(double);  // dynamic part
   hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(k_backward_mfma),
                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   if (e != hipSuccess) return e;

@@ -27,6 +27,8 @@ namespace rmfma {
 constexpr int THREADS = 256;  // four wavefronts
 constexpr int WAVES = THREADS / 64;
 constexpr int MPF = 16;  // record prefetch registers per thread: D <= 4096
+constexpr int NU_MAX = 32;  // pivoted-LDLT permutation tables (static __shared__ below)
+constexpr size_t STATIC_LDS_BYTES = 2 * NU_MAX * sizeof(int);
 
 typedef double d4 __attribute__((ext_vector_type(4)));
 
@@ -100,7 +102,7 @@ __device__ inline void backward_seed_mfma(const MD& m, int nq, int nv, int nu, i
   double* r = col + nu;
   double* tmp = r + nu;  // nu: LDLT scratch
   double* dl = tmp + nu;  // FD record of the current step, D doubles
-  __shared__ int trn[32], perm[32];
+  __shared__ int trn[NU_MAX], perm[NU_MAX];  // STATIC_LDS_BYTES
   double* T4 = A;
   double* Vn = V;
 
@@ -201,7 +203,7 @@ __device__ inline void backward_seed_mfma(const MD& m, int nq, int nv, int nu, i
         for (int a = 0; a < nu; a++) x[a] = col[a];
     }
     {
-      const int j = lane * WAVES + wave;
+      const int j = lane * WAVES + wave;  // one column per thread: nx + 1 <= THREADS (launch_backward_mfma)
       ldlt_solve_reg(nu, Mm, perm, j < nx ? Y1 + j * LU : kl, j < nx + 1);
     }
     __syncthreads();

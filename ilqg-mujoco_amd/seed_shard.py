@@ -67,11 +67,14 @@ def broadcast_winner_control(best: int, ctrl_first: torch.Tensor, seeds_per_rank
     `best` broadcasts that seed's first control (nu doubles) to every rank.
     ctrl_first: this rank's [seeds_per_rank, nu] first controls (on the GPU, a
     view of the resident trajectory at point N).  Returns the winner's control."""
+    # owner: the rank within `group` (the all-gather concatenates in group-rank order)
     owner, local = divmod(int(best), seeds_per_rank)
     out = ctrl_first[local].clone() if owner == (dist.get_rank(group) if world > 1 else 0) else \
         torch.empty(ctrl_first.shape[1], dtype=ctrl_first.dtype, device=ctrl_first.device)
     if world > 1:
-        dist.broadcast(out, src=owner, group=group)
+        # dist.broadcast takes a global rank
+        src = owner if group is None else dist.get_global_rank(group, owner)
+        dist.broadcast(out, src=src, group=group)
     return out
 
 

@@ -68,7 +68,12 @@ const char* ilqg_last_error(void);
 int ilqg_version(void);
 int ilqg_device_count(int* count);
 
-/* ---- model: replaces mj_loadXML / mj_deleteModel (cmd/basic.cpp:123) ---- */
+/* ---- model: replaces mj_loadXML / mj_deleteModel (cmd/basic.cpp:123) ----
+   Model-size limit: every device path runs one physics evaluation per
+   workgroup with its workspace (mjData equivalent) in LDS, so the workspace
+   must fit one CU's 160 KB (the bundled humanoid, nv = 27 with 12 contact
+   slots, uses 147 KB).  A larger model is refused at load with
+   ILQG_ERR_UNSUPPORTED; the reference's CPU path has no such limit. */
 int ilqg_model_load_xml(const char* path, ilqg_model** out);
 int ilqg_model_load_xml_string(const char* xml, ilqg_model** out);
 void ilqg_model_free(ilqg_model* m);

@@ -135,3 +135,71 @@ def test_exchange_with_solver_costs_gloo(tmp_path):
         assert np.array_equal(x["gathered"], allc)
         assert int(x["best"]) == best
         assert np.array_equal(x["u"], allu[best])
+
+
+# ---- bench.py's own multi-rank path, driven through main() on CPU: the
+# launcher (bench.py --gpus N with no WORLD_SIZE starts N ranks itself), the
+# gloo process group, the per-iteration cost all-gather, max-over-ranks timing
+# and rank-0-only printing (--dry-run stands in for the GPU solver's costs)
+def _bench(args, env_extra=None, drop=("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT")):
+    import subprocess
+    env = {k: v for k, v in os.environ.items() if k not in drop}
+    env.update(env_extra or {})
+    return subprocess.run([sys.executable, os.path.join(ROOT, "bench.py")] + args, env=env,
+                          capture_output=True, text=True, timeout=300)
+
+
+def test_bench_launches_ranks_itself_dry_run():
+    import json
+    steps, warm = 2, 1
+    r = _bench(["--gpus", "2", "--dry-run", "--steps", str(steps), "--warmup", str(warm)])
+    assert r.returncode == 0, r.stderr
+    # both ranks started, and only rank 0 printed a line
+    assert "rank 0/2 started" in r.stderr and "rank 1/2 started" in r.stderr
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1
+    out = json.loads(lines[0])
+    assert out["n_gpus"] == 2 and out["dry_run"] is True and out["value"] is None
+    ex = out["exchange"]
+    assert ex["costs_gathered"] == 2 * 8
+    # the gathered costs are every global seed's, in rank order, from the last iteration
+    g = np.arange(16)
+    expect = np.abs(np.sin(1.0 + g * 0.37 + (steps + warm))) * (1.0 + g)
+    assert np.array_equal(np.array(ex["costs"]), expect)
+    assert ex["best_seed"] == int(np.argmin(expect))
+
+
+def test_bench_refuses_world_size_mismatch():
+    r = _bench(["--gpus", "4", "--dry-run", "--steps", "1", "--warmup", "0"],
+               env_extra={"WORLD_SIZE": "2", "RANK": "0", "LOCAL_RANK": "0"})
+    assert r.returncode != 0
+    assert "mislabelled" in r.stderr
+    assert not [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+
+
+def _worker_group(rank, port, outdir):
+    """world size 3; the exchange runs on the sub-group of global ranks {1, 2},
+    whose group ranks 0, 1 are global ranks 1, 2"""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=3)
+    try:
+        from seed_shard import CostExchange, broadcast_winner_control
+        grp = dist.new_group([1, 2])
+        if rank in (1, 2):
+            gr = rank - 1
+            costs = torch.tensor([5.0, 4.0] if gr == 0 else [3.0, 6.0], dtype=torch.float64)
+            u0 = torch.tensor([[10.0 * rank + j, -1.0] for j in range(2)], dtype=torch.float64)
+            ex = CostExchange(costs, 2, group=grp)
+            best = int(ex().item())  # global seed 2: group rank 1 (global rank 2), local seed 0
+            u = broadcast_winner_control(best, u0, 2, 2, group=grp)
+            np.savez(os.path.join(outdir, f"g{rank}.npz"), best=best, u=u.numpy().copy())
+    finally:
+        dist.destroy_process_group()
+
+
+def test_winner_broadcast_on_subgroup_gloo(tmp_path):
+    mp.spawn(_worker_group, args=(_free_port(), str(tmp_path)), nprocs=3, join=True)
+    for r in (1, 2):
+        x = np.load(tmp_path / f"g{r}.npz")
+        assert int(x["best"]) == 2
+        assert np.array_equal(x["u"], [20.0, -1.0])  # global rank 2's seed 0

@@ -133,3 +133,24 @@ def test_static_specialisations_selected(ia):
     anything else, e.g. the humanoid, runs the generic kernels"""
     ids = {n: ia.Model.load(model_path(n)).static_id() for n in ("inverted_pendulum", "hopper", "humanoid")}
     assert ids == {"inverted_pendulum": 1, "hopper": 2, "humanoid": 0}
+
+
+def _chain_xml(n):
+    """a planar chain of n hinged capsules over a floor (n dofs, every link can touch the floor)"""
+    body = ""
+    for i in reversed(range(n)):
+        body = (f'<body name="b{i}" pos="0 0 {0.3 if i == 0 else 0.2}"><joint name="j{i}" type="hinge" axis="0 1 0"/>'
+                f'<geom type="capsule" fromto="0 0 0 0 0 0.2" size="0.05"/>{body}</body>')
+    acts = "".join(f'<motor joint="j{i}" gear="1"/>' for i in range(n))
+    return (f'<mujoco><worldbody><geom type="plane" size="5 5 0.1"/>{body}</worldbody>'
+            f'<actuator>{acts}</actuator></mujoco>')
+
+
+def test_model_lds_limit_refused_at_load(ia):
+    """the device paths keep one evaluation's workspace in one CU's LDS
+    (include/ilqg_amd.h, model-size limit): a model over 160 KB fails cleanly
+    at load with ILQG_ERR_UNSUPPORTED (no GPU needed), a small one loads"""
+    small = ia.Model.from_string(_chain_xml(4))
+    assert (small.nv, small.nu) == (4, 4)
+    with pytest.raises(ia.IlqgError, match=r"code 4\).*exceeds one CU's LDS"):
+        ia.Model.from_string(_chain_xml(48))
