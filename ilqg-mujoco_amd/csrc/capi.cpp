@@ -243,7 +243,7 @@ struct ilqg_solver {
   int S = 0, A = 0, P = 0, D = 0, nx = 0, ncol = 0;
   // FD records at a padded stride Dp (whole 128-byte lines: handoff.h); the
   // fused sweep (fd_fused) also streams the backward pass behind the FD teams
-  int Dp = 0, WCp = 0, lag = 0, nvt = 0, cv = 0, nut = 0;
+  int Dp = 0, WCp = 0, nut = 0;
   bool fused = false;
   int riccati = ILQG_RICCATI_EXACT;  // ilqg_solver_set_riccati
   int fdprec = ILQG_FD_F64;          // ilqg_solver_set_fd_precision
@@ -456,17 +456,8 @@ static bool fused_ok(const ilqg_model* m) {
   return coop_ok(m) && h.nv <= 64 && D <= 512 && getenv_int("ILQG_FUSED", 1) != 0;
 }
 static int round16(int n) { return (n + 15) / 16 * 16; }
-// qvel columns per V team, and the lag (points) between a centre team and its column teams.
-// Default lag = P: every centre team is issued first, so column teams never wait on
-// a centre still running (hopper bench, MI355X: lag 8 -> 12.9 ms, 64 -> 11.5, P -> 10.6)
-static int fd_cv() { return std::max(1, getenv_int("ILQG_FD_CV", 1)); }
-// ctrl columns on teams of their own (1) or on the centre team (0)
-static int fd_nut(const HostModel& h) { return getenv_int("ILQG_FD_USPLIT", 1) ? std::min(h.nu, h.nv) : 0; }
-static int fd_lag(int S, int P) {
-  (void)S;
-  const int l = getenv_int("ILQG_FD_LAG", P);
-  return std::max(0, std::min(l, P));
-}
+// ctrl columns on teams of their own, min(nu, nv) of them (mjderivative.cpp:78-82)
+static int fd_nut(const HostModel& h) { return std::min(h.nu, h.nv); }
 // sync block: ticket, pad x3, cflag[npts], done[npts] (u32), padded to 16 bytes
 static size_t sync_bytes(size_t npts) { return ((4 + 2 * npts) * 4 + 15) / 16 * 16; }
 
@@ -596,7 +587,7 @@ int ilqg_fd_batch(const ilqg_model* mc, int n, const double* qpos, const double*
   TrajDev st{s.time.as<double>(), s.qpos.as<double>(), s.qvel.as<double>(), s.warm.as<double>(), s.ctrl.as<double>()};
   if (fused_ok(m)) {
     // n points as n one-point trajectories through the fused sweep (no backward roles)
-    const int Dp = round16(D), WCp = round16(h.nv + 1), cv = fd_cv();
+    const int Dp = round16(D), WCp = round16(h.nv + 1);
     DevBuf cw, sy, fl, outp;
     HIPCHK(cw.alloc((size_t)n * WCp * 8));
     HIPCHK(sy.alloc(sync_bytes(n)));
@@ -605,7 +596,7 @@ int ilqg_fd_batch(const ilqg_model* mc, int n, const double* qpos, const double*
     HIPCHK(hipMemsetAsync(fl.p, 0, 16, m->stream));
     HIPCHK(hipMemsetAsync(sy.p, 0, sync_bytes(n), m->stream));
     FdFused a{};
-    a.tr = st; a.S = n; a.P = 1; a.nB = 0; a.lag = fd_lag(n, 1); a.cv = cv; a.nvt = (h.nv + cv - 1) / cv; a.nut = fd_nut(h);
+    a.tr = st; a.S = n; a.P = 1; a.nB = 0; a.nv = h.nv; a.nut = fd_nut(h);
     a.Dp = Dp; a.WCp = WCp; a.qfrc_applied = s.qa.as<double>(); a.xfrc_applied = s.xf.as<double>(); a.cost = cd;
     a.cw = cw.as<double>(); a.deriv = outp.as<double>(); a.sync = sy.as<unsigned>(); a.fault = fl.as<unsigned>();
     HIPCHK(launch_fd_fused_coop(m->dm, m->Lc, m->C, m->X, a, m->stream));
@@ -650,10 +641,7 @@ int ilqg_solver_create(const ilqg_model* mc, const ilqg_solver_opts* o, const il
   s->Dp = round16(s->D);
   s->WCp = round16(h.nv + 1);
   s->fused = fused_ok(m);
-  s->cv = fd_cv();
-  s->nvt = (h.nv + s->cv - 1) / s->cv;
   s->nut = fd_nut(h);
-  s->lag = fd_lag(o->nseed, o->horizon + 1);
   s->host_alphas.assign(o->nalpha, 1.0);
   if (o->alphas) std::copy(o->alphas, o->alphas + o->nalpha, s->host_alphas.begin());
   s->opts.alphas = nullptr;
@@ -880,10 +868,8 @@ static hipError_t fused_launch(ilqg_solver* s, const SeedRange& r, int mode) {
   a.S = r.ns;
   a.P = s->P;
   a.nB = mode ? r.ns : 0;
-  a.lag = s->lag;
-  a.nvt = s->nvt;
+  a.nv = h.nv;
   a.nut = s->nut;
-  a.cv = s->cv;
   a.Dp = s->Dp;
   a.WCp = s->WCp;
   a.qfrc_applied = s->qfrc_applied.as<double>() + s0 * h.nv;

@@ -27,6 +27,10 @@ static __device__ unsigned long long g_stamp_acc[48];
 static __device__ unsigned long long g_stamp_cnt[48];
 static __device__ unsigned long long g_newton_iters;  // all workgroups: Newton iterations
 static __device__ unsigned long long g_newton_calls;  // all workgroups: solver calls
+// line searches of the wave-parallel Newton solver: calls, iterations, calls
+// that ran to LS_ITER, active rows summed over the evaluations, evaluations
+// whose active set differed from the previous one
+static __device__ unsigned long long g_ls[5];
 __shared__ unsigned long long s_stamp_acc[STAMP_N], s_stamp_cnt[STAMP_N], s_stamp_prev, s_stamp_prevb;
 #define STAMP_AT(lane, prev, id)                                             \
   do {                                                                       \
@@ -2219,14 +2223,34 @@ __device__ inline void fwd_constraint_fast(const auto& m, const auto& L, const a
         eval(0.0);
         if (!(d1 >= 0)) {
           real gtol = LS_TOL * fabs(d1);
+#ifdef ILQG_STAMPS
+          int it_ = 0, chg_ = 0, act_ = 0;
+#endif
           for (int it = 0; it < LS_ITER; it++) {
             real anew = alpha - div_ref_lane<0>(d1, d2, rd2);
             if (hi >= 0 && !(anew > lo && anew < hi)) anew = 0.5 * (lo + hi);
             alpha = anew;
+#ifdef ILQG_STAMPS
+            const unsigned long long pm_ = pmask;
+#endif
             eval(alpha);
+#ifdef ILQG_STAMPS
+            it_ = it + 1;
+            chg_ += pm_ != pmask;
+            act_ += __popcll(pmask);
+#endif
             if (fabs(d1) < gtol) break;
             if (d1 < 0) lo = alpha; else hi = alpha;
           }
+#ifdef ILQG_STAMPS
+          if (T.tid == 0) {
+            atomicAdd(&g_ls[0], 1ull);
+            atomicAdd(&g_ls[1], (unsigned long long)it_);
+            atomicAdd(&g_ls[2], (unsigned long long)(it_ == LS_ITER));
+            atomicAdd(&g_ls[3], (unsigned long long)act_);
+            atomicAdd(&g_ls[4], (unsigned long long)chg_);
+          }
+#endif
         }
       }
     }

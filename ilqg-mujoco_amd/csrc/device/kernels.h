@@ -38,14 +38,13 @@ hipError_t launch_backward_mfma(const DevModel& m, int S, int P, double mu, cons
 size_t backward_mfma_lds_bytes(int nv, int nu);
 bool backward_mfma_supported(int nv, int nu);
 
-// fused FD sweep + streamed backward pass (kernels_coop.hip)
+// fused FD sweep + streamed backward pass (kernels_fd.hip)
 struct FdFused {
   TrajDev tr;
   int S, P;
   int nB;        // backward roles (S, or 0 for the sweep alone)
-  int lag;       // points between a centre team and its column teams
-  int nvt, cv;   // qvel teams per point, columns per qvel team
-  int nut;       // ctrl teams per point (one per ctrl column), or 0: the centre team runs them
+  int nv;        // qvel and qpos teams per point (one column each)
+  int nut;       // ctrl teams per point, min(nu, nv) (mjderivative.cpp:78-82)
   int Dp, WCp;   // padded record strides (doubles, multiples of 16 = 128 B)
   const double* qfrc_applied;
   const double* xfrc_applied;

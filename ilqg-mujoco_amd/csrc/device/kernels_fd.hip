@@ -151,28 +151,26 @@ __global__ __launch_bounds__(TEAM, FD_WAVES_PER_EU) void k_fd_cols_s(DevModel mg
 // ---- fused FD sweep with the backward pass streamed behind it ------------
 // One launch per sweep.  A workgroup takes a ticket (an atomic counter) when it
 // starts; tickets < nB are backward-pass roles (one per seed), the rest are FD
-// teams in point-major order, terminal point first -- the order the Riccati
-// recursion consumes them (inc/ilqr.h:144):
+// teams: first every centre team C(s,p), then per point p the column teams of
+// every seed, points in the order the Riccati recursion consumes them
+// (terminal point first, inc/ilqr.h:144):
 //   C(s,p): cpMjData + mj_forward + 2 forwardSkip(VEL) (mjderivative.cpp:61-75),
-//           publishes the centre warm start and cost (then, when nut = 0, the
-//           ctrl columns (:78-111) on its own position/velocity stages, the
-//           reference's forwardSkip(mjSTAGE_VEL));
+//           publishes the centre warm start and cost;
 //   U(s,p,i): ctrl column i (:78-111) on a position/velocity stage of its own
-//           (nut > 0: the centre's 3 + 2 nu evaluations in a row were the
-//           longest chain of the sweep; a Newton solve runs up to 30 iterations
-//           at tolerance 0, :241-242);
-//   V(s,p,k): qvel columns k*cv .. (:114-142) on one position stage
-//           (forwardSkip(mjSTAGE_POS));
+//           (ctrl enters only the acceleration stage);
+//   V(s,p,i): qvel column i (:114-142);
 //   Q(s,p,i): qpos column i (:145-206).
-// U, V and Q teams run their first position/velocity stages before they wait for
-// C's warm start (those stages never read it); the U/V/Q teams of point p are
-// issued `lag` points after C(p).  A team stores its deriv entries
-// write-through and announces them on done[s,p] (handoff.h); the backward role
-// reads record p once all 1 + nut + nvt + nv teams have announced.  Every evaluation
-// reads exactly the inputs the two-kernel sweep gives it, so the records are
-// bit-identical.  Deadlock-free: a team waits only on work holding a smaller
-// ticket (already running, never waiting), the backward roles only on FD teams
-// (which never wait on them).
+// Every team runs exactly one evaluation pair and no loop around the physics
+// pipeline (a loop let the compiler hoist model reads out of it and keep them
+// live across the whole pipeline: 51 VGPRs spilled).  U, V and Q teams run
+// their first position/velocity stages before they wait for C's warm start
+// (those stages never read it).  A team stores its deriv entries write-through
+// and announces them on done[s,p] (handoff.h); the backward role reads record p
+// once all 1 + nu + 2 nv teams have announced.  Every evaluation reads exactly
+// the inputs the two-kernel sweep gives it, so the records are bit-identical.
+// Deadlock-free: a team waits only on work holding a smaller ticket (already
+// running, never waiting), the backward roles only on FD teams (which never
+// wait on them).
 __device__ inline unsigned take_ticket(unsigned* sync) {
   unsigned t = 0;
   if ((threadIdx.x & (TEAM - 1)) == 0)
@@ -180,36 +178,23 @@ __device__ inline unsigned take_ticket(unsigned* sync) {
   return __builtin_amdgcn_readfirstlane(t);
 }
 
-// FD item u -> role (0 = C, 1 = V, 2 = Q, 3 = U), seed, point, index; ntm = nut + nvt + nv
+// FD item u -> role (0 = C, 1 = V, 2 = Q, 3 = U), seed, point, index; ntm = nu + 2 nv
+// column teams per (seed, point)
 __device__ inline void fd_decode(const FdFused& a, unsigned ntm, unsigned u, int& role, int& s, int& p, int& idx) {
-  const unsigned nC = a.S, nW = a.S * ntm, lag = a.lag, P = a.P;
+  const unsigned nC = a.S * a.P, nW = a.S * ntm;
   idx = 0;
-  if (u < lag * nC) {
-    role = 0; p = u / nC; s = u % nC;
+  if (u < nC) {
+    role = 0; p = u / a.S; s = u % a.S;
     return;
   }
-  u -= lag * nC;
-  const unsigned blk = nC + nW;
-  unsigned g, o;
-  if (u < (P - lag) * blk) {
-    g = lag + u / blk;
-    o = u % blk;
-    if (o < nC) {
-      role = 0; p = g; s = o;
-      return;
-    }
-    o -= nC;
-  } else {
-    u -= (P - lag) * blk;
-    g = P + u / nW;
-    o = u % nW;
-  }
-  p = g - lag;
+  u -= nC;
+  p = u / nW;
+  const unsigned o = u % nW;
   s = o / ntm;
   const int w = o % ntm;
   if (w < a.nut) { role = 3; idx = w; }
-  else if (w < a.nut + a.nvt) { role = 1; idx = w - a.nut; }
-  else { role = 2; idx = w - a.nut - a.nvt; }
+  else if (w < a.nut + a.nv) { role = 1; idx = w - a.nut; }
+  else { role = 2; idx = w - a.nut - a.nv; }
 }
 
 __device__ inline void fd_fused_body(const auto& m, const auto& L, const auto& C, const auto& X, const Team& T,
@@ -218,7 +203,7 @@ __device__ inline void fd_fused_body(const auto& m, const auto& L, const auto& C
   const int nv = m.nv, nu = m.nu, nq = m.nq;
   const int nctrl = nu < nv ? nu : nv;  // mjderivative.cpp:78-82 (assumes nv >= nu)
   int role, s, p, idx;
-  fd_decode(a, a.nut + a.nvt + nv, u, role, s, p, idx);
+  fd_decode(a, a.nut + 2 * nv, u, role, s, p, idx);
   const int pt = s * a.P + p;
   double* dr = a.deriv + (size_t)pt * a.Dp;
   double* cwp = a.cw + (size_t)pt * a.WCp;
@@ -244,8 +229,11 @@ __device__ inline void fd_fused_body(const auto& m, const auto& L, const auto& C
     costCenter = ld_sc1(cwp + nv);
   };
   if (role == 0) {
+    // centre: mj_forward + nwarmup - 1 = 2 forwardSkip(VEL) (written out: no loop)
+    static_assert(FD_NWARMUP == 3, "centre warm-up");
     forward_skip(m, L, C, X, T, STAGE_NONE, FD_NITER, 0.0);
-    for (int rep = 1; rep < FD_NWARMUP; rep++) forward_skip(m, L, C, X, T, STAGE_VEL, FD_NITER, 0.0);
+    forward_skip(m, L, C, X, T, STAGE_VEL, FD_NITER, 0.0);
+    forward_skip(m, L, C, X, T, STAGE_VEL, FD_NITER, 0.0);
     wc = tid < nv ? warm[tid] : 0.0;
     costCenter = step_cost(m, a.cost, qpos, qvel, ctrl);
     if (tid < nv) st_sc1(cwp + tid, wc);
@@ -253,23 +241,6 @@ __device__ inline void fd_fused_body(const auto& m, const auto& L, const auto& C
     drain_stores();
     TSYNC();
     if (tid == 0) signal_set(cflag, 1u);
-    for (int i = 0; i < (a.nut ? 0 : nctrl); i++) {
-      const double u0 = ctrl[i];
-      TSYNC();
-      if (tid == 0) {
-        ctrl[i] = u0 + FD_EPS;
-        st_sc1(dr + G + 2 * nv + i, (step_cost(m, a.cost, qpos, qvel, ctrl) - costCenter) / FD_EPS);
-      }
-      set_warm();
-      forward_skip(m, L, C, X, T, STAGE_VEL, FD_NITER, 0.0);
-      const double qp = tid < nv ? qacc[tid] : 0.0;
-      if (tid == 0) ctrl[i] = u0 - FD_EPS;
-      set_warm();
-      forward_skip(m, L, C, X, T, STAGE_VEL, FD_NITER, 0.0);
-      if (tid < nv) st_sc1(dr + 2 * nv * nv + i + tid * nu, (qp - qacc[tid]) / (2 * FD_EPS));
-      if (tid == 0) ctrl[i] = u0;
-      TSYNC();
-    }
   } else if (role == 3) {
     // ctrl column idx on its own position/velocity stages (ctrl enters only the
     // acceleration stage, so they equal the centre's)
@@ -290,24 +261,21 @@ __device__ inline void fd_fused_body(const auto& m, const auto& L, const auto& C
     forward_skip(m, L, C, X, T, STAGE_VEL, FD_NITER, 0.0);
     if (tid < nv) st_sc1(dr + 2 * nv * nv + i + tid * nu, (qp - qacc[tid]) / (2 * FD_EPS));
   } else if (role == 1) {
-    const int i0 = idx * a.cv, i1 = i0 + a.cv < nv ? i0 + a.cv : nv;
-    for (int i = i0; i < i1; i++) {
-      const double v0 = qvel[i];
-      TSYNC();
-      if (tid == 0) qvel[i] = v0 + FD_EPS;
-      forward_posvel(m, L, C, X, T, i == i0 ? STAGE_NONE : STAGE_POS);
-      if (i == i0) get_centre();
-      if (tid == 0) st_sc1(dr + G + nv + i, (step_cost(m, a.cost, qpos, qvel, ctrl) - costCenter) / FD_EPS);
-      set_warm();
-      forward_acc(m, L, C, X, T, FD_NITER, 0.0);
-      const double qp = tid < nv ? qacc[tid] : 0.0;
-      if (tid == 0) qvel[i] = v0 - FD_EPS;
-      set_warm();
-      forward_skip(m, L, C, X, T, STAGE_POS, FD_NITER, 0.0);
-      if (tid < nv) st_sc1(dr + nv * nv + i + tid * nv, (qp - qacc[tid]) / (2 * FD_EPS));
-      if (tid == 0) qvel[i] = v0;
-      TSYNC();
-    }
+    // qvel column idx: + side from a position stage of its own, - side reusing it
+    const int i = idx;
+    const double v0 = qvel[i];
+    TSYNC();
+    if (tid == 0) qvel[i] = v0 + FD_EPS;
+    forward_posvel(m, L, C, X, T, STAGE_NONE);
+    get_centre();
+    if (tid == 0) st_sc1(dr + G + nv + i, (step_cost(m, a.cost, qpos, qvel, ctrl) - costCenter) / FD_EPS);
+    set_warm();
+    forward_acc(m, L, C, X, T, FD_NITER, 0.0);
+    const double qp = tid < nv ? qacc[tid] : 0.0;
+    if (tid == 0) qvel[i] = v0 - FD_EPS;
+    set_warm();
+    forward_skip(m, L, C, X, T, STAGE_POS, FD_NITER, 0.0);
+    if (tid < nv) st_sc1(dr + nv * nv + i + tid * nv, (qp - qacc[tid]) / (2 * FD_EPS));
   } else {
     const int i = idx;
     const int jid = m.dof_jntid[i];
@@ -368,7 +336,7 @@ __device__ inline void fd_backward_role(const MD& mg, const FdFused& a, int s) {
   if (s == 0 && threadIdx.x == 0) g_fused_diag[3] = t0_;
 #endif
   backward_seed<NV, NU>(mg, mg.nq, mg.nv, mg.nu, a.P, mg.opt_timestep, a.mu, a.deriv, a.Dp, a.tr, a.K, a.k, a.V,
-                        a.v, s, threadIdx.x, lds, a.sync + 4 + (size_t)a.S * a.P, (unsigned)(1 + a.nut + a.nvt + mg.nv),
+                        a.v, s, threadIdx.x, lds, a.sync + 4 + (size_t)a.S * a.P, (unsigned)(1 + a.nut + 2 * a.nv),
                         a.fault);
 #ifdef ILQG_STAMPS
   if (s < 16 && threadIdx.x == 0) g_fused_diag[8 + s] = __builtin_amdgcn_s_memtime() - t0_;
@@ -393,24 +361,9 @@ __global__ __launch_bounds__(TEAM, FD_WAVES_PER_EU) void k_fd_fused_coop(DevMode
   fd_fused_body(m, L, C, X, T, a, t - a.nB);
 }
 
-template <class SM, class SX>
-__global__ __launch_bounds__(TEAM, FD_WAVES_PER_EU) void k_fd_fused_s(DevModel mg, FdFused a) {
-  const unsigned t = take_ticket(a.sync);
-  if (t < (unsigned)a.nB) {
-    fd_backward_role<SM::nv, SM::nu>(mg, a, (int)t);
-    return;
-  }
-  static constexpr WsLayout L = make_layout(SM{}, SX::npair);
-  static constexpr CoopLayout C = make_coop_layout(SM{}, SX::npair);
-  static constexpr SX X{};
-  Team T = make_team(L, C);
-  SM m;
-  stage_model_s(mg, L, C, T, m);
-  fd_fused_body(m, L, C, X, T, a, t - a.nB);
-}
-
-// the same with the model read from its global image (L1/L2 cached) instead of
-// an LDS copy: the team's LDS drops by the image, so more teams fit a CU
+// compile-time models: the model read from its global image (L1/L2 cached)
+// rather than an LDS copy, so the team's LDS holds only the workspace (8 teams
+// per CU for the hopper instead of 7)
 template <class SM, class SX>
 __global__ __launch_bounds__(TEAM, FD_WAVES_PER_EU) void k_fd_fused_g(DevModel mg, FdFused a) {
   const unsigned t = take_ticket(a.sync);
@@ -490,34 +443,21 @@ hipError_t launch_fd_cols_coop(const DevModel& m, const WsLayout& L, const CoopL
   return hipGetLastError();
 }
 
-static bool fd_global_image() {
-  const char* e = getenv("ILQG_FD_GIMG");
-  return !(e && *e == '0');  // default on (ILQG_FD_GIMG=0: LDS copy)
-}
-
 hipError_t launch_fd_fused_coop(const DevModel& m, const WsLayout& L, const CoopLayout& C, const CoopAux& X,
                                 const FdFused& a, hipStream_t st) {
-  const long items = (long)a.S * a.P * (1 + a.nut + a.nvt + m.nv);
+  const long items = (long)a.S * a.P * (1 + a.nut + 2 * m.nv);
   const long blocks = items + a.nB;
   if (items <= 0) return hipSuccess;
   size_t lds = coop_lds_bytes(L, C);
   if (a.nB > 0) lds = std::max(lds, backward_lds_bytes(m.nv, m.nu));
   hipError_t e;
-  const bool gimg = fd_global_image();
   const size_t lds_g = std::max((size_t)(L.nd + C.nd) * sizeof(double) + (size_t)(L.ni + C.ni) * sizeof(int),
                                 a.nB > 0 ? backward_lds_bytes(m.nv, m.nu) : (size_t)0);
 #define ILQG_CASE(id, SMT, SXT)                                                                                 \
   case id:                                                                                                      \
-    if (gimg) {                                                                                                 \
-      e = allow_lds(k_fd_fused_g<stat::SMT, stat::SXT>, lds_g);                                                 \
-      if (e != hipSuccess) return e;                                                                            \
-      hipLaunchKernelGGL((k_fd_fused_g<stat::SMT, stat::SXT>), dim3((unsigned)blocks), dim3(TEAM), lds_g, st, m, \
-                         a);                                                                                    \
-      return hipGetLastError();                                                                                 \
-    }                                                                                                           \
-    e = allow_lds(k_fd_fused_s<stat::SMT, stat::SXT>, lds);                                                     \
+    e = allow_lds(k_fd_fused_g<stat::SMT, stat::SXT>, lds_g);                                                   \
     if (e != hipSuccess) return e;                                                                              \
-    hipLaunchKernelGGL((k_fd_fused_s<stat::SMT, stat::SXT>), dim3((unsigned)blocks), dim3(TEAM), lds, st, m, a); \
+    hipLaunchKernelGGL((k_fd_fused_g<stat::SMT, stat::SXT>), dim3((unsigned)blocks), dim3(TEAM), lds_g, st, m, a); \
     return hipGetLastError();
   switch (m.static_id) {
     ILQG_STATIC_MODELS(ILQG_CASE)
@@ -545,6 +485,15 @@ extern "C" int ilqg_debug_fused(unsigned long long* d, int reset) {
 #endif
 
 #ifdef ILQG_STAMPS
+// the FD kernels' line-search counters (dcoop_impl.h g_ls)
+extern "C" int ilqg_debug_ls_fd(unsigned long long* out5, int reset) {
+  if (hipMemcpyFromSymbol(out5, HIP_SYMBOL(ilqg::coop::g_ls), sizeof(unsigned long long) * 5) != hipSuccess) return 3;
+  if (reset) {
+    unsigned long long z[5] = {0};
+    (void)hipMemcpyToSymbol(HIP_SYMBOL(ilqg::coop::g_ls), z, sizeof(z));
+  }
+  return 0;
+}
 // the FD kernels' copy of the stamp counters (tools/stamps.py)
 extern "C" int ilqg_debug_stamps_fd(unsigned long long* acc, unsigned long long* cnt, int reset) {
   if (hipMemcpyFromSymbol(acc, HIP_SYMBOL(ilqg::coop::g_stamp_acc), sizeof(unsigned long long) * 48) != hipSuccess)

@@ -449,6 +449,15 @@ hipError_t launch_forward_coop(const DevModel& m, const WsLayout& L, const CoopL
 }  // namespace ilqg
 
 #ifdef ILQG_STAMPS
+// the rollout kernels' line-search counters (dcoop_impl.h g_ls)
+extern "C" int ilqg_debug_ls_rollout(unsigned long long* out5, int reset) {
+  if (hipMemcpyFromSymbol(out5, HIP_SYMBOL(ilqg::coop::g_ls), sizeof(unsigned long long) * 5) != hipSuccess) return 3;
+  if (reset) {
+    unsigned long long z[5] = {0};
+    (void)hipMemcpyToSymbol(HIP_SYMBOL(ilqg::coop::g_ls), z, sizeof(z));
+  }
+  return 0;
+}
 extern "C" int ilqg_debug_stamps(unsigned long long* acc, unsigned long long* cnt, int reset) {
   if (hipMemcpyFromSymbol(acc, HIP_SYMBOL(ilqg::coop::g_stamp_acc), sizeof(unsigned long long) * 48) != hipSuccess)
     return 3;

@@ -424,15 +424,11 @@ def test_riccati_mfma_step(ia, fixture):
     assert all(e <= 1e-12 for e in errs.values()), errs
 
 
-@pytest.mark.parametrize("env", [{"ILQG_FUSED": "0"}, {"ILQG_FD_LAG": "0"}, {"ILQG_FD_LAG": "1"},
-                                 {"ILQG_FD_LAG": "7", "ILQG_FD_CV": "1"}, {"ILQG_FD_CV": "6"},
-                                 {"ILQG_FD_USPLIT": "0"}, {"ILQG_FD_USPLIT": "0", "ILQG_FD_LAG": "3"},
-                                 {"ILQG_FD_GIMG": "1"}, {"ILQG_FD_GIMG": "0"}])
+@pytest.mark.parametrize("env", [{}, {"ILQG_FUSED": "0"}])
 def test_fused_sweep_schedules(ia, ora, env, monkeypatch):
-    """The fused FD sweep + streamed backward pass (k_fd_fused_s): every hand-off
-    schedule (centre lag, qvel columns per team, ctrl columns on their own teams
-    or the centre's) and the two-kernel sweep give the
-    oracle's iterate bit for bit (seeds x points x columns vary the ticket order)"""
+    """The fused FD sweep + streamed backward pass (k_fd_fused_g) and the
+    two-kernel sweep (ILQG_FUSED=0) give the oracle's iterate bit for bit
+    (3 seeds x 41 points x 16 column teams: the ticket order interleaves seeds)"""
     import workloads
     for k, v in env.items():
         monkeypatch.setenv(k, v)

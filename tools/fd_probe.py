@@ -1,7 +1,7 @@
 """Probe: per-kernel times of the bench workload's pieces (HIP events):
 fused FD sweep alone, standalone backward pass, and the fused sweep with the
-backward pass streamed behind it (iterate).  Env knobs ILQG_FD_LAG / ILQG_FD_CV
-/ ILQG_FUSED apply.   python tools/fd_probe.py [label]"""
+backward pass streamed behind it (iterate).  ILQG_FUSED=0 selects the
+two-kernel sweep.   python tools/fd_probe.py [label]"""
 import os
 import sys
 

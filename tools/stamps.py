@@ -28,13 +28,20 @@ else:
     g = ia.ILQR(m, dmain, 500 if m.nv == 6 else 200, ia.HOPPER_COST if m.nv == 6 else ia.PENDULUM_COST)
 g.iterate(); g.synchronize()
 g.set_timing(True)
-for what, fn, rd in (("rollout (1 seed)", g.forward_pass, L.ilqg_debug_stamps),
-                     ("fd sweep", g.fd_sweep, L.ilqg_debug_stamps_fd)):
+ls = (ctypes.c_ulonglong * 5)()
+for what, fn, rd, rls in (("rollout (1 seed)", g.forward_pass, L.ilqg_debug_stamps, L.ilqg_debug_ls_rollout),
+                          ("fd sweep", g.fd_sweep, L.ilqg_debug_stamps_fd, L.ilqg_debug_ls_fd)):
     rd(acc, cnt, 1)
+    rls(ls, 1)
     g.timing()
     fn(); g.synchronize()
     tm = g.timing()
     rd(acc, cnt, 1)
+    rls(ls, 1)
+    if ls[0]:
+        print(f"   line searches (all workgroups): {ls[0]} calls, {ls[1] / ls[0]:.2f} iterations per call, "
+              f"{ls[2]} ran to LS_ITER, {ls[3] / max(ls[1], 1):.2f} active rows per evaluation, "
+              f"active set changed in {ls[4] / max(ls[1], 1):.1%} of evaluations")
     # wave 0's stamps partition its time: top-level stages, their sub-stages
     # (11-23: kinematics and Newton pieces, which restart the stage clock) and
     # the barrier waits
