@@ -27,10 +27,30 @@ static __device__ unsigned long long g_stamp_acc[48];
 static __device__ unsigned long long g_stamp_cnt[48];
 static __device__ unsigned long long g_newton_iters;  // all workgroups: Newton iterations
 static __device__ unsigned long long g_newton_calls;  // all workgroups: solver calls
-// line searches of the wave-parallel Newton solver: calls, iterations, calls
-// that ran to LS_ITER, active rows summed over the evaluations, evaluations
-// whose active set differed from the previous one
-static __device__ unsigned long long g_ls[5];
+// line searches of the wave-parallel Newton solver: [0] calls, [1] iterations,
+// [2] calls that ran to LS_ITER, [3] constraint rows summed over the calls,
+// [4] calls on the uniform-row form (ne <= LS_NE), [5] cycles in line searches,
+// [6] cycles in fwd_constraint_fast, [7] FD team lifetimes (kernels_fd.hip)
+static __device__ unsigned long long g_ls[8];
+// the same counted per workgroup in LDS (lane 0 of wave 0) and added to the
+// globals once when the workgroup ends: per-event global atomics from
+// thousands of teams distorted the timings they measure ([8], [9]: Newton
+// iterations and solver calls)
+__shared__ unsigned long long s_cnt[10];
+__device__ __forceinline__ void cnt_add_g(unsigned long long* g, unsigned long long v) {
+  if (v) __hip_atomic_fetch_add(g, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void cnt_flush() {
+  const unsigned long long c0 = s_cnt[0], c1 = s_cnt[1], c2 = s_cnt[2], c3 = s_cnt[3], c4 = s_cnt[4];
+  const unsigned long long c5 = s_cnt[5], c6 = s_cnt[6], c7 = s_cnt[7], c8 = s_cnt[8], c9 = s_cnt[9];
+  cnt_add_g(g_ls + 0, c0); cnt_add_g(g_ls + 1, c1); cnt_add_g(g_ls + 2, c2); cnt_add_g(g_ls + 3, c3);
+  cnt_add_g(g_ls + 4, c4); cnt_add_g(g_ls + 5, c5); cnt_add_g(g_ls + 6, c6); cnt_add_g(g_ls + 7, c7);
+  cnt_add_g(&g_newton_iters, c8); cnt_add_g(&g_newton_calls, c9);
+}
+#define CNT_ADD(i, v)                     \
+  do {                                    \
+    if (threadIdx.x == 0) __hip_atomic_fetch_add(&s_cnt[i], (unsigned long long)(v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP); \
+  } while (0)
 __shared__ unsigned long long s_stamp_acc[STAMP_N], s_stamp_cnt[STAMP_N], s_stamp_prev, s_stamp_prevb;
 #define STAMP_AT(lane, prev, id)                                             \
   do {                                                                       \
@@ -48,18 +68,24 @@ __shared__ unsigned long long s_stamp_acc[STAMP_N], s_stamp_cnt[STAMP_N], s_stam
 #define STAMPB(id) STAMP_AT(64, s_stamp_prevb, id)
 #define STAMP_INIT()                                                         \
   do {                                                                       \
-    if (threadIdx.x == 0 && blockIdx.x == 0) {                               \
-      for (int i_ = 0; i_ < STAMP_N; i_++) s_stamp_acc[i_] = s_stamp_cnt[i_] = 0; \
-      s_stamp_prev = s_stamp_prevb = __builtin_amdgcn_s_memtime();           \
+    if (threadIdx.x == 0) {                                                  \
+      for (int i_ = 0; i_ < 10; i_++) s_cnt[i_] = 0;                         \
+      if (blockIdx.x == 0) {                                                 \
+        for (int i_ = 0; i_ < STAMP_N; i_++) s_stamp_acc[i_] = s_stamp_cnt[i_] = 0; \
+        s_stamp_prev = s_stamp_prevb = __builtin_amdgcn_s_memtime();         \
+      }                                                                      \
     }                                                                        \
   } while (0)
 #define STAMP_FLUSH()                                                        \
   do {                                                                       \
-    if (threadIdx.x == 0 && blockIdx.x == 0)                                 \
-      for (int i_ = 0; i_ < STAMP_N; i_++) {                                 \
-        g_stamp_acc[i_] += s_stamp_acc[i_];                                  \
-        g_stamp_cnt[i_] += s_stamp_cnt[i_];                                  \
-      }                                                                      \
+    if (threadIdx.x == 0) {                                                  \
+      cnt_flush();                                                           \
+      if (blockIdx.x == 0)                                                   \
+        for (int i_ = 0; i_ < STAMP_N; i_++) {                               \
+          g_stamp_acc[i_] += s_stamp_acc[i_];                                \
+          g_stamp_cnt[i_] += s_stamp_cnt[i_];                                \
+        }                                                                    \
+    }                                                                        \
   } while (0)
 #else
 #define STAMP(id) \
@@ -1821,6 +1847,105 @@ __device__ inline void hessian_factor(const auto& m, const auto& L, const auto& 
   }
 }
 
+// ---- the exact line search's iterations (oracle linesearch), rows uniform --
+// After the lane form's eval(0) (one constraint row per lane), a solve with
+// NE <= LS_NE rows copies rows 0..NE-1 (jr, jv, D, D jv^2) into wave-uniform
+// registers once, and each iteration then forms every row's term on every
+// lane and adds the active ones in row order -- the oracle's expressions and
+// order, inactive rows adding -0.0 (the exact identity) -- with no cross-lane
+// operation on the chain d1 -> step -> x -> term -> d1.  The active set is
+// still taken lane-parallel (one ballot), and d2 and its reciprocal are formed
+// again only when it changes.  At tolerance 0 (the FD solves,
+// mjderivative.cpp:241-242) most line searches run all LS_ITER iterations.
+#ifndef ILQG_LS_NE
+#define ILQG_LS_NE 8
+#endif
+constexpr int LS_NE = ILQG_LS_NE;
+template <int NE>
+__device__ inline real ls_iterate_rows(real g1, real g2, real jr, real jv, real Di, real c2, bool row, real d1,
+                                       real d2c, real rd2, unsigned long long pmask, real gtol, int& iters) {
+  real ujr[NE], ujv[NE], uD[NE], uc2[NE];
+  sfor<0, NE>(SLAM(jj) {
+    constexpr int j = SK(jj);
+    ujr[j] = bcast(jr, j);
+    ujv[j] = bcast(jv, j);
+    uD[j] = bcast(Di, j);
+    uc2[j] = bcast(c2, j);
+  });
+  real alpha = 0, lo = 0, hi = -1;
+  int it = 0;
+  while (it < LS_ITER) {
+    real anew = alpha - div_ref_lane<0>(d1, d2c, rd2);
+    if (hi >= 0 && !(anew > lo && anew < hi)) anew = 0.5 * (lo + hi);
+    alpha = anew;
+    const unsigned long long am = __ballot(row && jr + alpha * jv < 0);
+    real s = g1 + g2 * alpha;
+    bool act[NE];
+    sfor<0, NE>(SLAM(jj) {
+      constexpr int j = SK(jj);
+      const real x = ujr[j] + alpha * ujv[j];
+      const real t = uD[j] * x * ujv[j];
+      act[j] = x < 0;
+      s += act[j] ? t : (real)-0.0;
+    });
+    d1 = s;
+    it++;
+    if (am != pmask) {
+      real d2 = g2;
+      sfor<0, NE>(SLAM(jj) { d2 += act[SK(jj)] ? uc2[SK(jj)] : (real)-0.0; });
+      d2c = d2;
+      rd2 = rcp_ref(d2c);
+      pmask = am;
+    }
+    if (__ballot(fabs(d1) < gtol) != 0) break;  // uniform
+    if (d1 < 0) lo = alpha; else hi = alpha;
+  }
+  iters = it;
+  return alpha;
+}
+
+// the line search from the lane form's state after eval(0): returns alpha
+__device__ inline real ls_iterate(int ne, real g1, real g2, real jr, real jv, real Di, real c2, bool row, real d1,
+                                  real d2c, real rd2, unsigned long long pmask, int& iters) {
+  const real gtol = LS_TOL * fabs(d1);
+  switch (ne) {
+#define ILQG_LS_CASE(n)                                                                     \
+  case n:                                                                                   \
+    if constexpr (n <= LS_NE) return ls_iterate_rows<n>(g1, g2, jr, jv, Di, c2, row, d1, d2c, rd2, pmask, gtol, iters); \
+    break;
+    ILQG_LS_CASE(1) ILQG_LS_CASE(2) ILQG_LS_CASE(3) ILQG_LS_CASE(4)
+    ILQG_LS_CASE(5) ILQG_LS_CASE(6) ILQG_LS_CASE(7) ILQG_LS_CASE(8)
+#undef ILQG_LS_CASE
+    default:
+      break;
+  }
+  // more rows: the terms stay on their lanes, summed in lane order over the
+  // active ones
+  real alpha = 0, lo = 0, hi = -1, d2 = d2c;
+  int it = 0;
+  while (it < LS_ITER) {
+    real anew = alpha - div_ref_lane<0>(d1, d2, rd2);
+    if (hi >= 0 && !(anew > lo && anew < hi)) anew = 0.5 * (lo + hi);
+    alpha = anew;
+    const real x = jr + alpha * jv;
+    const bool on = row && x < 0;
+    const real c1 = Di * x * jv;
+    const unsigned long long am = __ballot(on);
+    d1 = lane_sum_mask(g1 + g2 * alpha, c1, am);
+    if (am != pmask) {
+      d2c = lane_sum_mask(g2, c2, am);
+      rd2 = rcp_ref(d2c);
+      pmask = am;
+    }
+    d2 = d2c;
+    it++;
+    if (fabs(d1) < gtol) break;
+    if (d1 < 0) lo = alpha; else hi = alpha;
+  }
+  iters = it;
+  return alpha;
+}
+
 __device__ inline void solver_newton(const auto& m, const auto& L, const auto& C, const Team& T,
                                      int maxiter, real tol) {
   const int nv = m.nv, ne = T.iw[L.nefc];
@@ -1854,7 +1979,7 @@ __device__ inline void solver_newton(const auto& m, const auto& L, const auto& C
   STAMP(19);
   int iter = 0;
 #ifdef ILQG_STAMPS
-  if (T.tid == 0) atomicAdd(&g_newton_calls, 1ull);
+  CNT_ADD(9, 1ull);
 #endif
   while (iter < maxiter) {
     // search = -H^-1 grad ; line search ; all on lane 0 except the parallel products
@@ -1891,7 +2016,7 @@ __device__ inline void solver_newton(const auto& m, const auto& L, const auto& C
         const int r = T.tid;
         const bool row = r < ne;
         const real jr = row ? jar[r] : (real)0, jv = row ? Jv[r] : (real)0, Di = row ? Dv[r] : (real)0;
-        real g1 = 0, g2 = 0, d1, d2, lo = 0, hi = -1;
+        real g1 = 0, g2 = 0, d1, d2;
         for (int j = 0; j < nv; j++) g1 += search[j] * (Ma[j] - qfs[j]);
         for (int j = 0; j < nv; j++) g2 += search[j] * Mv[j];
         unsigned long long pmask = 0;
@@ -1914,15 +2039,8 @@ __device__ inline void solver_newton(const auto& m, const auto& L, const auto& C
         };
         eval(0.0);
         if (!(d1 >= 0)) {
-          const real gtol = LS_TOL * fabs(d1);
-          for (int it = 0; it < LS_ITER; it++) {
-            real anew = alpha - div_ref_lane<0>(d1, d2, rd2);
-            if (hi >= 0 && !(anew > lo && anew < hi)) anew = 0.5 * (lo + hi);
-            alpha = anew;
-            eval(alpha);
-            if (fabs(d1) < gtol) break;
-            if (d1 < 0) lo = alpha; else hi = alpha;
-          }
+          int iters = 0;
+          alpha = ls_iterate(ne, g1, g2, jr, jv, Di, c2, row, d1, d2c, rd2, pmask, iters);
         }
       }
       if (T.tid == 0) bc[3] = alpha;
@@ -1973,7 +2091,7 @@ __device__ inline void solver_newton(const auto& m, const auto& L, const auto& C
     TSYNC();
     iter++;
 #ifdef ILQG_STAMPS
-    if (T.tid == 0) atomicAdd(&g_newton_iters, 1ull);
+    CNT_ADD(8, 1ull);
 #endif
     STAMP(17);
     real oldcost = cost;
@@ -2109,6 +2227,9 @@ __device__ inline void newton_warm_prep(const auto& m, const auto& L, const auto
 // concurrently; exactly one __syncthreads (after the smooth start's cost)
 __device__ inline void fwd_constraint_fast(const auto& m, const auto& L, const auto& C, const auto& X,
                                            const Team& T, int maxiter, real tol, bool dual = false) {
+#ifdef ILQG_STAMPS
+  const unsigned long long tnt_ = __builtin_amdgcn_s_memtime();
+#endif
   const int nv = m.nv, ne = T.iw[L.nefc];
   const real scale = 1 / (m.stat_meaninertia * (nv > 1 ? nv : 1));
   real* s = T.w + L.s_newton;
@@ -2183,7 +2304,7 @@ __device__ inline void fwd_constraint_fast(const auto& m, const auto& L, const a
   hmask = mask;
   int iter = 0;
 #ifdef ILQG_STAMPS
-  if (T.tid == 0) atomicAdd(&g_newton_calls, 1ull);
+  CNT_ADD(9, 1ull);
 #endif
   while (iter < maxiter) {
     chol_solve_rows(nv, T.tid, H, grad, search);
@@ -2197,7 +2318,7 @@ __device__ inline void fwd_constraint_fast(const auto& m, const auto& L, const a
     {
       real snorm = sqrt(tdot(search, search, nv));
       if (!(snorm < MINVAL)) {
-        real g1 = 0, g2 = 0, d1, d2, lo = 0, hi = -1;
+        real g1 = 0, g2 = 0, d1, d2;
         for (int j = 0; j < nv; j++) g1 += search[j] * (Ma[j] - qfs[j]);
         for (int j = 0; j < nv; j++) g2 += search[j] * Mv[j];
         // active rows only (the others add -0.0); d2 depends on the active set
@@ -2222,34 +2343,18 @@ __device__ inline void fwd_constraint_fast(const auto& m, const auto& L, const a
         };
         eval(0.0);
         if (!(d1 >= 0)) {
-          real gtol = LS_TOL * fabs(d1);
+          int iters = 0;
 #ifdef ILQG_STAMPS
-          int it_ = 0, chg_ = 0, act_ = 0;
+          const unsigned long long tls_ = __builtin_amdgcn_s_memtime();
 #endif
-          for (int it = 0; it < LS_ITER; it++) {
-            real anew = alpha - div_ref_lane<0>(d1, d2, rd2);
-            if (hi >= 0 && !(anew > lo && anew < hi)) anew = 0.5 * (lo + hi);
-            alpha = anew;
+          alpha = ls_iterate(ne, g1, g2, jr, jv, Di, c2, row, d1, d2c, rd2, pmask, iters);
 #ifdef ILQG_STAMPS
-            const unsigned long long pm_ = pmask;
-#endif
-            eval(alpha);
-#ifdef ILQG_STAMPS
-            it_ = it + 1;
-            chg_ += pm_ != pmask;
-            act_ += __popcll(pmask);
-#endif
-            if (fabs(d1) < gtol) break;
-            if (d1 < 0) lo = alpha; else hi = alpha;
-          }
-#ifdef ILQG_STAMPS
-          if (T.tid == 0) {
-            atomicAdd(&g_ls[0], 1ull);
-            atomicAdd(&g_ls[1], (unsigned long long)it_);
-            atomicAdd(&g_ls[2], (unsigned long long)(it_ == LS_ITER));
-            atomicAdd(&g_ls[3], (unsigned long long)act_);
-            atomicAdd(&g_ls[4], (unsigned long long)chg_);
-          }
+          CNT_ADD(5, __builtin_amdgcn_s_memtime() - tls_);
+          CNT_ADD(0, 1ull);
+          CNT_ADD(1, (unsigned long long)iters);
+          CNT_ADD(2, (unsigned long long)(iters == LS_ITER));
+          CNT_ADD(3, (unsigned long long)ne);
+          CNT_ADD(4, (unsigned long long)(ne <= LS_NE));
 #endif
         }
       }
@@ -2264,7 +2369,7 @@ __device__ inline void fwd_constraint_fast(const auto& m, const auto& L, const a
     TSYNC();
     iter++;
 #ifdef ILQG_STAMPS
-    if (T.tid == 0) atomicAdd(&g_newton_iters, 1ull);
+    CNT_ADD(8, 1ull);
 #endif
     STAMP(17);
     const real oldcost = cost;
@@ -2285,6 +2390,9 @@ __device__ inline void fwd_constraint_fast(const auto& m, const auto& L, const a
   if (row) jar[r] = jr;
   FOR_T(i, nv) warm[i] = qacc[i];
   TSYNC();
+#ifdef ILQG_STAMPS
+  CNT_ADD(6, __builtin_amdgcn_s_memtime() - tnt_);
+#endif
 }
 
 __device__ inline void fwd_constraint(const auto& m, const auto& L, const auto& C, const auto& X, const Team& T,

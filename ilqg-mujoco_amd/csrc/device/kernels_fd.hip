@@ -200,6 +200,9 @@ __device__ inline void fd_decode(const FdFused& a, unsigned ntm, unsigned u, int
 __device__ inline void fd_fused_body(const auto& m, const auto& L, const auto& C, const auto& X, const Team& T,
                                      const FdFused& a, unsigned u) {
   STAMP_INIT();
+#ifdef ILQG_STAMPS
+  const unsigned long long tteam_ = __builtin_amdgcn_s_memtime();
+#endif
   const int nv = m.nv, nu = m.nu, nq = m.nq;
   const int nctrl = nu < nv ? nu : nv;  // mjderivative.cpp:78-82 (assumes nv >= nu)
   int role, s, p, idx;
@@ -320,6 +323,7 @@ __device__ inline void fd_fused_body(const auto& m, const auto& L, const auto& C
   if (tid == 0) signal_add(done);
 #ifdef ILQG_STAMPS
   if (tid == 0) atomicMax(&g_fused_diag[4], __builtin_amdgcn_s_memtime());
+  if (tid == 0) coop::s_cnt[7] += __builtin_amdgcn_s_memtime() - tteam_;
 #endif
   STAMP_FLUSH();
 }
@@ -487,9 +491,9 @@ extern "C" int ilqg_debug_fused(unsigned long long* d, int reset) {
 #ifdef ILQG_STAMPS
 // the FD kernels' line-search counters (dcoop_impl.h g_ls)
 extern "C" int ilqg_debug_ls_fd(unsigned long long* out5, int reset) {
-  if (hipMemcpyFromSymbol(out5, HIP_SYMBOL(ilqg::coop::g_ls), sizeof(unsigned long long) * 5) != hipSuccess) return 3;
+  if (hipMemcpyFromSymbol(out5, HIP_SYMBOL(ilqg::coop::g_ls), sizeof(unsigned long long) * 8) != hipSuccess) return 3;
   if (reset) {
-    unsigned long long z[5] = {0};
+    unsigned long long z[8] = {0};
     (void)hipMemcpyToSymbol(HIP_SYMBOL(ilqg::coop::g_ls), z, sizeof(z));
   }
   return 0;

@@ -1,5 +1,14 @@
 // Cooperative rollout kernels (inc/ilqr.h:116-130): one workgroup per
 // (seed, alpha) candidate; two-wave teams (step_dual) by default.
+//
+// The rollout's Newton solves use the model's tolerance, and their line
+// searches take ~1.4 iterations: the uniform-row line search (dcoop_impl.h
+// ls_iterate_rows, for the FD sweep's tolerance-0 solves) does not pay here,
+// and its code grew the hopper rollout kernel from 240 to 299 KB, slowing
+// every stage (instruction cache): this translation unit keeps the lane form.
+#ifndef ILQG_LS_NE
+#define ILQG_LS_NE 0
+#endif
 #include "coop_common.h"
 
 namespace ilqg {
@@ -451,9 +460,9 @@ hipError_t launch_forward_coop(const DevModel& m, const WsLayout& L, const CoopL
 #ifdef ILQG_STAMPS
 // the rollout kernels' line-search counters (dcoop_impl.h g_ls)
 extern "C" int ilqg_debug_ls_rollout(unsigned long long* out5, int reset) {
-  if (hipMemcpyFromSymbol(out5, HIP_SYMBOL(ilqg::coop::g_ls), sizeof(unsigned long long) * 5) != hipSuccess) return 3;
+  if (hipMemcpyFromSymbol(out5, HIP_SYMBOL(ilqg::coop::g_ls), sizeof(unsigned long long) * 8) != hipSuccess) return 3;
   if (reset) {
-    unsigned long long z[5] = {0};
+    unsigned long long z[8] = {0};
     (void)hipMemcpyToSymbol(HIP_SYMBOL(ilqg::coop::g_ls), z, sizeof(z));
   }
   return 0;

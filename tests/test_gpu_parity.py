@@ -502,6 +502,55 @@ def test_bench_workload_bitexact(ia, ora):
     assert picked != {0}, "the workload must exercise a non-alpha=1 selection"
 
 
+def test_cfg4_all_shards_one_gpu(ia, ora):
+    """BASELINE.json configs[3]: all 64 cfg-4 seeds (the shares of ranks 0..7,
+    seed_offset = 8 r) on one GPU as one S = 64 solver, two line-search
+    iterations (8 alphas, min-cost).  One seed of every shard (seed 9 r) is
+    compared bit for bit with the oracle's line-search iLQR; all 64 are finite
+    and the whole run is deterministic (a second solver gives the same bits).
+    Each rank's own solver (seed_offset = 8 r) starts from these same states
+    (workloads.hopper_dmain), so this covers every rank's inputs."""
+    import workloads
+    m, om = setup(ia, ora, "hopper", ia.HOPPER_COST)
+    om.lib.L.ora_set_nthread(1)
+    S, H, iters = 64, 500, 2
+    alphas = workloads.LINESEARCH_ALPHAS
+    dmain = workloads.hopper_dmain(m, S, sigma=0.01)
+    for r in range(8):  # the shard of rank r is exactly hopper_dmain(..., seed_offset=8r)
+        shard = workloads.hopper_dmain(m, 8, sigma=0.01, seed_offset=8 * r)
+        assert np.array_equal(shard.qpos, dmain.qpos[8 * r:8 * r + 8])
+        assert np.array_equal(shard.qvel, dmain.qvel[8 * r:8 * r + 8])
+    runs = []
+    for _ in range(2):
+        g = ia.ILQR(m, dmain, H, ia.HOPPER_COST, alphas=alphas, select="min_cost")
+        for _ in range(iters):
+            g.iterate()
+        g.synchronize()
+        runs.append((g.traj(), g.gains(), g.costs()))
+        del g
+    (t1, (K1, k1), (c1, s1)), (t2, (K2, k2), (c2, s2)) = runs
+    for a, b, nm in ((t1.qpos, t2.qpos, "qpos"), (t1.qvel, t2.qvel, "qvel"), (t1.ctrl, t2.ctrl, "ctrl"),
+                     (K1, K2, "K"), (k1, k2, "k"), (c1, c2, "costs"), (s1, s2, "selection")):
+        exact(a, b, f"determinism {nm}")
+        assert np.all(np.isfinite(a)), nm
+    P = H + 1
+    for r in range(8):
+        s = 9 * r  # rank r's local seed r
+        d = om.make_data()
+        d.set_state(**_state_dict(dmain, s))
+        il = ora.OILQR(om, d, H, cost_fn="ora_cost_desc_fn")
+        il.set_dinit(d)
+        for _ in range(iters):
+            oc, osel = il.iterate_ls(alphas, "min_cost")
+        ot, oa = il.traj(), il.arrays()
+        for f in ("qpos", "qvel", "warm", "ctrl"):
+            exact(getattr(t1, f)[s * P:(s + 1) * P].reshape(ot[f].shape), ot[f], f"seed {s} traj.{f}")
+        exact(K1[s], oa["K"], f"seed {s} K")
+        exact(k1[s], oa["k"], f"seed {s} k")
+        exact(c1[s], oc, f"seed {s} candidate costs")
+        assert int(s1[s]) == osel
+
+
 def test_fault_word_reported_once_then_cleared(ia, ora):
     """A tripped hand-off (preset fault word) is reported by synchronize()
     exactly once; the next iterate() runs every wait again and is bit-exact."""

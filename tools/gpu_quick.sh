@@ -11,4 +11,5 @@ timeout -k 10 600 python bench.py --no-cpu-baseline --steps ${STEPS:-10} > $OUT/
 python3 -c "import json; d=json.load(open('$OUT/bench.json')); print('value', round(d['value'],1), {k: round(v['avg_ms'],2) for k,v in d['kernels'].items()})"
 if [[ -n "$STAMPS" ]]; then
   timeout -k 10 300 env ILQG_LIB=ilqg-mujoco_amd/lib/libilqg_amd_diag.so python3 tools/stamps.py > $OUT/stamps.log 2>&1 || { echo "stamps failed"; tail -20 $OUT/stamps.log; exit 1; }
+  timeout -k 10 300 env ILQG_LIB=ilqg-mujoco_amd/lib/libilqg_amd_diag.so python3 tools/fused_diag.py 8 4 > $OUT/fused_diag.log 2>&1 || { echo "fused_diag failed"; tail -20 $OUT/fused_diag.log; exit 1; }
 fi

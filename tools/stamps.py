@@ -28,7 +28,7 @@ else:
     g = ia.ILQR(m, dmain, 500 if m.nv == 6 else 200, ia.HOPPER_COST if m.nv == 6 else ia.PENDULUM_COST)
 g.iterate(); g.synchronize()
 g.set_timing(True)
-ls = (ctypes.c_ulonglong * 5)()
+ls = (ctypes.c_ulonglong * 8)()
 for what, fn, rd, rls in (("rollout (1 seed)", g.forward_pass, L.ilqg_debug_stamps, L.ilqg_debug_ls_rollout),
                           ("fd sweep", g.fd_sweep, L.ilqg_debug_stamps_fd, L.ilqg_debug_ls_fd)):
     rd(acc, cnt, 1)
@@ -40,8 +40,11 @@ for what, fn, rd, rls in (("rollout (1 seed)", g.forward_pass, L.ilqg_debug_stam
     rls(ls, 1)
     if ls[0]:
         print(f"   line searches (all workgroups): {ls[0]} calls, {ls[1] / ls[0]:.2f} iterations per call, "
-              f"{ls[2]} ran to LS_ITER, {ls[3] / max(ls[1], 1):.2f} active rows per evaluation, "
-              f"active set changed in {ls[4] / max(ls[1], 1):.1%} of evaluations")
+              f"{ls[2]} ran to LS_ITER, {ls[3] / ls[0]:.2f} constraint rows per call, "
+              f"{ls[4] / ls[0]:.1%} on the uniform-row form")
+    if ls[7]:
+        print(f"   all FD teams: {ls[7] / 2.4e3:.0f} team-us in total; Newton solves {ls[6] / ls[7]:.1%} of it, "
+              f"line searches {ls[5] / ls[7]:.1%}")
     # wave 0's stamps partition its time: top-level stages, their sub-stages
     # (11-23: kinematics and Newton pieces, which restart the stage clock) and
     # the barrier waits
