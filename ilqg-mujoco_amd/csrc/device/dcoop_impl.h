@@ -88,6 +88,9 @@ __shared__ unsigned long long s_stamp_acc[STAMP_N], s_stamp_cnt[STAMP_N], s_stam
     }                                                                        \
   } while (0)
 #else
+#define CNT_ADD(i, v) \
+  do {                \
+  } while (0)
 #define STAMP(id) \
   do {            \
   } while (0)
@@ -2223,10 +2226,318 @@ __device__ inline void newton_warm_prep(const auto& m, const auto& L, const auto
   TSYNC();
 }
 
+// ---- Newton solver in wave-uniform registers (compile-time nv <= RMAX) ----
+// The primal Newton solver of oracle/mjsub.c (fwd_constraint + solver_newton)
+// with every nv-vector (qacc, M qacc, gradient, search direction, M search,
+// J' force) and the Hessian's Cholesky factor held IN REGISTERS ON EVERY LANE
+// (each lane computes the same values), while constraint row r keeps its
+// jacobian row, D and residual on lane r.  The serial recursions (the
+// factorization, both substitutions, the cost and gradient sums) then run as
+// straight-line VALU code on values already in registers: no LDS round trip,
+// no wave barrier and no cross-lane broadcast on their chains.  The row-parallel
+// products (M search, J search, the Hessian entries) run one output per lane
+// and are gathered once.  Every scalar is the oracle's expression with the
+// oracle's summation order, so the results are bit-identical to the lane-
+// parallel form (fwd_constraint_fast below) it replaces for these models.
+
+// v[j] = p[j] on every lane (uniform LDS reads)
+template <int N>
+__device__ __forceinline__ void ldu(real (&v)[N], const real* p) {
+  sfor<0, N>(SLAM(jj) { v[SK(jj)] = p[SK(jj)]; });
+}
+// s = 0 + a[0] b[0] + a[1] b[1] + ... (the oracle's dotn)
+template <int N>
+__device__ __forceinline__ real dotu(const real (&a)[N], const real (&b)[N]) {
+  real r = 0;
+  sfor<0, N>(SLAM(jj) { r += a[SK(jj)] * b[SK(jj)]; });
+  return r;
+}
+// a wave-uniform value (a readlane result, held in SGPRs) moved to a VGPR:
+// the solver keeps dozens of uniform values live, and left in SGPRs they
+// overflow the scalar file (spilled to VGPR lanes, each reload a v_readlane
+// on the chain)
+__device__ __forceinline__ real vreg(real x) {
+  asm("" : "+v"(x));
+  return x;
+}
+// out[j] = value of x on lane j (x: one entry per lane)
+template <int N>
+__device__ __forceinline__ void gatheru(real (&out)[N], real x) {
+  sfor<0, N>(SLAM(jj) { out[SK(jj)] = vreg(bcast(x, SK(jj))); });
+}
+// out[j] = 0 + p[j](lane i0) + p[j](lane i1) + ... over the set lanes of mask,
+// ascending (uniform mask): N ordered sums sharing one walk of the mask
+template <int N>
+__device__ __forceinline__ void lane_sums_mask(real (&out)[N], const real (&p)[N], unsigned long long mask) {
+  sfor<0, N>(SLAM(jj) { out[SK(jj)] = 0; });
+  for (unsigned long long mm = mask; mm; mm &= mm - 1) {
+    const int i = __builtin_ctzll(mm);
+    sfor<0, N>(SLAM(jj) { out[SK(jj)] += bcast(p[SK(jj)], i); });
+  }
+}
+// a / b, uniform operands, divisor reciprocal r = rcp_ref(b) (dsmall.h)
+__device__ __forceinline__ real divu(real a, real b, real r) { return div_ref_lane<0>(a, b, r); }
+
+// H = M + J' diag(D * active) J (oracle hessian_factor), entries one per lane
+// (lane e = r NV + c, c <= r; J and D read from LDS), gathered, then the
+// dense Cholesky in registers; rd[j] = rcp_ref of the factor's diagonal
+template <int NV>
+__device__ inline void hessian_factor_u(const real* qM, const real* J, const real* D, unsigned long long amask,
+                                        int tid, real (&Hf)[NV][NV], real (&rd)[NV]) {
+  const int r = tid / NV, c = tid % NV;
+  real h = 0;
+  if (tid < NV * NV && c <= r) {
+    for (unsigned long long mm = amask; mm; mm &= mm - 1) {
+      const int i = __builtin_ctzll(mm);
+      h += J[i * NV + r] * D[i] * J[i * NV + c];
+    }
+    h = qM[tid] + h;
+  }
+  sfor<0, NV>(SLAM(rr) {
+    sfor<0, SK(rr) + 1>(SLAM(cc) { Hf[SK(rr)][SK(cc)] = vreg(bcast(h, SK(rr) * NV + SK(cc))); });
+  });
+  sfor<0, NV>(SLAM(jc) {
+    constexpr int j = SK(jc);
+    real t = Hf[j][j];
+    if constexpr (j > 0) {
+      real q = 0;
+      sfor<0, j>(SLAM(qq) { q += Hf[j][SK(qq)] * Hf[j][SK(qq)]; });
+      t -= q;
+    }
+    if (t < MINVAL) t = MINVAL;
+    Hf[j][j] = sqrt(t);
+    const real ti = 1 / Hf[j][j];
+    sfor<j + 1, NV>(SLAM(ii) {
+      constexpr int i = SK(ii);
+      real q = 0;
+      sfor<0, j>(SLAM(qq) { q += Hf[i][SK(qq)] * Hf[j][SK(qq)]; });
+      Hf[i][j] = (Hf[i][j] - q) * ti;
+    });
+  });
+  sfor<0, NV>(SLAM(jj) { rd[SK(jj)] = rcp_ref(Hf[SK(jj)][SK(jj)]); });
+}
+// the factor computed elsewhere (newton_warm_prep's LDS H, row-major nv x nv)
+template <int NV>
+__device__ inline void factor_load_u(const real* H, real (&Hf)[NV][NV], real (&rd)[NV]) {
+  sfor<0, NV>(SLAM(rr) {
+    sfor<0, SK(rr) + 1>(SLAM(cc) { Hf[SK(rr)][SK(cc)] = H[SK(rr) * NV + SK(cc)]; });
+  });
+  sfor<0, NV>(SLAM(jj) { rd[SK(jj)] = rcp_ref(Hf[SK(jj)][SK(jj)]); });
+}
+// search = -(L L')^-1 g (oracle chol_solve and the sign flip)
+template <int NV>
+__device__ inline void chol_solve_u(const real (&Hf)[NV][NV], const real (&rd)[NV], const real (&g)[NV],
+                                    real (&sv)[NV]) {
+  real x[NV], acc[NV];
+  sfor<0, NV>(SLAM(ii) { acc[SK(ii)] = 0; });
+  // forward: x[i] = (g[i] - dotn(L_i, x, i)) / L_ii, the dot products grown as
+  // the x[j] are final (ascending j from +0: dotn's order)
+  sfor<0, NV>(SLAM(ii) {
+    constexpr int i = SK(ii);
+    real t = g[i];
+    if constexpr (i > 0) t -= acc[i];
+    x[i] = divu(t, Hf[i][i], rd[i]);
+    sfor<i + 1, NV>(SLAM(kk) { acc[SK(kk)] += Hf[SK(kk)][i] * x[i]; });
+  });
+  // backward: x[i] -= L[j][i] x[j] for j = i+1.. ascending, then / L_ii
+  sfor<0, NV>(SLAM(ii) {
+    constexpr int i = NV - 1 - SK(ii);
+    real t = x[i];
+    sfor<i + 1, NV>(SLAM(jj) { t -= Hf[SK(jj)][i] * x[SK(jj)]; });
+    x[i] = divu(t, Hf[i][i], rd[i]);
+  });
+  sfor<0, NV>(SLAM(jj) { sv[SK(jj)] = -x[SK(jj)]; });
+}
+// 0.5 sum_j (Ma_j - qfs_j)(qacc_j - qas_j) (oracle gauss_cost)
+template <int N>
+__device__ __forceinline__ real gauss_uu(const real (&Ma)[N], const real (&qfs)[N], const real (&qa)[N],
+                                         const real (&qas)[N]) {
+  real g = 0;
+  sfor<0, N>(SLAM(jj) { g += (Ma[SK(jj)] - qfs[SK(jj)]) * (qa[SK(jj)] - qas[SK(jj)]); });
+  return 0.5 * g;
+}
+
+// the exact line search (oracle linesearch) from lane-row terms: eval(0) in
+// the lane form, then ls_iterate; returns alpha (uniform)
+__device__ inline real linesearch_rows(int ne, real g1, real g2, real jr, real jv, real Di, bool row, const Team& T) {
+  const real c2 = Di * jv * jv;
+  const real x0 = jr + 0.0 * jv;  // the oracle's LS_EVAL(0.0)
+  const real c10 = Di * x0 * jv;
+  const unsigned long long am = __ballot(row && x0 < 0);
+  const real d1 = lane_sum_mask(g1 + g2 * 0.0, c10, am);
+  if (d1 >= 0) return 0;
+  const real d2c = lane_sum_mask(g2, c2, am);
+  const real rd2 = rcp_ref(d2c);
+  int iters = 0;
+#ifdef ILQG_STAMPS
+  const unsigned long long tls_ = __builtin_amdgcn_s_memtime();
+#endif
+  const real alpha = ls_iterate(ne, g1, g2, jr, jv, Di, c2, row, d1, d2c, rd2, am, iters);
+#ifdef ILQG_STAMPS
+  CNT_ADD(5, __builtin_amdgcn_s_memtime() - tls_);
+  CNT_ADD(0, 1ull);
+  CNT_ADD(1, (unsigned long long)iters);
+  CNT_ADD(2, (unsigned long long)(iters == LS_ITER));
+  CNT_ADD(3, (unsigned long long)ne);
+  CNT_ADD(4, (unsigned long long)(ne <= LS_NE));
+#endif
+  (void)T;
+  return alpha;
+}
+
+// fwd_constraint + solver_newton for a compile-time nv <= RMAX and nefc <= 64
+// (dual: the rollout's primary wave, whose helper ran newton_warm_prep)
+template <int NV>
+__device__ inline void fwd_constraint_u(const auto& m, const auto& L, const auto& C, const Team& T, int maxiter,
+                                        real tol, bool dual) {
+#ifdef ILQG_STAMPS
+  const unsigned long long tnt_ = __builtin_amdgcn_s_memtime();
+#endif
+  const int ne = T.iw[L.nefc];
+  const real scale = 1 / (m.stat_meaninertia * (NV > 1 ? NV : 1));
+  real* sn = T.w + L.s_newton;
+  real* jar_l = sn + 4 * NV + NV * NV;
+  const real* qM = T.w + L.qM;
+  const real* J = T.w + L.efc_J;
+  const int r = T.tid;
+  const bool row = r < ne;
+  const real Di = row ? T.w[L.efc_D + r] : 0.0;
+  const real aref = row ? T.w[L.efc_aref + r] : 0.0;
+  real Jr[NV], Mr[NV];  // lane r: jacobian row r; lane i < NV: row i of M
+  sfor<0, NV>(SLAM(jj) {
+    constexpr int j = SK(jj);
+    Jr[j] = row ? J[r * NV + j] : 0.0;
+    Mr[j] = r < NV ? qM[r * NV + j] : 0.0;
+  });
+  real qas[NV], qfs[NV], warm[NV];
+  ldu(qas, T.w + L.qacc_smooth);
+  ldu(qfs, T.w + L.qfrc_smooth);
+  ldu(warm, T.w + L.warm);
+  // warm-start selection (oracle fwd_constraint)
+  const real jb = row ? dotu(Jr, qas) - aref : 0.0;
+  const bool acts = row && jb < 0;
+  const unsigned long long ms = __ballot(acts);
+  const real cost_smooth = lane_sum_mask(0.0, acts ? 0.5 * Di * jb * jb : -0.0, ms);
+  real jw, cost_warm, Ma[NV];
+  unsigned long long mw;
+  if (dual) {
+    __syncthreads();  // the helper's newton_warm_prep is in LDS
+    jw = row ? jar_l[r] : 0.0;
+    mw = (unsigned long long)__double_as_longlong((double)T.c[C.bc + 5]);
+    ldu(Ma, sn);
+    cost_warm = gauss_uu(Ma, qfs, warm, qas) + T.c[C.bc + 4];
+  } else {
+    jw = row ? dotu(Jr, warm) - aref : 0.0;
+    gatheru(Ma, dotu(Mr, warm));
+    const bool actw = row && jw < 0;
+    mw = __ballot(actw);
+    cost_warm = gauss_uu(Ma, qfs, warm, qas) + lane_sum_mask(0.0, actw ? 0.5 * Di * jw * jw : -0.0, mw);
+  }
+  const bool use_smooth = __ballot(cost_warm > cost_smooth) != 0;  // uniform
+  // solver start (oracle solver_newton)
+  real qacc[NV], qc[NV], grad[NV], Hf[NV][NV], rd[NV];
+  real jr, cost;
+  unsigned long long mask;
+  sfor<0, NV>(SLAM(jj) { qacc[SK(jj)] = use_smooth ? qas[SK(jj)] : warm[SK(jj)]; });
+  if (use_smooth) {
+    jr = jb;
+    gatheru(Ma, dotu(Mr, qas));
+    mask = ms;
+    cost = gauss_uu(Ma, qfs, qacc, qas) + cost_smooth;
+  } else {
+    jr = jw;
+    mask = mw;
+    cost = cost_warm;
+  }
+  if (!use_smooth && dual) {
+    // forces, J' force and the factor of the warm start's active set: the helper's
+    ldu(qc, T.w + L.qfrc_con);
+    factor_load_u<NV>(sn + 4 * NV, Hf, rd);
+  } else {
+    real p[NV];
+    const real f = (row && jr < 0) ? -Di * jr : 0.0;
+    sfor<0, NV>(SLAM(jj) { p[SK(jj)] = Jr[SK(jj)] * f; });
+    lane_sums_mask(qc, p, mask);
+    hessian_factor_u<NV>(qM, J, T.w + L.efc_D, mask, r, Hf, rd);
+  }
+  sfor<0, NV>(SLAM(jj) { grad[SK(jj)] = (Ma[SK(jj)] - qfs[SK(jj)]) - qc[SK(jj)]; });
+  unsigned long long hmask = mask;
+  int iter = 0;
+  CNT_ADD(9, 1ull);
+  STAMP(10);
+  while (iter < maxiter) {
+    real sv[NV], Mv[NV];
+    chol_solve_u<NV>(Hf, rd, grad, sv);
+    STAMP(14);
+    gatheru(Mv, dotu(Mr, sv));
+    const real jv = row ? dotu(Jr, sv) : 0.0;
+    STAMP(15);
+    real alpha = 0;
+    if (!(sqrt(dotu(sv, sv)) < MINVAL)) {
+      real g1 = 0, g2 = 0;
+      sfor<0, NV>(SLAM(jj) { g1 += sv[SK(jj)] * (Ma[SK(jj)] - qfs[SK(jj)]); });
+      sfor<0, NV>(SLAM(jj) { g2 += sv[SK(jj)] * Mv[SK(jj)]; });
+      alpha = linesearch_rows(ne, g1, g2, jr, jv, Di, row, T);
+    }
+    STAMP(16);
+    if (__ballot(alpha == 0) != 0) break;  // uniform
+    sfor<0, NV>(SLAM(jj) {
+      qacc[SK(jj)] += alpha * sv[SK(jj)];
+      Ma[SK(jj)] += alpha * Mv[SK(jj)];
+    });
+    jr += alpha * jv;
+    iter++;
+    CNT_ADD(8, 1ull);
+    STAMP(17);
+    const real oldcost = cost;
+    const bool act = row && jr < 0;
+    mask = __ballot(act);
+    cost = gauss_uu(Ma, qfs, qacc, qas) + lane_sum_mask(0.0, act ? 0.5 * Di * jr * jr : -0.0, mask);
+    {
+      real p[NV];
+      const real f = act ? -Di * jr : 0.0;
+      sfor<0, NV>(SLAM(jj) { p[SK(jj)] = Jr[SK(jj)] * f; });
+      lane_sums_mask(qc, p, mask);
+    }
+    sfor<0, NV>(SLAM(jj) { grad[SK(jj)] = (Ma[SK(jj)] - qfs[SK(jj)]) - qc[SK(jj)]; });
+    const real improvement = scale * (oldcost - cost);
+    const real gradient = scale * sqrt(dotu(grad, grad));
+    STAMP(18);
+    if (__ballot(improvement < tol || gradient < tol) != 0) break;
+    // the factor is a function of (qM, J, D, active set) alone: rebuilt only
+    // when the active set changed since it was computed (the same bits)
+    if (mask != hmask) {
+      hessian_factor_u<NV>(qM, J, T.w + L.efc_D, mask, r, Hf, rd);
+      hmask = mask;
+    }
+    STAMP(19);
+  }
+  if (row) jar_l[r] = jr;
+  real* qa_l = T.w + L.qacc;
+  real* wm_l = T.w + L.warm;
+  sfor<0, NV>(SLAM(jj) {
+    if (r == SK(jj)) {
+      qa_l[SK(jj)] = qacc[SK(jj)];
+      wm_l[SK(jj)] = qacc[SK(jj)];
+    }
+  });
+  TSYNC();
+#ifdef ILQG_STAMPS
+  CNT_ADD(6, __builtin_amdgcn_s_memtime() - tnt_);
+#endif
+}
+
 // dual: the primary wave of a two-wave team whose helper runs newton_warm_prep
 // concurrently; exactly one __syncthreads (after the smooth start's cost)
 __device__ inline void fwd_constraint_fast(const auto& m, const auto& L, const auto& C, const auto& X,
                                            const Team& T, int maxiter, real tol, bool dual = false) {
+  using MT = std::remove_cvref_t<decltype(m)>;
+  if constexpr (StaticModel<MT>) {
+    if constexpr (MT::nv <= RMAX) {
+      fwd_constraint_u<MT::nv>(m, L, C, T, maxiter, tol, dual);
+      return;
+    }
+  }
 #ifdef ILQG_STAMPS
   const unsigned long long tnt_ = __builtin_amdgcn_s_memtime();
 #endif

@@ -5,7 +5,7 @@ import numpy as np
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "ilqg-mujoco_amd"))
 import ilqg_amd as ia, workloads
-NAMES = {0: "kinematics", 1: "com_pos", 2: "trn+crb", 3: "factor_ld(M)", 4: "collision", 5: "make_constraint",
+NAMES = {10: " nt: start (warm/smooth choice, factor)", 0: "kinematics", 1: "com_pos", 2: "trn+crb", 3: "factor_ld(M)", 4: "collision", 5: "make_constraint",
          6: "fwd_velocity", 7: "fwd_acceleration", 8: "fwd_constraint(newton)", 9: "integrator",
          11: " kin: joint quats", 12: " kin: lane-0 chain / position chain", 13: " kin: body frames", 14: " nt: chol solve",
          15: " nt: Mv,Jv", 16: " nt: linesearch", 17: " nt: update", 18: " nt: cost+grad", 19: " nt: hessian",
@@ -48,7 +48,7 @@ for what, fn, rd, rls in (("rollout (1 seed)", g.forward_pass, L.ilqg_debug_stam
     # wave 0's stamps partition its time: top-level stages, their sub-stages
     # (11-23: kinematics and Newton pieces, which restart the stage clock) and
     # the barrier waits
-    tot = sum(acc[i] for i in list(range(10)) + list(range(11, 24)) + list(range(24, 30)))
+    tot = sum(acc[i] for i in list(range(11)) + list(range(11, 24)) + list(range(24, 30)))
     ms = sum(v[0] for v in tm.values())
     print(f"== {what}: block 0, lane 0, total {tot} ticks (wave-0 stages + barriers); kernel time {ms:.3f} ms "
           f"-> {tot / (ms * 1e3):.0f} ticks/us if the stages were all of it")
