@@ -62,7 +62,7 @@ def algorithmic_bytes(m, S, A, P):
     return {"fd_sweep": S * fd, "backward": S * bw, "rollout": S * A * fw, "fd_backward": S * (fd + bw)}
 
 
-def cpu_baseline(budget_s, horizon, threads, nalpha):
+def cpu_baseline(budget_s, horizon, threads, nalpha, model="hopper", cost=None):
     """The CPU side of the comparison, timed on this host (rank 0, N=1 only;
     oracle/cpu_bench.py, test infrastructure run as child processes):
       value   the reference-faithful iterate() (restated src/mjderivative.cpp
@@ -73,14 +73,16 @@ def cpu_baseline(budget_s, horizon, threads, nalpha):
       tuned   like-for-like throughput: `threads` single-threaded processes,
               one per pinned core, each iterating its own seed of the bench
               workload (8 alphas, min-cost selection) -> seed-iterations/s."""
-    m = ia.Model.load(workloads.model_file("hopper"))
+    cost = cost or ia.HOPPER_COST
+    m = ia.Model.load(workloads.model_file(model))
     tag = f"{os.getpid()}"
-    blob_path = os.path.join("/tmp", f"ilqg_hopper_blob_{tag}.bin")
-    cost_path = os.path.join("/tmp", f"ilqg_hopper_cost_{tag}.json")
+    blob_path = os.path.join("/tmp", f"ilqg_{model}_blob_{tag}.bin")
+    cost_path = os.path.join("/tmp", f"ilqg_{model}_cost_{tag}.json")
     with open(blob_path, "wb") as f:
         f.write(m.blob())
     with open(cost_path, "w") as f:
-        json.dump({k: list(v) for k, v in ia.HOPPER_COST.packed(m.nq, m.nv, m.nu).items()}, f)
+        json.dump({k: list(v) for k, v in cost.packed(m.nq, m.nv, m.nu).items()}, f)
+    state = "cfg-3 state" if model == "hopper" else "cfg-5 state: qpos0, root z = 1.4"
     script = os.path.join(ROOT, "oracle", "cpu_bench.py")
     allc = sorted(os.sched_getaffinity(0))
     cores = allc[:threads]
@@ -123,20 +125,20 @@ def cpu_baseline(budget_s, horizon, threads, nalpha):
         "unit": "iLQR iterations/s (1 seed)",
         "cores": ref["threads"],
         "kind": ref["kind"],
-        "sample": (f"hopper H={horizon}, 1 seed (cfg-3 state), alpha=1: 1 warm-up + {ref['iters']} timed iterate() "
+        "sample": (f"{model} H={horizon}, 1 seed ({state}), alpha=1, fp64 FD: 1 warm-up + {ref['iters']} timed iterate() "
                    f"calls in {ref['secs']:.1f}s, value = 1/median; FD = "
                    + ("the reference's own src/mjderivative.cpp (oracle/_ref)" if ref["kind"] == "reference" else
                       "the restated src/mjderivative.cpp driver (oracle/ilqr_ora.c)")
                    + f" with OpenMP nthread=omp_get_num_procs()={ref['threads']}, per-call mjData; host {cpu_model},"
                    f" {len(allc)} cpus visible, pinned to {len(cores)}"),
-        "protocol_note": ("BASELINE.md's protocol (1 warm-up + 10 iterations, median of 5 runs) takes ~3 min at this "
-                          "rate; the bench contract bounds the CPU sample to ~10-30 s, so this is one run of up to 10 "
-                          "iterations within the budget"),
+        "protocol_note": (f"BASELINE.md's protocol (1 warm-up + 10 iterations, median of 5 runs) would take "
+                          f"~{55 * ref['median_s']:.0f} s at this rate; the bench contract bounds the CPU sample to "
+                          f"~10-30 s, so this is one run of up to 10 iterations within a {budget_s:.0f} s budget"),
         "tuned_throughput": {
             "value": thr, "unit": "seed-iterations/s", "cores": len(tuned),
             "per_core": per_core,
             "sample": (f"{len(tuned)} single-threaded processes, one per pinned core, each iterating its own bench "
-                       f"seed (hopper H={horizon}, {nalpha} alphas, min-cost selection): "
+                       f"seed ({model} H={horizon}, {nalpha} alphas{', min-cost selection' if nalpha > 1 else ''}, fp64 FD): "
                        f"{sum(t['iters'] for t in tuned)} iterations in ~{tb:.0f}s each"),
             # the GPU box gives one GPU a share of its host (16 CPUs); the whole
             # host is not measured, only extrapolated linearly from the share
@@ -212,6 +214,80 @@ class DrySolver:
         return {}
 
 
+CFG5_METRIC = ("iLQR iterations/sec (FD+backward+forward) for Humanoid H=200, fp32 FD + fp64 MFMA Riccati "
+               "(BASELINE.json configs[4])")
+FP32_PEAK_TFS = 157.3    # MI355X_MICROARCH.md chip table, FP32 vector
+FP64_MFMA_PEAK_TFS = 78.6  # AMD spec, FP64 matrix (v_mfma_f64_16x16x4_f64); the guide lists no FP64 row
+
+
+def run_humanoid_cfg5(args, world, rank, local_rank):
+    """BASELINE.json configs[4]: humanoid, H = 200, one seed (qpos0 with the
+    root at z = 1.4, humanoid.xml:49-50), fp32 FD (eps 1e-3) with the fp64
+    Riccati recursion on the matrix cores (ilqg_solver_set_riccati MFMA).  A
+    single seed does not shard: at N > 1 every rank runs a replica and value
+    sums them.  A separate line, not the headline."""
+    H = 200
+    m = ia.Model.load(workloads.model_file("humanoid"))
+    st = m.reset_state(1)
+    st.qpos[0, 2] = 1.4
+    g = ia.ILQR(m, st, H, ia.HUMANOID_COST, device=local_rank)
+    g.set_riccati("mfma")
+    g.set_fd_precision("f32")
+    for _ in range(args.warmup):
+        g.iterate()
+    g.synchronize()
+    if world > 1:
+        dist.barrier()
+    g.set_timing(True)
+    g.timing()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        g.iterate()
+    g.synchronize()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = max_over_ranks(time.perf_counter() - t0, world, "cuda")
+    kt = {k: {"ms_total": v[0], "launches": v[1], "avg_ms": v[0] / v[1] if v[1] else 0.0} for k, v in g.timing().items()}
+    with open(FLOPS_JSON) as f:
+        hf = json.load(f)["models"]["humanoid"]
+    P = H + 1
+    fd_ms = sum(kt[k]["avg_ms"] for k in ("fd_centre", "fd_cols") if k in kt)
+    bw_ms = kt.get("backward", {}).get("avg_ms", 0.0)
+    roll_ms = kt.get("rollout", {}).get("avg_ms", 0.0)
+    fd_tf = P * hf["fd_point"]["flops"] / (fd_ms * 1e-3) / 1e12 if fd_ms else 0.0
+    bw_tf = H * hf["riccati_step"]["flops"] / (bw_ms * 1e-3) / 1e12 if bw_ms else 0.0
+    value = world * args.steps / elapsed
+    out = {
+        "metric": CFG5_METRIC, "value": value, "unit": "iLQR iterations/s (1 seed per GPU, replicas summed)",
+        "n_gpus": world, "steps": args.steps, "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3,
+        "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+        "dtype": "f32 (FD sweep) / f64 (rollout, Riccati)",
+        "data": "synthetic (humanoid qpos0, root z = 1.4, qvel 0; state-only quadratic cost)",
+        "config": {"workload": "humanoid_H200_cfg5", "model": "humanoid.xml", "horizon": H, "seeds_per_gpu": 1,
+                   "fd_precision": "f32 (eps 1e-3)", "riccati": "fp64 MFMA (v_mfma_f64_16x16x4_f64)",
+                   "parallelism": f"replicas x{world} (a single seed does not shard)"},
+        "kernels": kt,
+        "roofline": {
+            "rollout": {"bound": "latency", "us_per_step": roll_ms / P * 1e3},
+            "fd_sweep": {"bound": "fp32-valu", "flops_per_launch": P * hf["fd_point"]["flops"],
+                         "avg_launch_ms": fd_ms, "achieved_tflops": fd_tf, "peak_tflops": FP32_PEAK_TFS,
+                         "frac": fd_tf / FP32_PEAK_TFS,
+                         "flops_source": "tests/fixtures/flops.json (instrumented oracle, fp64 op count)"},
+            "backward": {"bound": "fp64-mfma", "flops_per_launch": H * hf["riccati_step"]["flops"],
+                         "avg_launch_ms": bw_ms, "achieved_tflops": bw_tf, "peak_tflops": FP64_MFMA_PEAK_TFS,
+                         "frac": bw_tf / FP64_MFMA_PEAK_TFS, "us_per_step": bw_ms / H * 1e3}},
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        cb = cpu_baseline(args.cpu_budget, H, args.cpu_threads, 1, model="humanoid", cost=ia.HUMANOID_COST)
+        out["cpu_baseline"] = cb
+        out["speedup_vs_cpu_per_seed"] = value / cb["value"]
+        out["speedup_vs_cpu_throughput"] = value / cb["tuned_throughput"]["value"]
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -229,6 +305,8 @@ def main():
     ap.add_argument("--roll-cus", type=int, default=128)
     # host-side rehearsal of the multi-rank path on CPU (gloo, no GPU, no measurement)
     ap.add_argument("--dry-run", action="store_true")
+    # the headline (cfg 4's per-GPU share) or cfg 5 as a separate line
+    ap.add_argument("--workload", choices=("hopper_cfg4", "humanoid_cfg5"), default="hopper_cfg4")
     argv = sys.argv[1:]
     args = ap.parse_args(argv)
 
@@ -252,6 +330,11 @@ def main():
         if world > 1:
             dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
 
+    if args.workload == "humanoid_cfg5" and not args.dry_run:
+        run_humanoid_cfg5(args, world, rank, local_rank)
+        if world > 1:
+            dist.destroy_process_group()
+        return
     S, A, H = args.seeds_per_gpu, args.alphas, args.horizon
     P = H + 1
     alphas = tuple(2.0 ** -i for i in range(A))

@@ -51,10 +51,16 @@ __device__ __forceinline__ void cnt_flush() {
   do {                                    \
     if (threadIdx.x == 0) __hip_atomic_fetch_add(&s_cnt[i], (unsigned long long)(v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP); \
   } while (0)
+// the workgroups whose stamps are taken: block 0, or (ILQG_STAMP_SAMPLE = k) every
+// 2^k-th block (the FD sweeps: a sample of all team roles)
+#ifndef ILQG_STAMP_SAMPLE
+#define ILQG_STAMP_SAMPLE 0
+#endif
+#define STAMP_BLOCK() ((blockIdx.x & ((1u << ILQG_STAMP_SAMPLE) - 1u)) == 0)
 __shared__ unsigned long long s_stamp_acc[STAMP_N], s_stamp_cnt[STAMP_N], s_stamp_prev, s_stamp_prevb;
 #define STAMP_AT(lane, prev, id)                                             \
   do {                                                                       \
-    if (threadIdx.x == (lane) && blockIdx.x == 0) {                          \
+    if (threadIdx.x == (lane) && STAMP_BLOCK()) {                            \
       unsigned long long t_ = __builtin_amdgcn_s_memtime();                  \
       if ((id) >= 0) {                                                       \
         s_stamp_acc[(id) < 0 ? 0 : (id)] += t_ - prev;                       \
@@ -70,7 +76,7 @@ __shared__ unsigned long long s_stamp_acc[STAMP_N], s_stamp_cnt[STAMP_N], s_stam
   do {                                                                       \
     if (threadIdx.x == 0) {                                                  \
       for (int i_ = 0; i_ < 10; i_++) s_cnt[i_] = 0;                         \
-      if (blockIdx.x == 0) {                                                 \
+      if (STAMP_BLOCK()) {                                                   \
         for (int i_ = 0; i_ < STAMP_N; i_++) s_stamp_acc[i_] = s_stamp_cnt[i_] = 0; \
         s_stamp_prev = s_stamp_prevb = __builtin_amdgcn_s_memtime();         \
       }                                                                      \
@@ -80,11 +86,12 @@ __shared__ unsigned long long s_stamp_acc[STAMP_N], s_stamp_cnt[STAMP_N], s_stam
   do {                                                                       \
     if (threadIdx.x == 0) {                                                  \
       cnt_flush();                                                           \
-      if (blockIdx.x == 0)                                                   \
-        for (int i_ = 0; i_ < STAMP_N; i_++) {                               \
-          g_stamp_acc[i_] += s_stamp_acc[i_];                                \
-          g_stamp_cnt[i_] += s_stamp_cnt[i_];                                \
-        }                                                                    \
+      if (STAMP_BLOCK())                                                     \
+        for (int i_ = 0; i_ < STAMP_N; i_++)                                 \
+          if (s_stamp_cnt[i_]) {                                             \
+            cnt_add_g(&g_stamp_acc[i_], s_stamp_acc[i_]);                    \
+            cnt_add_g(&g_stamp_cnt[i_], s_stamp_cnt[i_]);                    \
+          }                                                                  \
     }                                                                        \
   } while (0)
 #else
@@ -2324,29 +2331,60 @@ __device__ inline void factor_load_u(const real* H, real (&Hf)[NV][NV], real (&r
   });
   sfor<0, NV>(SLAM(jj) { rd[SK(jj)] = rcp_ref(Hf[SK(jj)][SK(jj)]); });
 }
+// a / b with b's refined reciprocal r (dsmall.h div_tail) and the fallback
+// deferred: `bad` collects the lanes where the divisor would have been scaled
+// (the caller redoes the whole computation with IEEE division then), so no
+// branch sits on the dependency chain
+__device__ __forceinline__ double div_defer(double a, double b, double r, bool& bad) {
+  bool ok;
+  const double q = div_tail(a, b, r, ok);
+  bad |= !ok;
+  return q;
+}
+__device__ __forceinline__ float div_defer(float a, float b, float, bool&) { return a / b; }
+template <bool EXACT>
+__device__ __forceinline__ real divx(real a, real b, real r, bool& bad) {
+  if constexpr (EXACT) return a / b;
+  else return div_defer(a, b, r, bad);
+}
+
 // search = -(L L')^-1 g (oracle chol_solve and the sign flip)
-template <int NV>
-__device__ inline void chol_solve_u(const real (&Hf)[NV][NV], const real (&rd)[NV], const real (&g)[NV],
-                                    real (&sv)[NV]) {
+template <int NV, bool EXACT>
+__device__ inline bool chol_solve_u_impl(const real (&Hf)[NV][NV], const real (&rd)[NV], const real (&g)[NV],
+                                         real (&sv)[NV]) {
+  bool bad = false;
   real x[NV], acc[NV];
   sfor<0, NV>(SLAM(ii) { acc[SK(ii)] = 0; });
   // forward: x[i] = (g[i] - dotn(L_i, x, i)) / L_ii, the dot products grown as
-  // the x[j] are final (ascending j from +0: dotn's order)
+  // the x[j] are final (ascending j from +0: dotn's order); the scheduling
+  // barriers keep each product right behind the x[j] it needs (in-order issue:
+  // the compiler otherwise sinks them to the next division's operand)
   sfor<0, NV>(SLAM(ii) {
     constexpr int i = SK(ii);
     real t = g[i];
     if constexpr (i > 0) t -= acc[i];
-    x[i] = divu(t, Hf[i][i], rd[i]);
+    x[i] = divx<EXACT>(t, Hf[i][i], rd[i], bad);
     sfor<i + 1, NV>(SLAM(kk) { acc[SK(kk)] += Hf[SK(kk)][i] * x[i]; });
+    __builtin_amdgcn_sched_barrier(0);
   });
   // backward: x[i] -= L[j][i] x[j] for j = i+1.. ascending, then / L_ii
+  real pr[NV][NV];  // pr[i][j] = L[j][i] x[j], formed as x[j] is final
   sfor<0, NV>(SLAM(ii) {
     constexpr int i = NV - 1 - SK(ii);
     real t = x[i];
-    sfor<i + 1, NV>(SLAM(jj) { t -= Hf[SK(jj)][i] * x[SK(jj)]; });
-    x[i] = divu(t, Hf[i][i], rd[i]);
+    sfor<i + 1, NV>(SLAM(jj) { t -= pr[i][SK(jj)]; });
+    x[i] = divx<EXACT>(t, Hf[i][i], rd[i], bad);
+    sfor<0, i>(SLAM(kk) { pr[SK(kk)][i] = Hf[i][SK(kk)] * x[i]; });
+    __builtin_amdgcn_sched_barrier(0);
   });
   sfor<0, NV>(SLAM(jj) { sv[SK(jj)] = -x[SK(jj)]; });
+  return bad;
+}
+template <int NV>
+__device__ inline void chol_solve_u(const real (&Hf)[NV][NV], const real (&rd)[NV], const real (&g)[NV],
+                                    real (&sv)[NV]) {
+  const bool bad = chol_solve_u_impl<NV, false>(Hf, rd, g, sv);
+  if (__builtin_expect(__ballot(bad) != 0, 0)) (void)chol_solve_u_impl<NV, true>(Hf, rd, g, sv);
 }
 // 0.5 sum_j (Ma_j - qfs_j)(qacc_j - qas_j) (oracle gauss_cost)
 template <int N>
@@ -2515,12 +2553,12 @@ __device__ inline void fwd_constraint_u(const auto& m, const auto& L, const auto
   if (row) jar_l[r] = jr;
   real* qa_l = T.w + L.qacc;
   real* wm_l = T.w + L.warm;
-  sfor<0, NV>(SLAM(jj) {
-    if (r == SK(jj)) {
-      qa_l[SK(jj)] = qacc[SK(jj)];
-      wm_l[SK(jj)] = qacc[SK(jj)];
-    }
-  });
+  real qv = qacc[0];
+  sfor<1, NV>(SLAM(jj) { qv = r == SK(jj) ? qacc[SK(jj)] : qv; });
+  if (r < NV) {
+    qa_l[r] = qv;
+    wm_l[r] = qv;
+  }
   TSYNC();
 #ifdef ILQG_STAMPS
   CNT_ADD(6, __builtin_amdgcn_s_memtime() - tnt_);

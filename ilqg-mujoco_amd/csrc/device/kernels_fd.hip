@@ -4,6 +4,8 @@
 //   k_fd_cols_coop    src/mjderivative.cpp:78-206  one workgroup per (point, column)
 //   k_fd_fused_*      the sweep with the Riccati recursion (inc/ilqr.h:133-176)
 //                     streamed behind it, one ticketed launch
+// diagnostic build: stamps from every 64th workgroup (a sample of every team role)
+#define ILQG_STAMP_SAMPLE 6
 #include "coop_common.h"
 #include "riccati.h"
 

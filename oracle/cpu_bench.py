@@ -56,8 +56,12 @@ def setup(blob_path, cost_path, lib, seed):
         for i, x in enumerate(v):
             arr[i] = x
     lib.L.ora_set_cost_desc(desc)
-    # cfg 3 state (tst/test_derivatives.cpp:38-47) + cfg 4's per-seed perturbation
     d = om.make_data()
+    if om.nq != om.nv:
+        # cfg 5 (humanoid): qpos0 with the root at z = 1.4 (humanoid.xml:49-50), qvel 0
+        d.arr("qpos")[2] = 1.4
+        return om, d
+    # cfg 3 state (tst/test_derivatives.cpp:38-47) + cfg 4's per-seed perturbation
     d.step(500)
     d.arr("ctrl")[:] -= 0.1
     if seed >= 0:
@@ -94,10 +98,16 @@ def tuned(blob, cost, H, budget, seed, nalpha):
     alphas = [2.0 ** -i for i in range(nalpha)]
     il = ora.OILQR(om, d, H, cost_fn="ora_cost_desc_fn")
     il.set_dinit(d)
-    il.iterate_ls(alphas, "min_cost")  # warm-up
+
+    def one():
+        if nalpha > 1:
+            il.iterate_ls(alphas, "min_cost")
+        else:
+            il.iterate()
+    one()  # warm-up
     n, t0 = 0, time.perf_counter()
     while True:
-        il.iterate_ls(alphas, "min_cost")
+        one()
         n += 1
         el = time.perf_counter() - t0
         if el > budget:

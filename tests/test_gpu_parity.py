@@ -675,11 +675,18 @@ def test_split_division_is_ieee(ia):
 # Stated tolerances on e = |d - d_ref| / (1 + |d_ref|) over every record entry
 # (measured on MI355X):
 FD32_EPS = 1e-3
-FD32_MEDIAN = 1e-3     # median e (measured 2.2e-4 humanoid)
-FD32_P99 = 0.1         # 99th percentile of e (measured 4.2e-2)
-FD32_FRAC_BIG = 5e-3   # fraction of entries with e > 0.1
-FD32_GAIN_RTOL = 0.1   # K, k, v after the H = 200 recursion, relative to each array's max
-FD32_V_RTOL = 1e-3     # V (measured 6.8e-5)
+# ~2x the measured deviations (round 3, MI355X): records of the humanoid at
+# cfg 5's state, H = 200 -- median e 2.2e-4, p99 4.2e-2, 0.27 % of entries
+# with e > 0.1 (max 15: evaluations where the fp32 perturbed state lands on
+# the other side of a contact or limit activation than the fp64 one); hopper
+# after 500 passive steps, H = 40 -- median 3.4e-5, p99 2.6e-3, max 7.3e-3
+FD32_MEDIAN = 5e-4     # median e
+FD32_P99 = 0.085       # 99th percentile of e
+FD32_FRAC_BIG = 5.5e-3  # fraction of entries with e > 0.1
+# after the H = 200 recursion, max deviation relative to each array's max:
+# measured K 3.7e-2, k 1.03e-2, v 1.15e-2, V 6.8e-5
+FD32_GAIN_RTOL = {"K": 0.075, "k": 0.025, "v": 0.025}
+FD32_V_RTOL = 1.5e-4
 
 
 def _fd32_stats(what, d, dref):
@@ -705,7 +712,7 @@ def test_humanoid_cfg5_fp32_fd(ia, ora):
     errs = {n: _rel(a, b) for n, a, b in (("K", K[0], oa["K"]), ("k", k[0], oa["k"]), ("V", V[0], oa["V"]),
                                           ("v", v[0], oa["v"]))}
     print("cfg5 fp32 FD gains, max relative deviation:", errs)
-    assert errs["V"] <= FD32_V_RTOL and all(errs[n] <= FD32_GAIN_RTOL for n in ("K", "k", "v")), errs
+    assert errs["V"] <= FD32_V_RTOL and all(errs[n] <= FD32_GAIN_RTOL[n] for n in ("K", "k", "v")), errs
 
 
 def test_fp32_fd_hopper_contacts(ia, ora):
@@ -726,3 +733,70 @@ def test_fp32_fd_hopper_contacts(ia, ora):
     g.iterate()
     g.synchronize()
     _fd32_stats("hopper H=40", g.deriv()[0], il.arrays()["deriv"])
+
+
+# multi-iteration fp32-FD runs: the line-search iLQR with the
+# fp32 FD sweep tracks the fp64 oracle run at the same eps iteration by
+# iteration.  (The reference iLQR -- fixed mu = 1000, the Q1 column-major B,
+# no regularization schedule -- does not lower the cost on these models: from
+# cfg 3's hopper state the oracle's own selected cost rises 110 -> 1.2e5 ->
+# 1.8e5 -> 3.6e5, so "the cost decreases" is not a property of the path being
+# reproduced; the fp32 run must follow the fp64 one instead.)  Iteration 1's
+# cost is the fp64 rollout of the initial trajectory (bit-exact); the gap then
+# grows with the iterations as the model's dynamics amplify it.
+# per iteration, ~2x measured (hopper 0, 2.3e-4, 1.2e-2; humanoid 0, 6.5e-3 --
+# its third iteration is past the point where the reference iLQR diverges:
+# the fp64 oracle's own cost there is 1.6e8)
+FD32_COST_RTOL = {"hopper": (1e-12, 5e-4, 3e-2), "humanoid": (1e-12, 1.3e-2)}
+
+
+def _fp32_cost_run(ia, ora, name, cost, st, H, iters, riccati):
+    import workloads
+    m, om = setup(ia, ora, name, cost)
+    alphas = workloads.LINESEARCH_ALPHAS
+    om.lib.L.ora_set_fd_eps(FD32_EPS)
+    try:
+        d = om.make_data()
+        d.set_state(**_state_dict(st, 0))
+        il = ora.OILQR(om, d, H, cost_fn="ora_cost_desc_fn")
+        il.set_dinit(d)
+        oc = []
+        for _ in range(iters):
+            c, sel = il.iterate_ls(alphas, "min_cost")
+            oc.append(float(c[sel]))
+    finally:
+        om.lib.L.ora_set_fd_eps(1e-6)
+    g = ia.ILQR(m, st, H, cost, alphas=alphas, select="min_cost")
+    g.set_riccati(riccati)
+    g.set_fd_precision("f32")
+    gcs = []
+    for _ in range(iters):
+        g.iterate()
+        g.synchronize()
+        c, sel = g.costs()
+        gcs.append(float(c[0][int(sel[0])]))
+    return np.array(gcs), np.array(oc)
+
+
+@pytest.mark.parametrize("name", ["hopper", "humanoid"])
+def test_fp32_fd_multi_iteration_cost(ia, ora, name):
+    """fp32 FD sweep (eps 1e-3) + fp64 Riccati, line-search iterations (8
+    alphas, min-cost; 3 for the hopper, 2 for the humanoid): the selected
+    trajectory cost of every iteration is
+    finite and within FD32_COST_RTOL of the fp64 oracle's at the same eps
+    (hopper: cfg 3's state, H = 100, exact Riccati; humanoid: cfg 5's state,
+    H = 50, MFMA Riccati)"""
+    import workloads
+    if name == "hopper":
+        m, _ = setup(ia, ora, "hopper", ia.HOPPER_COST)
+        st = workloads.hopper_dmain(m, 1)
+        gc, oc = _fp32_cost_run(ia, ora, "hopper", ia.HOPPER_COST, st, 100, len(FD32_COST_RTOL[name]), "exact")
+    else:
+        m, _ = setup(ia, ora, "humanoid", ia.HUMANOID_COST)
+        st = m.reset_state(1)
+        st.qpos[0, 2] = 1.4
+        gc, oc = _fp32_cost_run(ia, ora, "humanoid", ia.HUMANOID_COST, st, 50, len(FD32_COST_RTOL[name]), "mfma")
+    rel = np.abs(gc - oc) / np.abs(oc)
+    print(f"{name} fp32-FD selected costs {gc.tolist()}, fp64 oracle {oc.tolist()}, relative gaps {rel.tolist()}")
+    assert np.all(np.isfinite(gc))
+    assert np.all(rel <= np.array(FD32_COST_RTOL[name])), (rel, FD32_COST_RTOL[name])
