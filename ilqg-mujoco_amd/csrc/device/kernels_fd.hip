@@ -199,11 +199,28 @@ __device__ inline void fd_decode(const FdFused& a, unsigned ntm, unsigned u, int
   else { role = 2; idx = w - a.nut - a.nv; }
 }
 
+#ifdef ILQG_STAMPS
+// diagnostic timeline of the fused sweep: per FD item u (ticket - nB) its
+// start and end (s_memrealtime, 100 MHz) and its XCC / SE / CU; per backward
+// role its start and end (tools/fused_timeline.py)
+constexpr int TL_N = 65536;
+static __device__ unsigned long long g_tl[3 * TL_N];
+static __device__ unsigned long long g_tlb[2 * 64];
+__device__ inline unsigned long long hw_where() {
+  const unsigned hw = __builtin_amdgcn_s_getreg((4 << 0) | (0 << 6) | (31 << 11));       // HW_ID
+  const unsigned xcc = __builtin_amdgcn_s_getreg((20 << 0) | (0 << 6) | (15 << 11));     // XCC_ID
+  return ((unsigned long long)xcc << 32) | hw;
+}
+#endif
 __device__ inline void fd_fused_body(const auto& m, const auto& L, const auto& C, const auto& X, const Team& T,
                                      const FdFused& a, unsigned u) {
   STAMP_INIT();
 #ifdef ILQG_STAMPS
   const unsigned long long tteam_ = __builtin_amdgcn_s_memtime();
+  if (T.tid == 0 && u < (unsigned)TL_N) {
+    g_tl[3 * u] = __builtin_amdgcn_s_memrealtime();
+    g_tl[3 * u + 2] = hw_where();
+  }
 #endif
   const int nv = m.nv, nu = m.nu, nq = m.nq;
   const int nctrl = nu < nv ? nu : nv;  // mjderivative.cpp:78-82 (assumes nv >= nu)
@@ -324,6 +341,7 @@ __device__ inline void fd_fused_body(const auto& m, const auto& L, const auto& C
   TSYNC();
   if (tid == 0) signal_add(done);
 #ifdef ILQG_STAMPS
+  if (tid == 0 && u < (unsigned)TL_N) g_tl[3 * u + 1] = __builtin_amdgcn_s_memrealtime();
   if (tid == 0) atomicMax(&g_fused_diag[4], __builtin_amdgcn_s_memtime());
   if (tid == 0) coop::s_cnt[7] += __builtin_amdgcn_s_memtime() - tteam_;
 #endif
@@ -340,11 +358,13 @@ __device__ inline void fd_backward_role(const MD& mg, const FdFused& a, int s) {
 #ifdef ILQG_STAMPS
   const unsigned long long t0_ = __builtin_amdgcn_s_memtime();
   if (s == 0 && threadIdx.x == 0) g_fused_diag[3] = t0_;
+  if (s < 64 && threadIdx.x == 0) g_tlb[2 * s] = __builtin_amdgcn_s_memrealtime();
 #endif
   backward_seed<NV, NU>(mg, mg.nq, mg.nv, mg.nu, a.P, mg.opt_timestep, a.mu, a.deriv, a.Dp, a.tr, a.K, a.k, a.V,
                         a.v, s, threadIdx.x, lds, a.sync + 4 + (size_t)a.S * a.P, (unsigned)(1 + a.nut + 2 * a.nv),
                         a.fault);
 #ifdef ILQG_STAMPS
+  if (s < 64 && threadIdx.x == 0) g_tlb[2 * s + 1] = __builtin_amdgcn_s_memrealtime();
   if (s < 16 && threadIdx.x == 0) g_fused_diag[8 + s] = __builtin_amdgcn_s_memtime() - t0_;
   if (s == 0 && threadIdx.x == 0) {
     const unsigned long long t1_ = __builtin_amdgcn_s_memtime();
@@ -480,6 +500,20 @@ hipError_t launch_fd_fused_coop(const DevModel& m, const WsLayout& L, const Coop
 }  // namespace ilqg
 
 #ifdef ILQG_STAMPS
+// the fused sweep's timeline (g_tl: 3 words per FD item, then g_tlb: 2 per role)
+extern "C" int ilqg_debug_timeline(unsigned long long* out, int reset) {
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(ilqg::g_tl), sizeof(unsigned long long) * 3 * ilqg::TL_N) != hipSuccess)
+    return 3;
+  if (hipMemcpyFromSymbol(out + 3 * ilqg::TL_N, HIP_SYMBOL(ilqg::g_tlb), sizeof(unsigned long long) * 128) !=
+      hipSuccess)
+    return 3;
+  if (reset) {
+    static unsigned long long z[3 * ilqg::TL_N];
+    (void)hipMemcpyToSymbol(HIP_SYMBOL(ilqg::g_tl), z, sizeof(z));
+    (void)hipMemcpyToSymbol(HIP_SYMBOL(ilqg::g_tlb), z, sizeof(unsigned long long) * 128);
+  }
+  return 0;
+}
 extern "C" int ilqg_debug_fused(unsigned long long* d, int reset) {
   if (hipMemcpyFromSymbol(d, HIP_SYMBOL(ilqg::g_fused_diag), sizeof(unsigned long long) * 24) != hipSuccess) return 3;
   if (reset) {

@@ -1,0 +1,85 @@
+"""Diagnostic build only: timeline of one fused FD sweep + streamed backward pass
+(the bench workload: hopper H=500, 8 seeds x 8 alphas): per FD team its start,
+end and CU; concurrency over time, team durations per role, CUs used.
+  ILQG_LIB=ilqg-mujoco_amd/lib/libilqg_amd_diag.so python tools/fused_timeline.py [S]"""
+import ctypes
+import os
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "ilqg-mujoco_amd"))
+import ilqg_amd as ia  # noqa: E402
+import workloads  # noqa: E402
+
+TL_N = 65536
+L = ia.lib()
+buf = (ctypes.c_ulonglong * (3 * TL_N + 128))()
+S = int(sys.argv[1]) if len(sys.argv) > 1 else 8
+m = ia.Model.load(workloads.model_file("hopper"))
+g = ia.ILQR(m, workloads.hopper_dmain(m, S, sigma=0.01), 500, ia.HOPPER_COST,
+            alphas=tuple(2.0 ** -i for i in range(8)), select="min_cost")
+g.iterate()
+g.synchronize()
+L.ilqg_debug_timeline(buf, 1)
+g.set_timing(True)
+g.timing()
+g.iterate()
+g.synchronize()
+t = g.timing()
+L.ilqg_debug_timeline(buf, 0)
+a = np.frombuffer(buf, dtype=np.uint64)
+nv, nu, P = m.nv, m.nu, 501
+ntm = nu + 2 * nv
+n_items = S * P * (1 + ntm)
+tl = a[: 3 * TL_N].reshape(TL_N, 3)[:n_items]
+tb = a[3 * TL_N:].reshape(64, 2)[:S].astype(np.int64)
+st, en, hw = tl[:, 0].astype(np.int64), tl[:, 1].astype(np.int64), tl[:, 2]
+ok = (st > 0) & (en > 0)
+print(f"S={S}: fused launch {t['fd_backward'][0]:.3f} ms (HIP events); items {n_items}, recorded {ok.sum()}")
+t0 = min(st[ok].min(), tb[:, 0].min())
+us = lambda x: (x - t0) / 100.0  # noqa: E731  s_memrealtime: 100 MHz
+dur = (en - st) / 100.0
+u = np.arange(n_items)
+nC = S * P
+role = np.where(u < nC, 0, 0)
+w = (u - nC) % (S * ntm) % ntm
+role = np.where(u < nC, 0, np.where(w < nu, 3, np.where(w < nu + nv, 1, 2)))
+names = {0: "C (centre)", 1: "V (qvel col)", 2: "Q (qpos col)", 3: "U (ctrl col)"}
+for r in (0, 3, 1, 2):
+    d = dur[(role == r) & ok]
+    print(f"  {names[r]:14s} teams {d.size:6d}  duration us: mean {d.mean():7.1f}  p50 {np.median(d):7.1f}  "
+          f"p99 {np.percentile(d, 99):7.1f}  max {d.max():7.1f}")
+print(f"  team-us in total {dur[ok].sum():.0f}; span of FD teams {us(en[ok].max()) - us(st[ok].min()):.0f} us "
+      f"-> mean concurrency {dur[ok].sum() / (us(en[ok].max()) - us(st[ok].min())):.0f} teams")
+for s in range(S):
+    print(f"  backward role {s}: start {us(tb[s, 0]):7.1f} us, end {us(tb[s, 1]):7.1f} us")
+# concurrency over time in 50-us buckets
+T_end = us(max(en[ok].max(), tb[:, 1].max()))
+edges = np.arange(0, T_end + 50, 50)
+conc = []
+for b0 in edges[:-1]:
+    b1 = b0 + 50
+    ov = np.clip(np.minimum(us(en[ok]), b1) - np.maximum(us(st[ok]), b0), 0, None)
+    conc.append(ov.sum() / 50)
+print("  concurrency per 50 us: " + " ".join(f"{c:.0f}" for c in conc))
+# dispatch front: tickets started per 50 us
+starts = np.histogram(us(st[ok]), bins=edges)[0]
+print("  team starts per 50 us: " + " ".join(str(x) for x in starts))
+# per point: time the record is complete (all teams of (s, p) ended), seed 0
+pts = []
+for p in range(P):
+    idx = [p * S + 0] + [nC + p * S * ntm + 0 * ntm + k for k in range(ntm)]
+    pts.append(us(en[idx].max()))
+pts = np.array(pts)
+print("  seed 0 record complete (us) at points 0,50,...: " + " ".join(f"{pts[p]:.0f}" for p in range(0, P, 50)))
+cu = hw[ok]
+xcc = (cu >> 32) & 0xF
+hwid = cu & 0xFFFFFFFF
+cu_id = (hwid >> 8) & 0xF
+sh = (hwid >> 12) & 1
+se = (hwid >> 13) & 0x7
+key = xcc * 1000 + se * 100 + sh * 16 + cu_id
+print(f"  distinct (xcc, se, sh, cu) used: {len(np.unique(key))}; xcc histogram {np.bincount(xcc.astype(np.int64))}")
+del g
