@@ -1871,22 +1871,114 @@ __device__ inline void hessian_factor(const auto& m, const auto& L, const auto& 
 #define ILQG_LS_NE 8
 #endif
 constexpr int LS_NE = ILQG_LS_NE;
+// the compile-time-model Newton solver's line search entirely on uniform rows
+// (linesearch_u, rows padded to 4 or 8): the rollout's solves (model
+// tolerance, ~1.4 iterations per line search) spend most of theirs in eval(0)
+#ifndef ILQG_LS_U
+#define ILQG_LS_U 0
+#endif
+constexpr bool LS_U = ILQG_LS_U != 0;
+// Speculative bisection (FD translation units): at tolerance 0 nine in ten
+// line-search iterations are bisection steps (the Newton candidate falls
+// outside the bracket; measured on the oracle over the bench's FD sweep), and
+// a run of them is a walk down a binary tree whose nodes are fixed by the
+// bracket alone: node alpha = 0.5 (lo + hi), then lo or hi := alpha by the
+// sign of d1 there.  Once an iteration bisects, lane t evaluates node t of the
+// next LS_TREE_K levels (63 nodes) at once -- its alpha by the same midpoint
+// sequence, d1 and d2 by the same row sums, its own Newton candidate
+// alpha - d1 / d2 and the bisection test against its bracket -- and the wave
+// then walks the tree from the root with the three ballots: a node where
+// |d1| < gtol (or the LS_ITER-th iteration) ends the search, a node whose
+// Newton candidate lies inside its bracket hands its state (alpha, d1, d2,
+// lo, hi) back to the serial loop, else the walk descends.  Every value the
+// walk uses is the one the serial iteration computes, so the result is the
+// same; up to six iterations cost one pass.  Returns true when the search ended.
+#ifndef ILQG_LS_TREE
+#define ILQG_LS_TREE 1
+#endif
+constexpr bool LS_TREE = ILQG_LS_TREE != 0;
+constexpr int LS_TREE_K = 6;
+// rows up to which the tree runs (the uniform-row limit: at tolerance 0 the
+// hopper's bisection steps fall on 4-row (31 %) and 8-row (48 %) solves)
+#ifndef ILQG_LS_TREE_NE
+#define ILQG_LS_TREE_NE 8
+#endif
+constexpr int LS_TREE_NE = ILQG_LS_TREE_NE;
 template <int NE>
-__device__ inline real ls_iterate_rows(real g1, real g2, real jr, real jv, real Di, real c2, bool row, real d1,
-                                       real d2c, real rd2, unsigned long long pmask, real gtol, int& iters) {
-  real ujr[NE], ujv[NE], uD[NE], uc2[NE];
+__device__ inline bool ls_bisect_tree(const real (&ujr)[NE], const real (&ujv)[NE], const real (&uD)[NE],
+                                      const real (&uc2)[NE], real g1, real g2, real gtol, real& alpha, real& d1,
+                                      real& d2c, real& lo, real& hi, int& it) {
+  const int t = (int)__lane_id();
+  const unsigned p1 = (unsigned)(t < 63 ? t : 62) + 1u;  // heap index + 1: 1 b1 b2 .. b_depth
+  const int dt = 31 - __builtin_clz(p1);
+  real l_ = lo, h_ = hi, a_ = 0.5 * (lo + hi);
+  sfor<1, LS_TREE_K>(SLAM(kk) {
+    constexpr int lev = SK(kk);
+    const bool go = lev <= dt;
+    const bool right = go && ((p1 >> (go ? dt - lev : 0)) & 1u);  // d1 < 0 at the parent: lo := its alpha
+    l_ = (go && right) ? a_ : l_;
+    h_ = (go && !right) ? a_ : h_;
+    const real mid = 0.5 * (l_ + h_);
+    a_ = go ? mid : a_;
+  });
+  real s = g1 + g2 * a_, d2 = g2;
   sfor<0, NE>(SLAM(jj) {
     constexpr int j = SK(jj);
-    ujr[j] = bcast(jr, j);
-    ujv[j] = bcast(jv, j);
-    uD[j] = bcast(Di, j);
-    uc2[j] = bcast(c2, j);
+    const real x = ujr[j] + a_ * ujv[j];
+    const real tt = uD[j] * x * ujv[j];
+    const bool ac = x < 0;
+    s += ac ? tt : (real)-0.0;
+    d2 += ac ? uc2[j] : (real)-0.0;
   });
+  const bool neg = s < 0;
+  const real lo2 = neg ? a_ : l_, hi2 = neg ? h_ : a_;
+  const real cand = a_ - s / d2;
+  const unsigned long long mstop = __ballot(fabs(s) < gtol), mneg = __ballot(neg),
+                           mbis = __ballot(hi2 >= 0 && !(cand > lo2 && cand < hi2));
+  // the walk is scalar: the iteration count and node index stay in SGPRs
+  // (readfirstlane: the compiler cannot prove them uniform and would run the
+  // walk under exec masks)
+  int n = 0;
+  it = __builtin_amdgcn_readfirstlane(it);
+  for (int lev = 0; lev < LS_TREE_K; lev++) {
+    it++;
+    if (((mstop >> n) & 1ull) || it >= LS_ITER) {
+      alpha = bcast(a_, n);
+      return true;
+    }
+    if (!((mbis >> n) & 1ull) || lev == LS_TREE_K - 1) {
+      alpha = bcast(a_, n);
+      d1 = bcast(s, n);
+      d2c = bcast(d2, n);
+      lo = bcast(lo2, n);
+      hi = bcast(hi2, n);
+      return false;
+    }
+    n = __builtin_amdgcn_readfirstlane(2 * n + 1 + (int)((mneg >> n) & 1ull));
+  }
+  return false;  // not reached
+}
+
+// the iterations on rows already in wave-uniform registers (ujr, ujv, uD, uc2)
+template <int NE>
+__device__ inline real ls_iterate_u(const real (&ujr)[NE], const real (&ujv)[NE], const real (&uD)[NE],
+                                    const real (&uc2)[NE], real g1, real g2, real jr, real jv, bool row, real d1,
+                                    real d2c, real rd2, unsigned long long pmask, real gtol, int& iters) {
   real alpha = 0, lo = 0, hi = -1;
   int it = 0;
   while (it < LS_ITER) {
+    it = __builtin_amdgcn_readfirstlane(it);
     real anew = alpha - div_ref_lane<0>(d1, d2c, rd2);
-    if (hi >= 0 && !(anew > lo && anew < hi)) anew = 0.5 * (lo + hi);
+    const bool bis = __ballot(hi >= 0 && !(anew > lo && anew < hi)) != 0;  // uniform
+    if constexpr (LS_TREE && NE <= LS_TREE_NE) {
+      if (bis) {
+        if (ls_bisect_tree<NE>(ujr, ujv, uD, uc2, g1, g2, gtol, alpha, d1, d2c, lo, hi, it)) break;
+        rd2 = rcp_ref(d2c);
+        pmask = __ballot(row && jr + alpha * jv < 0);
+        continue;
+      }
+    }
+    if (bis) anew = 0.5 * (lo + hi);
     alpha = anew;
     const unsigned long long am = __ballot(row && jr + alpha * jv < 0);
     real s = g1 + g2 * alpha;
@@ -1911,6 +2003,56 @@ __device__ inline real ls_iterate_rows(real g1, real g2, real jr, real jv, real 
     if (d1 < 0) lo = alpha; else hi = alpha;
   }
   iters = it;
+  return alpha;
+}
+template <int NE>
+__device__ inline real ls_iterate_rows(real g1, real g2, real jr, real jv, real Di, real c2, bool row, real d1,
+                                       real d2c, real rd2, unsigned long long pmask, real gtol, int& iters) {
+  real ujr[NE], ujv[NE], uD[NE], uc2[NE];
+  sfor<0, NE>(SLAM(jj) {
+    constexpr int j = SK(jj);
+    ujr[j] = bcast(jr, j);
+    ujv[j] = bcast(jv, j);
+    uD[j] = bcast(Di, j);
+    uc2[j] = bcast(c2, j);
+  });
+  return ls_iterate_u<NE>(ujr, ujv, uD, uc2, g1, g2, jr, jv, row, d1, d2c, rd2, pmask, gtol, iters);
+}
+
+// the whole exact line search (eval(0) included) on wave-uniform rows, for a
+// solve with at most NE rows (lanes >= ne hold jr = jv = Di = 0, which never
+// activate: x = 0 + alpha 0 is not < 0): eval(0)'s two ordered sums formed on
+// every lane from the broadcast rows instead of two lane walks -- the lane
+// form's expressions and order (linesearch_rows below), inactive rows adding
+// the exact identity -0.0
+template <int NE>
+__device__ inline real linesearch_u(int ne, real g1, real g2, real jr, real jv, real Di, bool row) {
+  real ujr[NE], ujv[NE], uD[NE], uc2[NE];
+  sfor<0, NE>(SLAM(jj) {
+    constexpr int j = SK(jj);
+    ujr[j] = bcast(jr, j);
+    ujv[j] = bcast(jv, j);
+    uD[j] = bcast(Di, j);
+  });
+  real d1 = g1 + g2 * 0.0, d2c = g2;
+  bool a0[NE];
+  sfor<0, NE>(SLAM(jj) {
+    constexpr int j = SK(jj);
+    uc2[j] = uD[j] * ujv[j] * ujv[j];
+    const real x0 = ujr[j] + 0.0 * ujv[j];
+    const real c10 = uD[j] * x0 * ujv[j];
+    a0[j] = x0 < 0;
+    d1 += a0[j] ? c10 : (real)-0.0;
+  });
+  if (__ballot(d1 >= 0) != 0) return 0;  // uniform
+  sfor<0, NE>(SLAM(jj) { d2c += a0[SK(jj)] ? uc2[SK(jj)] : (real)-0.0; });
+  const unsigned long long am = __ballot(row && jr + 0.0 * jv < 0);
+  const real rd2 = rcp_ref(d2c);
+  int iters = 0;
+  const real alpha = ls_iterate_u<NE>(ujr, ujv, uD, uc2, g1, g2, jr, jv, row, d1, d2c, rd2, am,
+                                      LS_TOL * fabs(d1), iters);
+  (void)ne;
+  (void)iters;
   return alpha;
 }
 
@@ -2515,7 +2657,13 @@ __device__ inline void fwd_constraint_u(const auto& m, const auto& L, const auto
       real g1 = 0, g2 = 0;
       sfor<0, NV>(SLAM(jj) { g1 += sv[SK(jj)] * (Ma[SK(jj)] - qfs[SK(jj)]); });
       sfor<0, NV>(SLAM(jj) { g2 += sv[SK(jj)] * Mv[SK(jj)]; });
-      alpha = linesearch_rows(ne, g1, g2, jr, jv, Di, row, T);
+      if constexpr (LS_U) {
+        alpha = ne <= 4 ? linesearch_u<4>(ne, g1, g2, jr, jv, Di, row)
+                : ne <= 8 ? linesearch_u<8>(ne, g1, g2, jr, jv, Di, row)
+                          : linesearch_rows(ne, g1, g2, jr, jv, Di, row, T);
+      } else {
+        alpha = linesearch_rows(ne, g1, g2, jr, jv, Di, row, T);
+      }
     }
     STAMP(16);
     if (__ballot(alpha == 0) != 0) break;  // uniform
@@ -2926,6 +3074,102 @@ __device__ inline void euler(const auto& m, const auto& L, const auto& C, const 
   euler_finish(m, L, C, X, T, false);
 }
 
+// compile-time models with slide/hinge joints only (nq == nv <= RMAX) whose
+// ancestor masks are constants
+#ifndef ILQG_EULER_U
+#define ILQG_EULER_U 1
+#endif
+template <class MT>
+constexpr bool euler_regs_ok() {
+  if constexpr (StaticModel<MT> && ILQG_EULER_U) {
+    if constexpr (MT::nv <= RMAX && MT::nq == MT::nv) {
+      for (int j = 0; j < MT::njnt; j++)
+        if (MT::jnt_type[j] != JNT_SLIDE && MT::jnt_type[j] != JNT_HINGE) return false;
+      return true;
+    }
+  }
+  return false;
+}
+// euler_finish for those models when M + h D is damped and already factored
+// (the rollout's helper wave): the whole chain qacc -> M qacc -> (L'DL)^-1 ->
+// qvel -> qpos on wave-uniform registers, one LDS read phase and one write.
+// M qacc is one row per lane (tdot's order), gathered; the tree solve is
+// solve_ld_rows' sequence with compile-time ancestor sets (a skipped update
+// where x[i] == 0 becomes a select of the unchanged value); qvel += qacc h and
+// qpos += h qvel per joint as integrate_pos.  Returns false (nothing done)
+// when the general path must run.
+template <class MT>
+__device__ inline bool euler_finish_u(const auto& m, const auto& L, const auto& X, const Team& T) {
+  constexpr int NV = MT::nv;
+  using XT = std::remove_cvref_t<decltype(X)>;
+  (void)X;
+  if (!euler_damped(m, T)) return false;
+  const real* s = T.w + L.s_euler;
+  const real *qHLD = s + NV + NV * NV, *qHinv = s + NV + 2 * NV * NV;
+  const real* qM = T.w + L.qM;
+  real qa[NV], x[NV], qv[NV], qp[NV], dinv[NV], LDr[NV][NV];
+  ldu(qa, T.w + L.qacc);
+  ldu(qv, T.w + L.qvel);
+  ldu(qp, T.w + L.qpos);
+  ldu(dinv, qHinv);
+  sfor<0, NV>(SLAM(ii) {
+    constexpr int i = SK(ii);
+    sfor<0, i>(SLAM(jj) {
+      constexpr int j = SK(jj);
+      if constexpr ((XT::pmask[i] >> j) & 1) LDr[i][j] = qHLD[i * NV + j];
+    });
+  });
+  const int r = T.tid < NV ? T.tid : 0;
+  real Mr[NV];
+  sfor<0, NV>(SLAM(jj) { Mr[SK(jj)] = qM[r * NV + SK(jj)]; });
+  gatheru(x, dotu(Mr, qa));
+  // x[j] -= LD[i][j] x[i] for j in anc(i), i descending, where x[i] != 0
+  sfor<0, NV>(SLAM(ii) {
+    constexpr int i = NV - 1 - SK(ii);
+    const bool nz = x[i] != 0;
+    sfor<0, i>(SLAM(jj) {
+      constexpr int j = SK(jj);
+      if constexpr ((XT::pmask[i] >> j) & 1) {
+        const real u = x[j] - LDr[i][j] * x[i];
+        x[j] = nz ? u : x[j];
+      }
+    });
+  });
+  sfor<0, NV>(SLAM(ii) { x[SK(ii)] *= dinv[SK(ii)]; });
+  // x[i] -= LD[i][j] x[j] for j in anc(i) descending, i ascending
+  sfor<0, NV>(SLAM(ii) {
+    constexpr int i = SK(ii);
+    sfor<0, i>(SLAM(jj) {
+      constexpr int j = i - 1 - SK(jj);
+      if constexpr ((XT::pmask[i] >> j) & 1) x[i] -= LDr[i][j] * x[j];
+    });
+  });
+  const real h = m.opt_timestep;
+  sfor<0, NV>(SLAM(ii) { qv[SK(ii)] += x[SK(ii)] * h; });
+  sfor<0, MT::njnt>(SLAM(jj) {
+    constexpr int j = SK(jj);
+    constexpr int pa = MT::jnt_qposadr[j], va = MT::jnt_dofadr[j];
+    qp[pa] += h * qv[va];
+  });
+  real* sw = T.w + L.s_euler;
+  real* qvel = T.w + L.qvel;
+  real* qpos = T.w + L.qpos;
+  real xv = x[0], vv = qv[0], pv = qp[0];
+  sfor<1, NV>(SLAM(ii) {
+    xv = T.tid == SK(ii) ? x[SK(ii)] : xv;
+    vv = T.tid == SK(ii) ? qv[SK(ii)] : vv;
+    pv = T.tid == SK(ii) ? qp[SK(ii)] : pv;
+  });
+  if (T.tid < NV) {
+    sw[T.tid] = xv;
+    qvel[T.tid] = vv;
+    qpos[T.tid] = pv;
+  }
+  if (T.tid == 0) T.w[L.time] += h;
+  TSYNC();
+  return true;
+}
+
 __device__ inline void rk4(const auto& m, const auto& L, const auto& C, const auto& X, const Team& T,
                            int maxiter, real tol) {
   const real A[9] = {0.5, 0, 0, 0, 0.5, 0, 0, 0, 1};
@@ -3167,8 +3411,15 @@ __device__ inline void step_dual_split(const auto& m, const auto& L, const auto&
       reset_data(m, L, T);
       forward_skip(m, L, C, X, T, STAGE_NONE, m.opt_iterations, m.opt_tolerance);
     }
-    if (!eul) rk4(m, L, C, X, T, m.opt_iterations, m.opt_tolerance);
-    else euler_finish(m, L, C, X, T, !reset);
+    if (!eul) {
+      rk4(m, L, C, X, T, m.opt_iterations, m.opt_tolerance);
+    } else {
+      bool done = false;
+      using MT = std::remove_cvref_t<decltype(m)>;
+      if constexpr (euler_regs_ok<MT>())
+        if (!reset) done = euler_finish_u<MT>(m, L, X, T);
+      if (!done) euler_finish(m, L, C, X, T, !reset);
+    }
     STAMP(9);
   }
   __syncthreads();

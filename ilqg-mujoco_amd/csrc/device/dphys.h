@@ -90,6 +90,29 @@ __device__ inline double det_cos(double x) {
   }
 }
 
+// det_sin(x) and det_cos(x) at once, without branches: the four kernel
+// evaluations either function may return (small-angle k_sin / k_cos of x, and
+// k_sin / k_cos of the reduced argument) are all formed -- independent chains,
+// so they overlap -- and each result selects the one its branch would take,
+// with its sign.  Every returned double is the expression det_sin / det_cos
+// evaluate, so the values are identical; what goes is the divergent control
+// flow (two tests and a four-way switch per function, in series).
+__device__ inline void det_sincos(double x, double* s, double* c) {
+  const double PIO4 = 7.85398163397448278999e-01;
+  double y0, y1;
+  const int n = rem_pio2(x, &y0, &y1);
+  const double s0 = k_sin(x, 0.0, 0), c0 = k_cos(x, 0.0);
+  const double sr = k_sin(y0, y1, 1), cr = k_cos(y0, y1);
+  const bool small = fabs(x) < PIO4;
+  const int q = n & 3;
+  const double sl = (q & 1) ? cr : sr;  // sin: q 0 sr, 1 cr, 2 -sr, 3 -cr
+  const double cl = (q & 1) ? sr : cr;  // cos: q 0 cr, 1 -sr, 2 -cr, 3 sr
+  const double sv = (q & 2) ? -sl : sl;
+  const double cv = (q == 1 || q == 2) ? -cl : cl;
+  *s = small ? (x == 0 ? x : s0) : sv;
+  *c = small ? c0 : cv;
+}
+
 template <class A, class B>
 __device__ __forceinline__ auto dot3(const A* a, const B* b) { return a[0] * b[0] + a[1] * b[1] + a[2] * b[2]; }
 template <class R, class A, class B>
@@ -185,8 +208,10 @@ __device__ inline void axis_angle2quat(R* r, const A* axis, G angle) {
   if (angle == 0) {
     r[0] = 1; r[1] = 0; r[2] = 0; r[3] = 0;
   } else {
-    R s = det_sin(angle * 0.5);
-    r[0] = det_cos(angle * 0.5);
+    double sd, cd;
+    det_sincos(angle * 0.5, &sd, &cd);
+    R s = sd;
+    r[0] = cd;
     r[1] = axis[0] * s; r[2] = axis[1] * s; r[3] = axis[2] * s;
   }
 }

@@ -5,9 +5,18 @@
 // searches take ~1.4 iterations: the uniform-row line search (dcoop_impl.h
 // ls_iterate_rows, for the FD sweep's tolerance-0 solves) does not pay here,
 // and its code grew the hopper rollout kernel from 240 to 299 KB, slowing
-// every stage (instruction cache): this translation unit keeps the lane form.
+// every stage (instruction cache): this translation unit keeps the lane form
+// for the iterations of the generic solver, and runs the compile-time models'
+// line searches (eval(0) included) on rows padded to 4 or 8 (linesearch_u).
 #ifndef ILQG_LS_NE
 #define ILQG_LS_NE 0
+#endif
+#ifndef ILQG_LS_U
+#define ILQG_LS_U 1
+#endif
+// (~1.4 iterations per line search: the speculative bisection tree does not pay)
+#ifndef ILQG_LS_TREE
+#define ILQG_LS_TREE 0
 #endif
 #include "coop_common.h"
 
