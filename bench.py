@@ -37,6 +37,27 @@ HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md chip table (spec)
 # 78.6 TFLOP/s; half the guide's 157.3 TFLOP/s FP32 vector rate)
 FP64_PEAK_TFS = 78.6
 FLOPS_JSON = os.path.join(ROOT, "tests", "fixtures", "flops.json")
+SRC_SHA = ia.source_sha()
+
+
+def pmc_traffic(kernel):
+    """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC
+    summaries (profiles/r*_pmc_traffic.json, tools/pmc_summary.py): the newest
+    one taken on these kernel sources (src_sha); failing that the newest one,
+    marked stale"""
+    import glob
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r[0-9][0-9]*_pmc_traffic.json")))
+    docs = []
+    for f in files:
+        with open(f) as fh:
+            docs.append((f, json.load(fh)))
+    docs = [(f, d) for f, d in docs if d.get(kernel) is not None]
+    if not docs:
+        return {"bytes": None, "file": None, "src_sha": None, "head": None, "stale": None}
+    match = [(f, d) for f, d in docs if d.get("src_sha") == SRC_SHA]
+    f, d = (match or docs)[-1]
+    return {"bytes": d[kernel], "file": os.path.relpath(f, ROOT), "src_sha": d.get("src_sha"),
+            "head": d.get("head"), "stale": not match}
 
 
 def algorithmic_flops(S, A, P):
@@ -299,10 +320,9 @@ def main():
     ap.add_argument("--cpu-budget", type=float, default=15.0)
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    # pipelined seed groups (ilqg_solver_set_groups), off by default: G groups,
-    # rollouts on --roll-cus CUs and the FD sweeps on the rest
-    ap.add_argument("--groups", type=int, default=1)
-    ap.add_argument("--roll-cus", type=int, default=128)
+    # how the recursion reads the FD records: the reference's (quirk Q1, the
+    # headline) or the corrected Jacobians (ilqg_solver_set_layout; same work)
+    ap.add_argument("--layout", choices=("reference", "corrected"), default="reference")
     # host-side rehearsal of the multi-rank path on CPU (gloo, no GPU, no measurement)
     ap.add_argument("--dry-run", action="store_true")
     # the headline (cfg 4's per-GPU share) or cfg 5 as a separate line
@@ -352,8 +372,8 @@ def main():
         # legacy null stream, which does not order against the solver's own)
         stream = torch.cuda.Stream()
         solver.set_stream(stream.cuda_stream)
-        if args.groups > 1:
-            solver.set_groups(args.groups, args.roll_cus)
+        if args.layout != "reference":
+            solver.set_layout(args.layout)
         exchange = CostExchange(device_view(solver.device_costs_ptr(), S), world, solver=solver)
 
     def one_step():
@@ -413,11 +433,7 @@ def main():
     dom = max(gtime, key=gtime.get)
     dom_avg_ms = gtime[dom] / max(1, max(per_kernel[k]["launches"] for k in groups[dom]))
     achieved = abytes[dom] / (dom_avg_ms * 1e-3) / 1e9
-    traffic = None
-    pmc = os.path.join(ROOT, "profiles", "pmc_traffic.json")
-    if os.path.exists(pmc):
-        with open(pmc) as f:
-            traffic = json.load(f).get(dom)
+    traffic = pmc_traffic(dom)
 
     # the binding roof: FP64 VALU (algorithmic flops / launch time vs the vector peak)
     aflops = algorithmic_flops(S, A, P)
@@ -443,9 +459,11 @@ def main():
         "config": {"workload": f"hopper_H{H}_{S}seeds_x_{A}alphas_per_gpu", "model": "hopper.xml",
                    "horizon": H, "seeds_per_gpu": S, "linesearch_candidates": A, "global_seeds": world * S,
                    "parallelism": f"seed-sharded x{world} (RCCL all-gather of per-seed costs)",
-                   "seed_groups": args.groups},
+                   "layout": args.layout},
         "roofline": {"bound": "hbm", "kernel": dom, "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                     "frac": achieved / HBM_PEAK_GBS, "traffic": traffic["bytes"],
+                     "traffic_file": traffic["file"], "traffic_src_sha": traffic["src_sha"],
+                     "traffic_head": traffic["head"], "traffic_stale": traffic["stale"], "src_sha": SRC_SHA,
                      "algorithmic_bytes_per_launch": abytes[dom], "avg_launch_ms": dom_avg_ms,
                      "note": "latency/FP64-VALU-bound path; HBM fraction reported per contract",
                      "valu": {"bound": "fp64-valu", "peak_tflops": FP64_PEAK_TFS, "unit": "TFLOP/s",

@@ -259,35 +259,10 @@ struct ilqg_solver {
   // two streams shared a hardware queue: HIP does not guarantee that two
   // launches run concurrently, so every producer/consumer pair stays inside one
   // ticketed launch.)
-  // Pipelined seed groups (ilqg_solver_set_groups): G contiguous seed ranges.
-  // Each group's rollout + selection runs on its own stream (rs), the fused FD
-  // sweeps of all groups take turns on one sweep stream (fs).  The rollout is
-  // latency-bound on S*A/G workgroups while the sweep is throughput-bound, so
-  // while one group rolls out, another group's sweep uses the rest of the
-  // chip.  With a CU budget (roll_cus) the rollout streams and the sweep stream
-  // run on disjoint CU sets: a sweep never refills a rollout's CU (it would
-  // share the rollout's SIMDs) and a rollout never waits for a sweep to drain.
-  // Every kernel and every value is unchanged; only launch order and streams.
-  struct Group {
-    int s0 = 0, ns = 0;
-    hipStream_t rs = nullptr;
-    hipEvent_t costs = nullptr, fd = nullptr;
-    unsigned* sync = nullptr;
-  };
-  std::vector<Group> groups;  // empty: one group, on `stream`
-  hipStream_t fstream = nullptr;
-  hipEvent_t ev_start = nullptr;
-  int roll_cus = 0;
-  void free_groups() {
-    for (auto& g : groups) {
-      if (g.rs) (void)hipStreamDestroy(g.rs);
-      for (hipEvent_t e : {g.costs, g.fd})
-        if (e) (void)hipEventDestroy(e);
-    }
-    groups.clear();
-    if (fstream) (void)hipStreamDestroy(fstream);
-    fstream = nullptr;
-  }
+  // ilqg_solver_set_layout / ilqg_solver_set_value (device/kernels.h RicFlags)
+  int layout = ILQG_LAYOUT_REFERENCE;
+  bool vinit_pending = false;  // the next recursion starts from the uploaded V / v
+  RicFlags flags() const { return RicFlags{layout, vinit_pending ? 1 : 0}; }
   bool timing = false;
   std::vector<std::pair<hipEvent_t, hipEvent_t>> ev[ILQG_NKERNEL];
   std::vector<hipEvent_t> event_pool;
@@ -328,17 +303,9 @@ struct ilqg_solver {
                    c + 3 * nq + 3 * nv, c + 3 * nq + 3 * nv + nu, c + 3 * nq + 3 * nv + 2 * nu};
   }
   // every stream the solver launches on
-  hipError_t sync_all() {
-    hipError_t e = hipStreamSynchronize(stream);
-    for (auto& g : groups)
-      if (e == hipSuccess) e = hipStreamSynchronize(g.rs);
-    if (e == hipSuccess && fstream) e = hipStreamSynchronize(fstream);
-    return e;
-  }
+  hipError_t sync_all() { return hipStreamSynchronize(stream); }
   ~ilqg_solver() {
     (void)sync_all();
-    free_groups();
-    if (ev_start) (void)hipEventDestroy(ev_start);
     for (auto& v : ev)
       for (auto& p : v) {
         (void)hipEventDestroy(p.first);
@@ -816,9 +783,7 @@ static TrajDev toff(TrajDev t, size_t pts, const HostModel& h) {
 }
 
 // rollout of every (seed, alpha) candidate of the range, then selection + setDInit
-// before_select: an event the selection waits on (the previous iteration's
-// per-seed costs, which the selection overwrites, may still be read there)
-static hipError_t forward_range(ilqg_solver* s, const SeedRange& r, hipEvent_t before_select = nullptr) {
+static hipError_t forward_range(ilqg_solver* s, const SeedRange& r) {
   const ilqg_model* m = s->model;
   const HostModel& h = m->host;
   const size_t s0 = r.s0, P = s->P, A = s->A, nx = s->nx;
@@ -835,10 +800,6 @@ static hipError_t forward_range(ilqg_solver* s, const SeedRange& r, hipEvent_t b
                                s->alphas.as<double>(), di, qa, xf, 0, s->cview(), cc, r.st);
   }, r.st);
   if (e != hipSuccess) return e;
-  if (before_select) {
-    e = hipStreamWaitEvent(r.st, before_select, 0);
-    if (e != hipSuccess) return e;
-  }
   return s->timed(1, [&] {
     return launch_select(m->dm, r.ns, s->A, s->P, s->opts.select_mode, multi ? 1 : 0, cc, s->sel.as<int>() + s0,
                          s->cost_sel.as<double>() + s0, outv, nom, di, r.st);
@@ -847,7 +808,6 @@ static hipError_t forward_range(ilqg_solver* s, const SeedRange& r, hipEvent_t b
 
 int ilqg_forward(ilqg_solver* s) {
   if (!s || !s->initialized) return fail(ILQG_ERR_ARG, "solver not initialised");
-  if (!s->groups.empty()) HIPCHK(s->sync_all());  // a lone forward pass: every group settled
   HIPCHK(forward_range(s, whole(s)));
   return ILQG_OK;
 }
@@ -884,6 +844,7 @@ static hipError_t fused_launch(ilqg_solver* s, const SeedRange& r, int mode) {
   a.k = s->k.as<double>() + s0 * P * h.nu;
   a.V = s->V.as<double>() + s0 * nx * nx;
   a.v = s->v.as<double>() + s0 * nx;
+  a.fl = s->flags();
   return launch_fd_fused_coop(m->dm, m->Lc, m->C, m->X, a, r.st);
 }
 
@@ -892,7 +853,6 @@ int ilqg_fd_sweep(ilqg_solver* s) {
   const ilqg_model* m = s->model;
   TrajDev nom = s->tview(s->traj);
   const int npts = s->S * s->P;
-  if (!s->groups.empty()) HIPCHK(s->sync_all());
   if (s->fused) {
     HIPCHK(s->timed(3, [&] { return fused_launch(s, whole(s), 0); }));
     return ILQG_OK;
@@ -921,48 +881,27 @@ int ilqg_fd_sweep(ilqg_solver* s) {
 int ilqg_backward(ilqg_solver* s) {
   if (!s || !s->initialized) return fail(ILQG_ERR_ARG, "solver not initialised");
   const ilqg_model* m = s->model;
-  if (!s->groups.empty()) HIPCHK(s->sync_all());
   HIPCHK(s->timed(4, [&] {
     if (s->riccati == ILQG_RICCATI_MFMA)
       return launch_backward_mfma(m->dm, s->S, s->P, s->opts.mu, s->deriv.as<double>(), s->Dp, s->tview(s->traj),
                                   s->K.as<double>(), s->k.as<double>(), s->V.as<double>(), s->v.as<double>(),
-                                  s->stream);
+                                  s->flags(), s->stream);
     return launch_backward(m->dm, s->S, s->P, s->opts.mu, s->deriv.as<double>(), s->Dp, s->tview(s->traj),
-                           s->K.as<double>(), s->k.as<double>(), s->V.as<double>(), s->v.as<double>(), s->stream);
+                           s->K.as<double>(), s->k.as<double>(), s->V.as<double>(), s->v.as<double>(), s->flags(),
+                           s->stream);
   }));
-  return ILQG_OK;
-}
-
-// pipelined seed groups: per group g, on its own stream, the rollout (after
-// g's previous sweep, which read the trajectory it overwrites) and the
-// selection (after the solver stream's start-of-iteration point); then g's
-// fused sweep on the shared sweep stream.  The solver stream waits for every
-// group's selection only -- the per-seed costs of this iteration are ordered
-// there for the cost exchange -- while the sweeps run on behind it.
-static int iterate_groups(ilqg_solver* s) {
-  if (!s->ev_start) HIPCHK(hipEventCreateWithFlags(&s->ev_start, hipEventDisableTiming));
-  HIPCHK(hipEventRecord(s->ev_start, s->stream));
-  for (auto& gr : s->groups) {
-    HIPCHK(hipStreamWaitEvent(gr.rs, gr.fd, 0));
-    HIPCHK(forward_range(s, SeedRange{gr.s0, gr.ns, gr.rs, gr.sync}, s->ev_start));
-    HIPCHK(hipEventRecord(gr.costs, gr.rs));
-    HIPCHK(hipStreamWaitEvent(s->fstream, gr.costs, 0));
-    SeedRange r{gr.s0, gr.ns, s->fstream, gr.sync};
-    HIPCHK(s->timed(5, [&] { return fused_launch(s, r, 1); }, s->fstream));
-    HIPCHK(hipEventRecord(gr.fd, s->fstream));
-  }
-  for (auto& gr : s->groups) HIPCHK(hipStreamWaitEvent(s->stream, gr.costs, 0));
+  s->vinit_pending = false;
   return ILQG_OK;
 }
 
 int ilqg_iterate(ilqg_solver* s) {
   if (!s || !s->initialized) return fail(ILQG_ERR_ARG, "solver not initialised");
-  if (!s->groups.empty()) return iterate_groups(s);
   int rc = ilqg_forward(s);
   if (rc) return rc;
   if (s->fused) {
     // FD sweep with the Riccati recursion of every seed streamed behind it (one launch)
     HIPCHK(s->timed(5, [&] { return fused_launch(s, whole(s), 1); }));
+    s->vinit_pending = false;
     return ILQG_OK;
   }
   rc = ilqg_fd_sweep(s);
@@ -1054,7 +993,6 @@ int ilqg_solver_set_riccati(ilqg_solver* s, int mode) {
   if (mode == ILQG_RICCATI_MFMA) {
     if (!backward_mfma_supported(h.nv, h.nu))
       return fail(ILQG_ERR_UNSUPPORTED, "MFMA Riccati: nu <= 32, 2 nv + 1 <= 256, FD record <= 4096 doubles, LDS <= 160 KB");
-    if (!s->groups.empty()) return fail(ILQG_ERR_UNSUPPORTED, "MFMA Riccati with seed groups");
   }
   HIPCHK(s->sync_all());
   s->riccati = mode;
@@ -1066,10 +1004,7 @@ int ilqg_solver_set_riccati(ilqg_solver* s, int mode) {
 
 int ilqg_solver_set_fd_precision(ilqg_solver* s, int prec) {
   if (!s || (prec != ILQG_FD_F64 && prec != ILQG_FD_F32)) return fail(ILQG_ERR_ARG, "bad argument");
-  if (prec == ILQG_FD_F32) {
-    if (!s->groups.empty()) return fail(ILQG_ERR_UNSUPPORTED, "fp32 FD with seed groups");
-    if (coop_lds_bytes_f32(s->model->Lc, s->model->C) > kMaxLds) return lds_fail();
-  }
+  if (prec == ILQG_FD_F32 && coop_lds_bytes_f32(s->model->Lc, s->model->C) > kMaxLds) return lds_fail();
   HIPCHK(s->sync_all());
   s->fdprec = prec;
   // the fused sweep is the fp64 one: fp32 FD runs the two-kernel sweep, then the recursion
@@ -1077,62 +1012,20 @@ int ilqg_solver_set_fd_precision(ilqg_solver* s, int prec) {
   return ILQG_OK;
 }
 
-int ilqg_solver_set_groups(ilqg_solver* s, int ngroups, int roll_cus) {
-  if (!s || ngroups < 1 || roll_cus < 0) return fail(ILQG_ERR_ARG, "bad argument");
+int ilqg_solver_set_layout(ilqg_solver* s, int layout) {
+  if (!s || (layout != ILQG_LAYOUT_REFERENCE && layout != ILQG_LAYOUT_CORRECTED))
+    return fail(ILQG_ERR_ARG, "bad argument");
   HIPCHK(s->sync_all());
-  s->free_groups();
-  ngroups = std::min(ngroups, s->S);
-  s->roll_cus = 0;
-  if (ngroups == 1) return ILQG_OK;
-  if (!s->fused) return fail(ILQG_ERR_UNSUPPORTED, "seed groups need the fused FD sweep (cooperative model kernels)");
-  int ncu = 0;
-  HIPCHK(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, s->opts.device));
-  // CU masks: the rollout streams get roll_cus CUs spread evenly over the chip
-  // (every k-th CU, so over every XCD), the sweep stream the rest
-  std::vector<uint32_t> rmask((ncu + 31) / 32, 0), fmask(rmask);
-  const bool masked = roll_cus > 0 && roll_cus < ncu;
-  if (masked) {
-    for (int c = 0, j = 0; c < ncu; c++) {
-      const bool r = j < roll_cus && (long)c * roll_cus / ncu >= j;
-      if (r) j++;
-      (r ? rmask : fmask)[c / 32] |= 1u << (c % 32);
-    }
-  }
-  auto mkstream = [&](hipStream_t* st, std::vector<uint32_t>& mask) {
-    return masked ? hipExtStreamCreateWithCUMask(st, (uint32_t)mask.size(), mask.data())
-                  : hipStreamCreateWithFlags(st, hipStreamNonBlocking);
-  };
-  hipError_t e = mkstream(&s->fstream, fmask);
-  if (e != hipSuccess) return hip_fail(e, "seed group sweep stream");
-  s->groups.resize(ngroups);
-  const size_t P = s->P;
-  size_t off = 0;  // u32 words into the hand-off block, 16-byte aligned per group
-  for (int g = 0; g < ngroups; g++) {
-    auto& gr = s->groups[g];
-    gr.s0 = (int)((long)s->S * g / ngroups);
-    gr.ns = (int)((long)s->S * (g + 1) / ngroups) - gr.s0;
-    gr.sync = s->sync.as<unsigned>() + off;
-    off += sync_bytes((size_t)gr.ns * P) / 4;
-    e = mkstream(&gr.rs, rmask);
-    if (e == hipSuccess) e = hipEventCreateWithFlags(&gr.costs, hipEventDisableTiming);
-    if (e == hipSuccess) e = hipEventCreateWithFlags(&gr.fd, hipEventDisableTiming);
-    if (e != hipSuccess) {
-      s->free_groups();
-      return hip_fail(e, "seed group streams");
-    }
-  }
-  if (off * 4 > s->sync.n) {
-    s->free_groups();
-    return fail(ILQG_ERR_ARG, "seed groups: hand-off block too small");
-  }
-  s->roll_cus = masked ? roll_cus : 0;
+  s->layout = layout;
   return ILQG_OK;
 }
 
-int ilqg_solver_get_groups(ilqg_solver* s, int* ngroups, int* roll_cus) {
-  if (!s || !ngroups) return fail(ILQG_ERR_ARG, "bad argument");
-  *ngroups = s->groups.empty() ? 1 : (int)s->groups.size();
-  if (roll_cus) *roll_cus = s->roll_cus;
+int ilqg_solver_set_value(ilqg_solver* s, const double* V, const double* v) {
+  if (!s || !V || !v) return fail(ILQG_ERR_ARG, "bad argument");
+  HIPCHK(s->sync_all());
+  HIPCHK(hipMemcpy(s->V.p, V, s->V.n, hipMemcpyHostToDevice));
+  HIPCHK(hipMemcpy(s->v.p, v, s->v.n, hipMemcpyHostToDevice));
+  s->vinit_pending = true;
   return ILQG_OK;
 }
 

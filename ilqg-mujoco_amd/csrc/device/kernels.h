@@ -21,6 +21,32 @@ struct CostDev {
   const double *wq, *tq, *lq, *wv, *tv, *lv, *wu, *tu, *lu;
 };
 
+// How the Riccati recursion reads an FD record (ilqg_solver_set_layout).
+// The record is always the reference's (row-major by output, mjderivative.cpp:
+// 107,138,202).  REFERENCE: A's lower blocks and B are Eigen column-major maps
+// of those row-major blocks (differentiator.h:57-59,89-92, quirk Q1: dt J^T,
+// and a permuted dt J_u for nu > 1).  CORRECTED: the true Jacobians, dt J and
+// dt J_u.  The recursion stages entry e of a record from record index
+// rec_src(e): identity in the reference layout, the three Jacobian blocks
+// transposed in the corrected one.
+struct RicFlags {
+  int layout;  // 0 reference, 1 corrected
+  int vinit;   // 1: V0 / v0 are read from V / v instead of initV's (inc/ilqr.h:100-107)
+};
+__host__ __device__ inline int rec_src(int e, int nv, int nu, int layout) {
+  if (!layout) return e;
+  const int nn = nv * nv;
+  if (e < 2 * nn) {  // A block b (0 qpos, 1 qvel): staged (r + c nv) <- record (c + r nv)
+    const int b = e >= nn, f = e - b * nn, r = f % nv, c = f / nv;
+    return b * nn + c + r * nv;
+  }
+  if (e < 2 * nn + nv * nu) {  // B: staged (r + a nv) <- record (a + r nu)
+    const int f = e - 2 * nn, r = f % nv, a = f / nv;
+    return 2 * nn + a + r * nu;
+  }
+  return e;  // cost gradients
+}
+
 // candidate selection + setDInit(dArray[N])
 hipError_t launch_selftest_div(const double* a, const double* b, double* q, double* q2, int n, hipStream_t st);
 hipError_t launch_select(const DevModel& m, int S, int A, int P, int mode, int copy_cand, const double* cost_cand,
@@ -28,13 +54,13 @@ hipError_t launch_select(const DevModel& m, int S, int A, int P, int mode, int c
 // Riccati backward pass, one workgroup per seed
 // deriv records at stride Ds (>= D) doubles
 hipError_t launch_backward(const DevModel& m, int S, int P, double mu, const double* deriv, int Ds, TrajDev tr,
-                           double* K, double* k, double* V, double* v, hipStream_t st);
+                           double* K, double* k, double* V, double* v, RicFlags fl, hipStream_t st);
 size_t backward_lds_bytes(int nv, int nu);
 // the same recursion with the matrix products on the fp64 matrix cores
 // (riccati_mfma.h): one 4-wave workgroup per seed; agrees with the oracle to
 // rounding (the product sums run in the matrix core's order)
 hipError_t launch_backward_mfma(const DevModel& m, int S, int P, double mu, const double* deriv, int Ds, TrajDev tr,
-                                double* K, double* k, double* V, double* v, hipStream_t st);
+                                double* K, double* k, double* V, double* v, RicFlags fl, hipStream_t st);
 size_t backward_mfma_lds_bytes(int nv, int nu);
 bool backward_mfma_supported(int nv, int nu);
 
@@ -55,6 +81,7 @@ struct FdFused {
   unsigned* fault; // set by a timed-out wait
   double mu;
   double *K, *k, *V, *v;
+  RicFlags fl;
 };
 
 }  // namespace ilqg

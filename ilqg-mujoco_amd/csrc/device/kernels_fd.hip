@@ -362,7 +362,7 @@ __device__ inline void fd_backward_role(const MD& mg, const FdFused& a, int s) {
 #endif
   backward_seed<NV, NU>(mg, mg.nq, mg.nv, mg.nu, a.P, mg.opt_timestep, a.mu, a.deriv, a.Dp, a.tr, a.K, a.k, a.V,
                         a.v, s, threadIdx.x, lds, a.sync + 4 + (size_t)a.S * a.P, (unsigned)(1 + a.nut + 2 * a.nv),
-                        a.fault);
+                        a.fault, a.fl);
 #ifdef ILQG_STAMPS
   if (s < 64 && threadIdx.x == 0) g_tlb[2 * s + 1] = __builtin_amdgcn_s_memrealtime();
   if (s < 16 && threadIdx.x == 0) g_fused_diag[8 + s] = __builtin_amdgcn_s_memtime() - t0_;

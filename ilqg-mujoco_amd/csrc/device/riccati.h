@@ -221,12 +221,12 @@ template <int NV_, int NU_, class MD>
 __device__ inline void backward_seed(const MD& m, int nq, int nv_rt, int nu_rt, int P, double dt, double mu,
                                      const double* deriv, int Ds, TrajDev tr, double* Kg, double* kg, double* Vg,
                                      double* vg, int s, int tid, double* sh, const unsigned* done, unsigned target,
-                                     unsigned* fault) {
+                                     unsigned* fault, RicFlags fl) {
 #ifndef ILQG_RIC_LDS
   // bundled small models: the register/exchange formulation (riccati_reg.h)
   if constexpr (RicReg<NV_, NU_>::ok) {
     if (nq == NV_) {
-      backward_seed_reg<NV_, NU_>(m, P, dt, mu, deriv, Ds, tr, Kg, kg, Vg, vg, s, tid, sh, done, target, fault);
+      backward_seed_reg<NV_, NU_>(m, P, dt, mu, deriv, Ds, tr, Kg, kg, Vg, vg, s, tid, sh, done, target, fault, fl);
       return;
     }
   }
@@ -293,15 +293,16 @@ __device__ inline void backward_seed(const MD& m, int nq, int nv_rt, int nu_rt, 
   {
     ready(0);
     const double* q0 = deriv + ((size_t)s * P + 0) * Ds + 2 * nv * nv + nv * nu;
-    for (int i = tid; i < nx; i += BW_THREADS) v[i] = ld(q0 + i);
+    // v0 = dgdx at the terminal point, or the caller's (an initV override)
+    for (int i = tid; i < nx; i += BW_THREADS) v[i] = fl.vinit ? vg[(size_t)s * nx + i] : ld(q0 + i);
     ready(P > 1 ? 1 : 0);
     const double* d1 = deriv + ((size_t)s * P + (P > 1 ? 1 : 0)) * Ds;
     if (pref)
-      for (int i = tid; i < D; i += BW_THREADS) dl[i] = ld(d1 + i);
+      for (int i = tid; i < D; i += BW_THREADS) dl[i] = ld(d1 + rec_src(i, nv, nu, fl.layout));
     __syncthreads();
     for (int e = tid; e < nx * nx; e += BW_THREADS) {
       int i = e % nx, j = e / nx;
-      V[i + j * LX] = v[i] * v[j];
+      V[i + j * LX] = fl.vinit ? Vg[(size_t)s * nx * nx + e] : v[i] * v[j];
     }
     __syncthreads();
   }
@@ -330,10 +331,13 @@ __device__ inline void backward_seed(const MD& m, int nq, int nv_rt, int nu_rt, 
 #pragma unroll
       for (int t = 0; t < BW_PF; t++) {
         int i = tid + t * BW_THREADS;
-        pf[t] = i < D ? ld(dn1 + i) : 0.0;
+        pf[t] = i < D ? ld(dn1 + rec_src(i, nv, nu, fl.layout)) : 0.0;
       }
     }
-    const double* dn = pref ? dl : deriv + pc * Ds;
+    const double* dn0 = pref ? dl : deriv + pc * Ds;
+    // record entry e as the recursion reads it (staged records are already in the layout)
+    const int lay = pref ? 0 : fl.layout;
+    auto dn = [&](int e) -> double { return dn0[rec_src(e, nv, nu, lay)]; };
     // stage 1: symmetrise V, assemble A/B (differentiator.h:66-71,89-92), q, r, c
     for (int e = tid; e < nx * nx; e += BW_THREADS) {
       int i = e % nx, j = e / nx;
@@ -341,16 +345,16 @@ __device__ inline void backward_seed(const MD& m, int nq, int nv_rt, int nu_rt, 
       double val;
       if (i < nv && j < nv) val = (i == j) ? 1 : 0;
       else if (i < nv) val = (i == j - nv) ? dt : 0;
-      else if (j < nv) val = dn[(i - nv) + j * nv] * dt;
-      else val = ((i - nv) == (j - nv) ? 1 : 0) + dn[nv * nv + (i - nv) + (j - nv) * nv] * dt;
+      else if (j < nv) val = dn((i - nv) + j * nv) * dt;
+      else val = ((i - nv) == (j - nv) ? 1 : 0) + dn(nv * nv + (i - nv) + (j - nv) * nv) * dt;
       A[i + j * LX] = val;
     }
     for (int e = tid; e < nx * nu; e += BW_THREADS) {
       int i = e % nx, j = e / nx;
-      B[i + j * LX] = (i < nv) ? 0 : dn[2 * nv * nv + (i - nv) + j * nv] * dt;
+      B[i + j * LX] = (i < nv) ? 0 : dn(2 * nv * nv + (i - nv) + j * nv) * dt;
     }
     for (int i = tid; i < nx; i += BW_THREADS) {
-      q[i] = dn[2 * nv * nv + nv * nu + i];
+      q[i] = dn(2 * nv * nv + nv * nu + i);
       // c = x*_{n-1} (-) x*_n (inc/ilqr.h:154-157; tangent space for quaternion joints)
       if (xreg) {
         c[i] = xa - xb;  // i == tid
@@ -362,7 +366,7 @@ __device__ inline void backward_seed(const MD& m, int nq, int nv_rt, int nu_rt, 
         c[i] = xp - xc;
       }
     }
-    for (int a = tid; a < nu; a += BW_THREADS) r[a] = dn[2 * nv * nv + nv * nu + nx + a];
+    for (int a = tid; a < nu; a += BW_THREADS) r[a] = dn(2 * nv * nv + nv * nu + nx + a);
     __syncthreads();
     for (int i = tid; i < nx; i += BW_THREADS) Vs[i + i * LX] += mu;
     __syncthreads();

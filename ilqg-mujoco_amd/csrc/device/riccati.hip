@@ -48,25 +48,27 @@ namespace {
 
 __global__ __launch_bounds__(rmfma::THREADS) void k_backward_mfma(DevModel m, int nq, int nv, int nu, int P, double dt,
                                                                   double mu, const double* deriv, int Ds, TrajDev tr,
-                                                                  double* Kg, double* kg, double* Vg, double* vg) {
+                                                                  double* Kg, double* kg, double* Vg, double* vg,
+                                                                  RicFlags fl) {
   extern __shared__ double sh[];
-  rmfma::backward_seed_mfma(m, nq, nv, nu, P, dt, mu, deriv, Ds, tr, Kg, kg, Vg, vg, blockIdx.x, sh);
+  rmfma::backward_seed_mfma(m, nq, nv, nu, P, dt, mu, deriv, Ds, tr, Kg, kg, Vg, vg, blockIdx.x, sh, fl);
 }
 
 template <int NV_, int NU_>
 __global__ __launch_bounds__(BW_THREADS) void k_backward(DevModel m, int nq, int nv_rt, int nu_rt, int P, double dt,
                                                          double mu, const double* deriv, int Ds, TrajDev tr,
-                                                         double* Kg, double* kg, double* Vg, double* vg) {
+                                                         double* Kg, double* kg, double* Vg, double* vg,
+                                                         RicFlags fl) {
   extern __shared__ double sh[];
   backward_seed<NV_, NU_>(m, nq, nv_rt, nu_rt, P, dt, mu, deriv, Ds, tr, Kg, kg, Vg, vg, blockIdx.x, threadIdx.x, sh,
-                          nullptr, 0u, nullptr);
+                          nullptr, 0u, nullptr, fl);
 }
 
 template <int NV, int NU>
 void launch_t(const DevModel& m, int S, int P, double mu, const double* deriv, int Ds, TrajDev tr, double* K,
-              double* k, double* V, double* v, size_t lds, hipStream_t st) {
+              double* k, double* V, double* v, RicFlags fl, size_t lds, hipStream_t st) {
   hipLaunchKernelGGL((k_backward<NV, NU>), dim3(S), dim3(BW_THREADS), lds, st, m, m.nq, m.nv, m.nu, P,
-                     m.opt_timestep, mu, deriv, Ds, tr, K, k, V, v);
+                     m.opt_timestep, mu, deriv, Ds, tr, K, k, V, v, fl);
 }
 
 }  // namespace
@@ -91,19 +93,19 @@ bool backward_mfma_supported(int nv, int nu) {
 }
 
 hipError_t launch_backward_mfma(const DevModel& m, int S, int P, double mu, const double* deriv, int Ds, TrajDev tr,
-                                double* K, double* k, double* V, double* v, hipStream_t st) {
+                                double* K, double* k, double* V, double* v, RicFlags fl, hipStream_t st) {
   if (!backward_mfma_supported(m.nv, m.nu)) return hipErrorInvalidValue;
   const size_t lds = rmfma::lds_doubles(m.nv, m.nu) * sizeof(double);  // dynamic part
   hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(k_backward_mfma),
                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   if (e != hipSuccess) return e;
   hipLaunchKernelGGL(k_backward_mfma, dim3(S), dim3(rmfma::THREADS), lds, st, m, m.nq, m.nv, m.nu, P,
-                     m.opt_timestep, mu, deriv, Ds, tr, K, k, V, v);
+                     m.opt_timestep, mu, deriv, Ds, tr, K, k, V, v, fl);
   return hipGetLastError();
 }
 
 hipError_t launch_backward(const DevModel& m, int S, int P, double mu, const double* deriv, int Ds, TrajDev tr,
-                           double* K, double* k, double* V, double* v, hipStream_t st) {
+                           double* K, double* k, double* V, double* v, RicFlags fl, hipStream_t st) {
   if (m.nu > 32) return hipErrorInvalidValue;  // LDLT scratch bound
   const size_t lds = backward_lds_bytes(m.nv, m.nu);
   if (lds > 160 * 1024) return hipErrorInvalidValue;
@@ -114,9 +116,9 @@ hipError_t launch_backward(const DevModel& m, int S, int P, double mu, const dou
     hipError_t e = hipFuncSetAttribute(kf, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     if (e != hipSuccess) return e;
   }
-  if (m.nv == 6 && m.nu == 3) launch_t<6, 3>(m, S, P, mu, deriv, Ds, tr, K, k, V, v, lds, st);
-  else if (m.nv == 2 && m.nu == 1) launch_t<2, 1>(m, S, P, mu, deriv, Ds, tr, K, k, V, v, lds, st);
-  else launch_t<0, 0>(m, S, P, mu, deriv, Ds, tr, K, k, V, v, lds, st);
+  if (m.nv == 6 && m.nu == 3) launch_t<6, 3>(m, S, P, mu, deriv, Ds, tr, K, k, V, v, fl, lds, st);
+  else if (m.nv == 2 && m.nu == 1) launch_t<2, 1>(m, S, P, mu, deriv, Ds, tr, K, k, V, v, fl, lds, st);
+  else launch_t<0, 0>(m, S, P, mu, deriv, Ds, tr, K, k, V, v, fl, lds, st);
   return hipGetLastError();
 }
 

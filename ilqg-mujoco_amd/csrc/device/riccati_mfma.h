@@ -77,7 +77,7 @@ __host__ __device__ inline size_t lds_doubles(int nv, int nu) {
 template <class MD>
 __device__ inline void backward_seed_mfma(const MD& m, int nq, int nv, int nu, int P, double dt, double mu,
                                           const double* deriv, int Ds, TrajDev tr, double* Kg, double* kg,
-                                          double* Vg, double* vg, int s, double* sh) {
+                                          double* Vg, double* vg, int s, double* sh, RicFlags fl) {
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int nx = 2 * nv, D = nv * (2 * nv + nu) + 2 * nv + nu;
   const int LX = nx | 1, LU = nu | 1;
@@ -109,13 +109,14 @@ __device__ inline void backward_seed_mfma(const MD& m, int nq, int nv, int nu, i
   // initV at the terminal point dArray[0] (inc/ilqr.h:100-107)
   {
     const double* q0 = deriv + ((size_t)s * P) * Ds + 2 * nv * nv + nv * nu;
-    for (int i = tid; i < nx; i += THREADS) v[i] = q0[i];
+    // v0 = dgdx at the terminal point, or the caller's (an initV override)
+    for (int i = tid; i < nx; i += THREADS) v[i] = fl.vinit ? vg[(size_t)s * nx + i] : q0[i];
     const double* d1 = deriv + ((size_t)s * P + (P > 1 ? 1 : 0)) * Ds;
-    for (int i = tid; i < D; i += THREADS) dl[i] = d1[i];
+    for (int i = tid; i < D; i += THREADS) dl[i] = d1[rec_src(i, nv, nu, fl.layout)];
     __syncthreads();
     for (int e = tid; e < nx * nx; e += THREADS) {
       const int i = e % nx, j = e / nx;
-      V[i + j * LX] = v[i] * v[j];
+      V[i + j * LX] = fl.vinit ? Vg[(size_t)s * nx * nx + e] : v[i] * v[j];
     }
     __syncthreads();
   }
@@ -128,7 +129,7 @@ __device__ inline void backward_seed_mfma(const MD& m, int nq, int nv, int nu, i
 #pragma unroll
       for (int t = 0; t < MPF; t++) {
         const int i = tid + t * THREADS;
-        pf[t] = i < D ? dn1[i] : 0.0;
+        pf[t] = i < D ? dn1[rec_src(i, nv, nu, fl.layout)] : 0.0;
       }
     }
     const double* dn = dl;

@@ -200,7 +200,8 @@ struct RicReg {
 template <int NV, int NU, class MD>
 __device__ inline void backward_seed_reg(const MD& m, int P, double dt, double mu, const double* deriv, int Ds,
                                          TrajDev tr, double* Kg, double* kg, double* Vg, double* vg, int s, int tid,
-                                         double* sh, const unsigned* done, unsigned target, unsigned* fault) {
+                                         double* sh, const unsigned* done, unsigned target, unsigned* fault,
+                                         RicFlags fl) {
   using R = RicReg<NV, NU>;
   constexpr int NX = R::NX, LX = R::LX, RP = R::RP, D = R::D;
   using namespace rreg;
@@ -245,7 +246,7 @@ __device__ inline void backward_seed_reg(const MD& m, int P, double dt, double m
     const double* src = deriv + pt * Ds;
     sf<0, NPF>(RL(tt) {
       const int i = tid + RK(tt) * 64;
-      pf[RK(tt)] = i < D ? ld(src + i) : 0.0;
+      pf[RK(tt)] = i < D ? ld(src + rec_src(i, NV, NU, fl.layout)) : 0.0;
     });
   };
   auto park_rec = [&](const double (&pf)[NPF]) __attribute__((always_inline)) {
@@ -263,7 +264,8 @@ __device__ inline void backward_seed_reg(const MD& m, int P, double dt, double m
   {
     ready(0);
     const double* q0 = deriv + ((size_t)s * P) * Ds + 2 * NV * NV + NV * NU;
-    double v0 = tid < NX ? ld(q0 + tid) : 0.0;
+    // v0 = dgdx at the terminal point, or the caller's (an initV override)
+    double v0 = tid < NX ? (fl.vinit ? vg[(size_t)s * NX + tid] : ld(q0 + tid)) : 0.0;
     if (tid < NX) Vv[tid] = v0;  // parity 0 buffer: v before step 1
     if (P > 1) {
       ready(1);
@@ -272,7 +274,12 @@ __device__ inline void backward_seed_reg(const MD& m, int P, double dt, double m
       park_rec(pf);
     }
     wsync();
-    if (quad) {
+    if (quad && fl.vinit) {
+      sf<0, RP>(RL(rr) {
+        const int i = g + 4 * RK(rr);
+        Vb[i + j * LX] = Vg[(size_t)s * NX * NX + i + j * NX];
+      });
+    } else if (quad) {
       double vv[NX];
       lds_row<NX>(vv, Vv);
       sf<0, RP>(RL(rr) {

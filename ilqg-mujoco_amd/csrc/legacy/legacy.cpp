@@ -403,6 +403,11 @@ void SolverCore::init(const mjData* dmain, mjData* const* dArray) {
                          dmain->qfrc_applied, dmain->xfrc_applied),
         "ILQR init");
   pull_traj(dArray);
+  // the applied forces ride along in every cpMjData record (src/util.cpp:11-12)
+  for (int n = 0; n < I.P; n++) {
+    mju_copy(dArray[n]->qfrc_applied, dmain->qfrc_applied, I.nv);
+    mju_copy(dArray[n]->xfrc_applied, dmain->xfrc_applied, 6 * I.m->nbody);
+  }
 }
 
 void SolverCore::set_dinit(const mjData* d) {
@@ -420,21 +425,19 @@ void SolverCore::backward(mjData* const* dArray, mjtNum* K, mjtNum* k, mjtNum* V
   Impl& I = *p_;
   push_traj(dArray);
   check(ilqg_fd_sweep(I.s), "calcMJDerivatives sweep");
+  check(ilqg_solver_get_deriv(I.s, I.deriv.data()), "ILQR deriv");
   if (!I.device_cost && I.fn) {
     // cost-gradient entries by host evaluation of the user's callback
-    check(ilqg_solver_get_deriv(I.s, I.deriv.data()), "ILQR deriv");
     for (int n = 0; n < I.P; n++) host_cost_columns(I.m, dArray[n], I.fn, &I.deriv[(size_t)n * I.D]);
     check(ilqg_solver_set_deriv(I.s, I.deriv.data()), "ILQR deriv");
   }
+  // V0 / v0 from initV (virtual, inc/ilqr.h:100-107,142)
+  check(ilqg_solver_set_value(I.s, V, v), "ILQR initV");
   check(ilqg_backward(I.s), "backwardPass");
   check(ilqg_solver_get_gains(I.s, K, k), "ILQR gains");
   check(ilqg_solver_get_value(I.s, V, v), "ILQR value");
 }
 
-void SolverCore::iterate(mjData* const* dArray, mjtNum* K, mjtNum* k, mjtNum* V, mjtNum* v) {
-  forward(dArray, K, k);
-  set_dinit(dArray[p_->N]);  // inc/ilqr.h:183
-  backward(dArray, K, k, V, v);
-}
+const mjtNum* SolverCore::deriv(int n) const { return &p_->deriv[(size_t)n * p_->D]; }
 
 }  // namespace ilqg_legacy

@@ -62,12 +62,29 @@ EXPORTS = [
     "ilqg_forward", "ilqg_fd_sweep", "ilqg_backward", "ilqg_iterate", "ilqg_synchronize",
     "ilqg_solver_stream", "ilqg_solver_device_costs", "ilqg_solver_set_stream", "ilqg_solver_set_timing",
     "ilqg_solver_get_timing",
-    "ilqg_solver_debug_set_fault", "ilqg_solver_device_traj", "ilqg_solver_set_groups", "ilqg_solver_get_groups",
+    "ilqg_solver_debug_set_fault", "ilqg_solver_device_traj", "ilqg_solver_set_layout", "ilqg_solver_set_value",
     "ilqg_solver_set_riccati", "ilqg_selftest_div", "ilqg_solver_set_fd_precision",
 ]
 KERNELS = ("rollout", "select", "fd_centre", "fd_cols", "backward", "fd_backward")
 
 _lib = None
+
+
+def source_sha() -> str:
+    """sha256 (16 hex digits) of the device/host sources the library is built
+    from (csrc/**, Makefile): names the kernel code a measurement belongs to
+    without git (the GPU box has no .git)"""
+    import hashlib
+    h = hashlib.sha256()
+    root = os.path.dirname(os.path.abspath(__file__))
+    files = [os.path.join(root, "Makefile")]
+    for d, _, fs in sorted(os.walk(os.path.join(root, "csrc"))):
+        files += [os.path.join(d, f) for f in sorted(fs) if f.endswith((".h", ".hip", ".cpp", ".map"))]
+    for f in files:
+        h.update(os.path.relpath(f, root).encode())
+        with open(f, "rb") as fh:
+            h.update(fh.read())
+    return h.hexdigest()[:16]
 
 
 def lib() -> ctypes.CDLL:
@@ -272,17 +289,19 @@ class State:
         return State(self.time.copy(), self.qpos.copy(), self.qvel.copy(), self.warm.copy(), self.ctrl.copy())
 
 
-def assemble_AB(deriv: np.ndarray, nv: int, nu: int, dt: float):
-    """Differentiator::updateDerivatives (inc/differentiator.h:66-71,89-92),
-    reproducing the column-major Map of the row-major record (quirk Q1)."""
+def assemble_AB(deriv: np.ndarray, nv: int, nu: int, dt: float, layout: str = "reference"):
+    """Differentiator::updateDerivatives (inc/differentiator.h:66-71,89-92).
+    'reference' reproduces the column-major Map of the row-major record (quirk
+    Q1); 'corrected' reads the record's true Jacobians (ilqg_solver_set_layout)."""
     nx = 2 * nv
+    order = "F" if layout == "reference" else "C"
     A = np.zeros((nx, nx))
     A[:nv, :nv] = np.eye(nv)
     A[:nv, nv:] = np.eye(nv) * dt
-    A[nv:, :nv] = deriv[: nv * nv].reshape(nv, nv, order="F") * dt
-    A[nv:, nv:] = np.eye(nv) + deriv[nv * nv: 2 * nv * nv].reshape(nv, nv, order="F") * dt
+    A[nv:, :nv] = deriv[: nv * nv].reshape(nv, nv, order=order) * dt
+    A[nv:, nv:] = np.eye(nv) + deriv[nv * nv: 2 * nv * nv].reshape(nv, nv, order=order) * dt
     B = np.zeros((nx, nu))
-    B[nv:, :] = deriv[2 * nv * nv: 2 * nv * nv + nv * nu].reshape(nv, nu, order="F") * dt
+    B[nv:, :] = deriv[2 * nv * nv: 2 * nv * nv + nv * nu].reshape(nv, nu, order=order) * dt
     return A, B
 
 
@@ -398,11 +417,19 @@ class ILQR:
         """enqueue on an external hipStream_t (e.g. torch.cuda.current_stream().cuda_stream)"""
         _check(lib().ilqg_solver_set_stream(self._h, ctypes.c_void_p(stream) if stream else None), "set_stream")
 
-    def set_groups(self, ngroups: int, roll_cus: int = 0):
-        """pipelined seed groups (ilqg_solver_set_groups): ngroups seed ranges whose
-        rollouts overlap each other's FD sweeps; roll_cus > 0 puts the rollouts on
-        that many CUs and the sweeps on the rest.  Bit-identical to ngroups = 1."""
-        _check(lib().ilqg_solver_set_groups(self._h, int(ngroups), int(roll_cus)), "set_groups")
+    def set_layout(self, layout: str):
+        """'reference' (default: the Differentiator's column-major read of the
+        row-major FD blocks, quirk Q1) or 'corrected' (A lower = dt J, B lower =
+        dt J_u): ilqg_solver_set_layout"""
+        _check(lib().ilqg_solver_set_layout(self._h, {"reference": 0, "corrected": 1}[layout]), "set_layout")
+
+    def set_value(self, V, v):
+        """initV override (virtual ILQR::initV, inc/ilqr.h:100-107): the next
+        backward pass starts from V (S x nx x nx, column-major) and v (S x nx)"""
+        V = _f64(V); v = _f64(v)
+        if V.size != self.S * self.nx * self.nx or v.size != self.S * self.nx:
+            raise IlqgError(f"V / v must hold {self.S}x{self.nx}x{self.nx} / {self.S}x{self.nx} doubles")
+        _check(lib().ilqg_solver_set_value(self._h, _ptr(V), _ptr(v)), "set_value")
 
     def set_riccati(self, mode: str):
         """'exact' (bit-identical to the oracle, default) or 'mfma' (matrix-core
@@ -414,12 +441,6 @@ class ILQR:
         'f32' (BASELINE.json cfg 5: fp32 FD physics, eps 1e-3, fp64 records):
         ilqg_solver_set_fd_precision"""
         _check(lib().ilqg_solver_set_fd_precision(self._h, {"f64": 0, "f32": 1}[prec]), "set_fd_precision")
-
-    def groups(self):
-        """(ngroups, roll_cus) in effect"""
-        g, c = ctypes.c_int(), ctypes.c_int()
-        _check(lib().ilqg_solver_get_groups(self._h, ctypes.byref(g), ctypes.byref(c)), "get_groups")
-        return g.value, c.value
 
     def set_timing(self, enable: bool):
         _check(lib().ilqg_solver_set_timing(self._h, int(enable)), "set_timing")

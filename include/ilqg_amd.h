@@ -156,17 +156,22 @@ int ilqg_solver_set_stream(ilqg_solver* s, void* stream);
 int ilqg_solver_set_timing(ilqg_solver* s, int enable);
 /* synchronises; returns summed device ms and launch counts per kernel, then resets */
 int ilqg_solver_get_timing(ilqg_solver* s, double* ms, int* launches);
-/* MI355X extension (no reference counterpart; ILQR::iterate is one seed):
-   pipelined seed groups.  The solver's seeds as `ngroups` contiguous ranges;
-   each range's rollout + selection runs on a stream of its own, the ranges'
-   fused FD sweeps (with the Riccati recursion) take turns on one sweep
-   stream, so one range's latency-bound rollout overlaps another range's
-   throughput-bound sweep.  roll_cus > 0: the rollout streams run on that many
-   CUs (spread over every XCD), the sweep stream on the others.  Results are
-   bit-identical to ngroups = 1 (one stream).  ilqg_iterate returns with the
-   per-seed costs ordered on the solver stream (ilqg_solver_device_costs) and
-   the sweeps still running behind it; ilqg_synchronize waits for all of it. */
-int ilqg_solver_set_groups(ilqg_solver* s, int ngroups, int roll_cus);
+/* How the Riccati recursion reads the FD records (Differentiator::
+   updateDerivatives, inc/differentiator.h:85-93).  REFERENCE (default): as the
+   reference does -- Eigen column-major maps of the row-major deriv blocks
+   (differentiator.h:57-59), i.e. A's lower blocks are
+   dt J^T and B's lower block is a permutation of dt J_u when nu > 1.
+   CORRECTED: the true linearisation, A lower = [dt J_q, I + dt J_v], B lower =
+   dt J_u (SURVEY.md Appendix A Q1 "provide a corrected mode").  The FD records
+   themselves (ilqg_solver_get_deriv) are the reference's either way. */
+#define ILQG_LAYOUT_REFERENCE 0
+#define ILQG_LAYOUT_CORRECTED 1
+int ilqg_solver_set_layout(ilqg_solver* s, int layout);
+/* initV override (virtual ILQR::initV, inc/ilqr.h:100-107,142): the next
+   backward pass (ilqg_backward or ilqg_iterate) starts its recursion from
+   these V0 (nseed x nx x nx, column-major) and v0 (nseed x nx) instead of the
+   terminal point's v = dgdx, V = v'v.  One-shot: later passes use initV. */
+int ilqg_solver_set_value(ilqg_solver* s, const double* V, const double* v);
 /* Riccati recursion (inc/ilqr.h:133-176) engine.  EXACT (default): the
    oracle's loops, bit-identical K, k, V, v (streamed behind the FD sweep on
    cooperative models).  MFMA: every matrix product (B'V, Quu = -2B'VB - 2R,
@@ -178,7 +183,6 @@ int ilqg_solver_set_groups(ilqg_solver* s, int ngroups, int roll_cus);
 #define ILQG_RICCATI_EXACT 0
 #define ILQG_RICCATI_MFMA 1
 int ilqg_solver_set_riccati(ilqg_solver* s, int mode);
-int ilqg_solver_get_groups(ilqg_solver* s, int* ngroups, int* roll_cus);
 /* FD sweep precision (calcMJDerivatives, src/mjderivative.cpp:212-255).  F64
    (default): the reference's fp64 arithmetic and eps = 1e-6, bit-identical to
    the oracle.  F32: BASELINE.json configs[4]'s "fp32 FD with fp64 Riccati" --

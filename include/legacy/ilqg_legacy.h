@@ -20,10 +20,30 @@ struct Mat {
   mjtNum a[R * C] = {};
   mjtNum& operator()(int i, int j) { return a[i + j * R]; }
   const mjtNum& operator()(int i, int j) const { return a[i + j * R]; }
+  // vectors (R == 1 or C == 1): coefficient i, as Eigen's v(i)
+  mjtNum& operator()(int i) { return a[i]; }
+  const mjtNum& operator()(int i) const { return a[i]; }
   mjtNum* data() { return a; }
   const mjtNum* data() const { return a; }
   static constexpr int rows() { return R; }
   static constexpr int cols() { return C; }
+  static constexpr int size() { return R * C; }
+};
+
+// Column-major R x C view of caller memory, like Eigen::Map<Eigen::Matrix<
+// mjtNum, R, C>> (the reference's *_mt typedefs, inc/ilqr.h:25-33,
+// inc/differentiator.h:20-28).  Re-seated with placement new, as the
+// reference does (`new (x) x_mt(d->qpos)`, inc/differentiator.h:80).
+template <int R, int C>
+struct Map {
+  mjtNum* p;
+  explicit Map(mjtNum* data) : p(data) {}
+  mjtNum& operator()(int i, int j) const { return p[i + j * R]; }
+  mjtNum& operator()(int i) const { return p[i]; }
+  mjtNum* data() const { return p; }
+  static constexpr int rows() { return R; }
+  static constexpr int cols() { return C; }
+  static constexpr int size() { return R * C; }
 };
 
 // Register a device cost descriptor for a host cost callback: ILQR / calcMJDerivatives
@@ -49,8 +69,11 @@ class SolverCore {
   void init(const mjData* dmain, mjData* const* dArray);
   void set_dinit(const mjData* dinit);                    // inc/ilqr.h:110-113
   void forward(mjData* const* dArray, const mjtNum* K, const mjtNum* k);  // inc/ilqr.h:116-130
-  void backward(mjData* const* dArray, mjtNum* K, mjtNum* k, mjtNum* V, mjtNum* v);  // :133-176
-  void iterate(mjData* const* dArray, mjtNum* K, mjtNum* k, mjtNum* V, mjtNum* v);   // :179-186
+  // the Riccati recursion n = 1..N (inc/ilqr.h:144-175) from the V0 / v0 that
+  // initV left in V / v (uploaded, ilqg_solver_set_value); K, k, V, v out
+  void backward(mjData* const* dArray, mjtNum* K, mjtNum* k, mjtNum* V, mjtNum* v);
+  // the FD record (calcMJDerivatives layout) of point n from the last backward
+  const mjtNum* deriv(int n) const;
 
  private:
   void push_traj(mjData* const* dArray);

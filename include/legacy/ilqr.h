@@ -1,17 +1,26 @@
 // Legacy ILQR<nv,nu,N> (reference: inc/ilqr.h:14-188) over the MI355X path.
 //
-// Same constructor, public members and methods, so callers such as
+// Same typedefs, constructor, public members and methods, so callers such as
 // src/inverted_pendulum/inverted_pendulum.cpp compile unchanged:
 //   ILQR<nv,nu,N>(m, dmain, stepCostFn); setDInit(d); iterate();
 //   dArray[N]->ctrl (the first control of the optimised trajectory).
 // The passes run on the GPU (include/ilqg_amd.h, one seed, reference
 // semantics: alpha = 1, mu = 1000).  dArray / K / k / V / v are host mirrors,
-// uploaded before and refreshed after every pass.  Eigen is not required: K, k,
-// V, v are column-major ilqg_legacy::Mat with Eigen's storage order.
+// uploaded before and refreshed after every pass.  Eigen is not required: the
+// matrices are column-major ilqg_legacy::Mat (Eigen's storage order) and the
+// *_mt maps ilqg_legacy::Map views.
+//
+// initV is virtual, as in the reference (inc/ilqr.h:100,142): backwardPass
+// calls it, and the V / v it leaves (the terminal FD's v = dgdx, V = v'v by
+// default, or whatever an override sets) seed the device recursion
+// (ilqg_solver_set_value).
+//
 // Unlike the reference, every ILQR instance owns its own state (the
 // reference's function-static references in backwardPass, inc/ilqr.h:137-140,
-// would alias two instances of one <nv,nu,N>).
+// would alias two instances of one <nv,nu,N>), and the destructor frees it.
 #pragma once
+
+#include <new>
 
 #include "differentiator.h"
 #include "ilqg_legacy.h"
@@ -22,10 +31,28 @@
 template <int nv, int nu, int N>
 class ILQR {
  public:
+  // typedefs for env matrices/vectors (inc/ilqr.h:19-23)
+  typedef ilqg_legacy::Mat<2 * nv, 2 * nv> A_t;
+  typedef ilqg_legacy::Mat<2 * nv, nu> B_t;
+  typedef ilqg_legacy::Mat<2 * nv, 1> x_t;
+  typedef ilqg_legacy::Mat<nu, 1> u_t;
+  // typedefs for env maps (inc/ilqr.h:24-33)
+  typedef ilqg_legacy::Map<nv, nv> dqdq_mt;
+  typedef ilqg_legacy::Map<nv, nu> dqdu_mt;
+  typedef ilqg_legacy::Map<nv, 1> qpos_mt;
+  typedef ilqg_legacy::Map<nv, 1> qvel_mt;
+  typedef ilqg_legacy::Map<nv, 1> ctrl_mt;
+  typedef ilqg_legacy::Map<2 * nv, 1> x_mt;
+  typedef ilqg_legacy::Map<nu, 1> u_mt;
+  typedef ilqg_legacy::Map<1, 2 * nv> q_mt;
+  typedef ilqg_legacy::Map<1, nu> r_mt;
+  // typedefs specific to iLQR (inc/ilqr.h:34-40)
   typedef ilqg_legacy::Mat<nu, 2 * nv> K_t;
   typedef ilqg_legacy::Mat<nu, 1> k_t;
   typedef ilqg_legacy::Mat<2 * nv, 2 * nv> V_t;
   typedef ilqg_legacy::Mat<1, 2 * nv> v_t;
+  typedef ilqg_legacy::Mat<2 * nv, 2 * nv> Q_t;
+  typedef ilqg_legacy::Mat<nu, nu> R_t;
 
   mjModel* m;
   mjData* d = NULL;
@@ -33,45 +60,92 @@ class ILQR {
   mjData* dArray[N + 1];  // dArray[N]: initial state, dArray[0]: terminal state
   V_t* V;
   v_t* v;
-  K_t K[N + 1];
+  K_t K[N + 1];  // K/k[0] are never computed (inc/ilqr.h:56); zero here (quirk Q12)
   k_t k[N + 1];
+  // (qpos, qvel) and ctrl of d; xStar / uStar are re-seated per point by
+  // forwardPass and left on dArray[0] (inc/ilqr.h:59-62,90-93,124-125)
+  x_mt* x;
+  u_mt* u;
+  x_mt* xStar;
+  u_mt* uStar;
   mjtNum mu = 1000.0;  // the device solver is created with this value
 
   ILQR(mjModel* m, mjData* dmain, stepCostFn_t& stepCostFn) : m(m), core_(m, N, stepCostFn) {
     static_assert(sizeof(K_t) == sizeof(mjtNum) * nu * 2 * nv, "K must be dense");
     d = mj_makeData(m);
-    cpMjData(m, d, dmain);
+    setDInit(dmain);
     differentiator = new Differentiator<nv, nu>(m, d, stepCostFn);
     for (int n = N; n >= 0; n--) dArray[n] = mj_makeData(m);
+    // initial passive rollout on the device (inc/ilqr.h:82-87); d then holds
+    // the state one step past dArray[0], as the reference's loop leaves it
+    core_.init(dmain, dArray);
+    step_past_terminal();
+    x = new x_mt(d->qpos);
+    u = new u_mt(d->ctrl);
+    xStar = new x_mt(d->qpos);
+    uStar = new u_mt(d->ctrl);
     V = new V_t;
     v = new v_t;
-    core_.init(dmain, dArray);
   }
   virtual ~ILQR() {
     for (int n = 0; n <= N; n++) mj_deleteData(dArray[n]);
     mj_deleteData(d);
     delete differentiator;
+    delete x;
+    delete u;
+    delete xStar;
+    delete uStar;
     delete V;
     delete v;
   }
+  ILQR(const ILQR&) = delete;
+  ILQR& operator=(const ILQR&) = delete;
 
-  // initV runs on the device at the start of backwardPass (inc/ilqr.h:100-107)
-  virtual void initV() {}
-
-  void setDInit(mjData* dInit) {
-    cpMjData(m, d, dInit);
-    core_.set_dinit(d);
+  // inc/ilqr.h:100-107: FD at the terminal point (on the GPU), v = dgdx, V = v'v
+  virtual void initV() {
+    differentiator->setMJData(dArray[0]);
+    differentiator->updateDerivatives();
+    for (int i = 0; i < 2 * nv; i++) (*v)(0, i) = (*differentiator->dgdx)(0, i);
+    for (int j = 0; j < 2 * nv; j++)
+      for (int i = 0; i < 2 * nv; i++) (*V)(i, j) = (*v)(0, i) * (*v)(0, j);
   }
 
-  void forwardPass() { core_.forward(dArray, K[0].data(), k[0].data()); }
+  void setDInit(mjData* dInit) { cpMjData(m, d, dInit); }
 
-  void backwardPass() { core_.backward(dArray, K[0].data(), k[0].data(), V->data(), v->data()); }
+  // inc/ilqr.h:116-130: u = K[n](x - x*) + k[n] + u*, store, mj_step, n = N..0
+  // (on the device, from the state in d)
+  void forwardPass() {
+    core_.set_dinit(d);
+    core_.forward(dArray, K[0].data(), k[0].data());
+    step_past_terminal();
+    new (xStar) x_mt(dArray[0]->qpos);
+    new (uStar) u_mt(dArray[0]->ctrl);
+  }
 
+  // inc/ilqr.h:133-176: initV (virtual), then FD + Riccati for n = 1..N on the
+  // device; the differentiator is left at dArray[N] with its A / B, as the
+  // reference's last updateDerivatives leaves it
+  void backwardPass() {
+    initV();
+    core_.backward(dArray, K[0].data(), k[0].data(), V->data(), v->data());
+    differentiator->setMJData(dArray[N]);
+    mju_copy(differentiator->deriv, core_.deriv(N), Differentiator<nv, nu>::kD);
+    differentiator->assemble();
+  }
+
+  // inc/ilqr.h:179-186
   void iterate() {
-    core_.iterate(dArray, K[0].data(), k[0].data(), V->data(), v->data());
-    cpMjData(m, d, dArray[N]);
+    forwardPass();
+    setDInit(dArray[N]);
+    backwardPass();
   }
 
  private:
+  // d = dArray[0] stepped once: the reference's rollout loops (inc/ilqr.h:82-87,
+  // 121-129) end with d one mj_step past the terminal point
+  void step_past_terminal() {
+    cpMjData(m, d, dArray[0]);
+    mj_step(m, d);
+  }
   ilqg_legacy::SolverCore core_;
 };

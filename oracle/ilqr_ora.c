@@ -214,20 +214,32 @@ void ora_calcMJDerivatives_tuned(mjModel* m, mjData* dmain, mjtNum* deriv, stepC
   m->opt.tolerance = save_tolerance;
 }
 
-/* ---- A/B assembly, differentiator.h:66-71,89-92 (col-major, quirk Q1) ---- */
+/* ---- A/B assembly, differentiator.h:66-71,89-92 (col-major, quirk Q1) ----
+   Layout 0 (reference): the lower blocks are Eigen column-major maps of the
+   row-major deriv blocks (differentiator.h:57-59): A lower = dt J^T, B lower a
+   permutation of dt J_u when nu > 1.  Layout 1 (corrected, SURVEY.md Appendix A
+   Q1's optional mode): the true Jacobians, entry (r, c) of J_q at
+   deriv[c + r nv] (mjderivative.cpp:202), of J_u at deriv[2nv^2 + c + r nu]
+   (:107). */
+static int ora_layout = 0;
+void ora_set_layout(int layout) { ora_layout = layout; }
+int ora_get_layout(void) { return ora_layout; }
+
 void ora_assemble_AB(int nv, int nu, mjtNum dt, const mjtNum* deriv, mjtNum* A, mjtNum* B) {
-  int nx = 2 * nv;
+  int nx = 2 * nv, L = ora_layout;
   for (int c = 0; c < nx; c++)
     for (int r = 0; r < nx; r++) {
       mjtNum val;
+      int rr = r - nv, cc = c < nv ? c : c - nv;
       if (r < nv && c < nv) val = (r == c) ? 1 : 0;
       else if (r < nv) val = (r == c - nv) ? dt : 0;
-      else if (c < nv) val = deriv[(r - nv) + c * nv] * dt;
-      else val = ((r - nv) == (c - nv) ? 1 : 0) + deriv[nv * nv + (r - nv) + (c - nv) * nv] * dt;
+      else if (c < nv) val = deriv[L ? cc + rr * nv : rr + cc * nv] * dt;
+      else val = (rr == cc ? 1 : 0) + deriv[nv * nv + (L ? cc + rr * nv : rr + cc * nv)] * dt;
       A[r + c * nx] = val;
     }
   for (int c = 0; c < nu; c++)
-    for (int r = 0; r < nx; r++) B[r + c * nx] = (r < nv) ? 0 : deriv[2 * nv * nv + (r - nv) + c * nv] * dt;
+    for (int r = 0; r < nx; r++)
+      B[r + c * nx] = (r < nv) ? 0 : deriv[2 * nv * nv + (L ? c + (r - nv) * nu : (r - nv) + c * nv)] * dt;
 }
 
 /* ---- Eigen-style pivoted LDLT (Eigen/src/Cholesky/LDLT.h, lower) ---- */
@@ -516,17 +528,10 @@ void ora_ilqr_fd_point(ora_ilqr* s, int n) {
   s->calc(s->m, s->dArray[n], s->deriv + (size_t)n * s->D, s->cost);
 }
 
-void ora_ilqr_backwardPass(ora_ilqr* s) {
+/* the recursion n = 1..N from the V, v already in s (ilqr.h:144-175) */
+static void ora_ilqr_recursion(ora_ilqr* s) {
   int nv = s->nv, nu = s->nu, nx = s->nx;
   mjtNum dt = s->m->opt.timestep;
-  /* initV, ilqr.h:100-107 */
-  ora_ilqr_fd_point(s, 0);
-  {
-    const mjtNum* q = s->deriv + 2 * nv * nv + nv * nu;
-    for (int i = 0; i < nx; i++) s->v[i] = q[i];
-    for (int j = 0; j < nx; j++)
-      for (int i = 0; i < nx; i++) s->V[i + j * nx] = s->v[i] * s->v[j];
-  }
   for (int n = 1; n <= s->N; n++) {
     s->cout_lines += 2; /* ilqr.h:146-147 -> counted null sink */
     ora_ilqr_fd_point(s, n);
@@ -538,10 +543,40 @@ void ora_ilqr_backwardPass(ora_ilqr* s) {
   }
 }
 
+void ora_ilqr_backwardPass(ora_ilqr* s) {
+  int nv = s->nv, nu = s->nu, nx = s->nx;
+  /* initV, ilqr.h:100-107 */
+  ora_ilqr_fd_point(s, 0);
+  {
+    const mjtNum* q = s->deriv + 2 * nv * nv + nv * nu;
+    for (int i = 0; i < nx; i++) s->v[i] = q[i];
+    for (int j = 0; j < nx; j++)
+      for (int i = 0; i < nx; i++) s->V[i + j * nx] = s->v[i] * s->v[j];
+  }
+  ora_ilqr_recursion(s);
+}
+
+/* backwardPass with an overridden initV (virtual, ilqr.h:100,142): the
+   recursion starts from the caller's V0 (nx x nx col-major) and v0 */
+void ora_ilqr_backwardPass_v0(ora_ilqr* s, const mjtNum* V0, const mjtNum* v0) {
+  int nx = s->nx;
+  ora_ilqr_fd_point(s, 0);
+  memcpy(s->V, V0, sizeof(mjtNum) * nx * nx);
+  memcpy(s->v, v0, sizeof(mjtNum) * nx);
+  ora_ilqr_recursion(s);
+}
+
 void ora_ilqr_iterate(ora_ilqr* s) {
   ora_ilqr_forwardPass(s);
   ora_ilqr_setDInit(s, s->dArray[s->N]);
   ora_ilqr_backwardPass(s);
+}
+
+/* iterate() of an ILQR subclass whose initV override sets V0, v0 */
+void ora_ilqr_iterate_v0(ora_ilqr* s, const mjtNum* V0, const mjtNum* v0) {
+  ora_ilqr_forwardPass(s);
+  ora_ilqr_setDInit(s, s->dArray[s->N]);
+  ora_ilqr_backwardPass_v0(s, V0, v0);
 }
 
 /* ---- line-search extension (no reference counterpart,

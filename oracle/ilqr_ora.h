@@ -44,6 +44,8 @@ mjtNum ora_cost_eval_desc(const ora_cost_desc* c, const mjtNum* qpos, const mjtN
 void ora_calcMJDerivatives(mjModel* m, mjData* dmain, mjtNum* deriv, stepCostFn_t cost);
 void ora_calcMJDerivatives_tuned(mjModel* m, mjData* dmain, mjtNum* deriv, stepCostFn_t cost,
                                  mjData** pool, int npool);
+void ora_set_layout(int layout); /* 0 reference (quirk Q1), 1 corrected */
+int ora_get_layout(void);
 void ora_assemble_AB(int nv, int nu, mjtNum dt, const mjtNum* deriv, mjtNum* A, mjtNum* B);
 int ora_ldlt_factor(int n, mjtNum* mat, int* transp);
 void ora_ldlt_solve(int n, const mjtNum* L, const int* transp, mjtNum* x);
@@ -62,7 +64,9 @@ void ora_ilqr_setDInit(ora_ilqr* s, const mjData* dinit);
 void ora_ilqr_forwardPass(ora_ilqr* s);
 void ora_ilqr_fd_point(ora_ilqr* s, int n);
 void ora_ilqr_backwardPass(ora_ilqr* s);
+void ora_ilqr_backwardPass_v0(ora_ilqr* s, const mjtNum* V0, const mjtNum* v0);
 void ora_ilqr_iterate(ora_ilqr* s);
+void ora_ilqr_iterate_v0(ora_ilqr* s, const mjtNum* V0, const mjtNum* v0);
 void ora_ilqr_forward_candidates(ora_ilqr* s, int A, const mjtNum* alphas, int select_mode, mjtNum* costs,
                                  int* selected);
 void ora_ilqr_iterate_ls(ora_ilqr* s, int A, const mjtNum* alphas, int select_mode, mjtNum* costs, int* selected);

@@ -84,6 +84,9 @@ class Lib:
         for f in ("ora_ilqr_forward_candidates", "ora_ilqr_iterate_ls"):
             getattr(L, f).argtypes = [ctypes.c_void_p, ctypes.c_int, _dp, ctypes.c_int, _dp, _ip]
         L.ora_ilqr_set_gains.argtypes = [ctypes.c_void_p, _dp, _dp]
+        L.ora_set_layout.argtypes = [ctypes.c_int]
+        L.ora_ilqr_backwardPass_v0.argtypes = [ctypes.c_void_p, _dp, _dp]
+        L.ora_ilqr_iterate_v0.argtypes = [ctypes.c_void_p, _dp, _dp]
         L.ora_riccati_step.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_double, ctypes.c_double,
                                        _dp, _dp, _dp, _dp, _dp, _dp, _dp]
         if hasattr(L, "ref_calcMJDerivatives"):
@@ -200,6 +203,23 @@ class OData:
                 self.arr(k)[:] = v
 
 
+class layout:
+    """with oracle.layout("corrected"): ... -- the Differentiator's A/B
+    assembly in the corrected layout (SURVEY.md Appendix A Q1) for the block;
+    "reference" (quirk Q1) is the default."""
+
+    def __init__(self, name: str, lib: "Lib" = None):
+        self.value = {"reference": 0, "corrected": 1}[name]
+        self.lib = lib or oracle_lib()
+
+    def __enter__(self):
+        self.lib.L.ora_set_layout(self.value)
+        return self
+
+    def __exit__(self, *exc):
+        self.lib.L.ora_set_layout(0)
+
+
 def calc_derivatives(model: OModel, d: OData, cost_fn: str = "ora_cost_pendulum", use_ref=False, nthread=0):
     """calcMJDerivatives at d: the oracle restatement, or (use_ref) the reference's own
     compiled mjderivative.cpp.  cost_fn names a C function in the library."""
@@ -240,6 +260,19 @@ class OILQR:
 
     def iterate(self):
         self.lib.L.ora_ilqr_iterate(self.s)
+
+    def backward_pass_v0(self, V0, v0):
+        """backwardPass with an overridden initV (inc/ilqr.h:100,142): the
+        recursion starts from V0 (nx x nx, column-major) and v0."""
+        V0 = np.ascontiguousarray(V0, dtype=np.float64).ravel()
+        v0 = np.ascontiguousarray(v0, dtype=np.float64).ravel()
+        self.lib.L.ora_ilqr_backwardPass_v0(self.s, V0.ctypes.data_as(_dp), v0.ctypes.data_as(_dp))
+
+    def iterate_v0(self, V0, v0):
+        """iterate() of an ILQR subclass whose initV override sets V0, v0"""
+        V0 = np.ascontiguousarray(V0, dtype=np.float64).ravel()
+        v0 = np.ascontiguousarray(v0, dtype=np.float64).ravel()
+        self.lib.L.ora_ilqr_iterate_v0(self.s, V0.ctypes.data_as(_dp), v0.ctypes.data_as(_dp))
 
     def iterate_ls(self, alphas, select="min_cost"):
         """iterate() with the line-search extension (every candidate rolled out,

@@ -237,29 +237,6 @@ def test_full_size_properties(ia):
     assert np.all(c[np.arange(8), sel] == c.min(axis=1))
 
 
-@pytest.mark.parametrize("groups,roll_cus", [(2, 0), (2, 128), (3, 96), (8, 64)])
-def test_seed_groups_identical(ia, groups, roll_cus):
-    """pipelined seed groups (ilqg_solver_set_groups): the bench workload's
-    trajectories, gains, value functions, FD records and costs after three
-    iterations are the same bits as one group on one stream; ragged ranges
-    (3 groups of 8 seeds) and one seed per group included"""
-    import workloads
-    m = ia.Model.load(model_path("hopper"))
-    dmain = workloads.hopper_dmain(m, 8, sigma=0.01)
-    out = []
-    for G, cus in ((1, 0), (groups, roll_cus)):
-        g = ia.ILQR(m, dmain, 500, ia.HOPPER_COST, alphas=workloads.LINESEARCH_ALPHAS, select="min_cost")
-        g.set_groups(G, cus)
-        assert g.groups()[0] == G
-        for _ in range(3):
-            g.iterate()
-        g.synchronize()
-        t = g.traj()
-        out.append((t.qpos.copy(), t.qvel.copy(), *g.gains(), *g.value(), g.deriv(), *g.costs()))
-    for a, b in zip(*out):
-        exact(a, b, f"groups={groups} roll_cus={roll_cus}")
-
-
 def test_edge_cases(ia, ora):
     """horizon 1, a NaN state (mj_checkPos reset semantics), zero-length-ish inputs"""
     m, om = setup(ia, ora, "hopper", ia.HOPPER_COST)

@@ -5,8 +5,14 @@ FETCH_SIZE / WRITE_SIZE are rocprofv3 derived counters in KiB.  Per
 reports half the bytes of wide coalesced reads, so it is doubled here; that
 calibration is for 16 B/lane streaming reads -- our accesses are narrower, so
 the corrected figure is an upper-side estimate, not an exact byte count.
-Usage: python tools/pmc_summary.py gpurun_out/prof profiles/pmc_traffic.json"""
-import collections, csv, json, re, sys
+The summary records src_sha (ilqg_amd.source_sha(): the kernel sources the
+counters were taken on) and, when GIT_HEAD is set, the commit; bench.py takes
+roofline.traffic from the summary whose src_sha matches the code it runs.
+Usage: python tools/pmc_summary.py gpurun_out/prof profiles/rNN_pmc_traffic.json"""
+import collections, csv, json, os, re, sys
+
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "ilqg-mujoco_amd"))
+import ilqg_amd  # noqa: E402
 
 # kernel-name alternatives per group (model-specific *_s, two-wave *2*, generic *_coop)
 GROUPS = {"rollout": (("k_rollout2_s", "k_rollout_s", "k_rollout2_coop", "k_rollout_coop"),),
@@ -38,7 +44,8 @@ def main(src, dst):
         wa = sum(w[-3:]) / max(1, len(w[-3:]))
         kern[k] = {"launches_seen": len(f), "fetch_bytes_raw": fa, "fetch_bytes_x2": 2 * fa, "write_bytes": wa,
                    "traffic_bytes": 2 * fa + wa}
-    out = {"per_kernel": kern, "note": "FETCH_SIZE doubled per the gfx950 calibration; KiB->bytes x1024"}
+    out = {"per_kernel": kern, "note": "FETCH_SIZE doubled per the gfx950 calibration; KiB->bytes x1024",
+           "src_sha": ilqg_amd.source_sha(), "head": os.environ.get("GIT_HEAD")}
     for g, alts in GROUPS.items():
         picks = [next((k for k in a if k in kern), None) for a in alts]
         if all(picks):
