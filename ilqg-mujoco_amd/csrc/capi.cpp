@@ -225,6 +225,7 @@ struct ilqg_model {
     X.npair = npair;
     X.pmask = h.nv <= 64 ? reinterpret_cast<const unsigned long long*>(static_cast<unsigned char*>(buf.p) + pmask_at)
                          : nullptr;
+    X.haspm = X.pmask != nullptr;
     if (getenv("ILQG_VERBOSE"))
       fprintf(stderr, "ilqg: model nq=%d nv=%d static_id=%d lds/team=%zu B (ws %d + coop %d + image %d doubles, %d ints)\n",
               h.nq, h.nv, dm.static_id, coop_lds_bytes(Lc, C), Lc.nd, C.nd, C.imgd, Lc.ni + C.ni);
@@ -250,7 +251,7 @@ struct ilqg_solver {
   hipStream_t stream = nullptr;
   DevBuf traj[5], cand[5], dinit[5];
   DevBuf qfrc_applied, xfrc_applied, K, k, deriv, warm_c, cost_c, V, v, cost_cand, cost_sel, sel, alphas, cost;
-  DevBuf cw, sync, fault;
+  DevBuf cw, sync, fault, plan_dur, plan_order;
   std::vector<double> host_alphas;
   bool initialized = false;
   hipStream_t own_stream = nullptr;
@@ -634,7 +635,11 @@ int ilqg_solver_create(const ilqg_model* mc, const ilqg_solver_opts* o, const il
   ALLOC(s->deriv, S * P * s->Dp * 8);
   if (s->fused) {
     ALLOC(s->cw, S * P * s->WCp * 8);
-    ALLOC(s->sync, sync_bytes(S * P) + S * 32);  // + per-seed-group alignment
+    ALLOC(s->sync, sync_bytes(S * P));
+    // the ticket schedule and the per-item durations it is planned from (zero: no history)
+    const size_t items = S * P * (1 + (size_t)s->nut + 2 * (size_t)h.nv);
+    ALLOC(s->plan_dur, items * 4);
+    ALLOC(s->plan_order, items * 4);
   }
   ALLOC(s->fault, 16);
   ALLOC(s->warm_c, S * P * h.nv * 8);
@@ -845,6 +850,18 @@ static hipError_t fused_launch(ilqg_solver* s, const SeedRange& r, int mode) {
   a.V = s->V.as<double>() + s0 * nx * nx;
   a.v = s->v.as<double>() + s0 * nx;
   a.fl = s->flags();
+  // ticket schedule from the previous launch's item durations (ILQG_PLAN=0: identity)
+  if (s->plan_dur.p && getenv_int("ILQG_PLAN", 1)) {
+    static const float kthr = [] {
+      const char* e = getenv("ILQG_PLAN_K");
+      return e ? (float)atof(e) : 3.0f;
+    }();
+    e = launch_fd_plan(r.ns, s->P, s->nut + 2 * h.nv, getenv_int("ILQG_PLAN_P0", 8), kthr,
+                       s->plan_dur.as<unsigned>(), s->plan_order.as<unsigned>(), r.st);
+    if (e != hipSuccess) return e;
+    a.order = s->plan_order.as<unsigned>();
+    a.dur = s->plan_dur.as<unsigned>();
+  }
   return launch_fd_fused_coop(m->dm, m->Lc, m->C, m->X, a, r.st);
 }
 
@@ -954,6 +971,21 @@ int ilqg_solver_debug_set_fault(ilqg_solver* s, unsigned value) {
 }
 
 void* ilqg_solver_stream(ilqg_solver* s) { return s ? (void*)s->stream : nullptr; }
+
+int ilqg_solver_debug_plan(ilqg_solver* s, unsigned* order, unsigned* dur, int* nitems) {
+  if (!s || !nitems) return fail(ILQG_ERR_ARG, "bad argument");
+  const HostModel& h = s->model->host;
+  const int n = s->plan_dur.p ? (int)(s->plan_dur.n / 4) : 0;
+  *nitems = n;
+  if (!n || (!order && !dur)) return ILQG_OK;
+  HIPCHK(s->sync_all());
+  HIPCHK(launch_fd_plan(s->S, s->P, s->nut + 2 * h.nv, getenv_int("ILQG_PLAN_P0", 8), 3.0f, s->plan_dur.as<unsigned>(),
+                        s->plan_order.as<unsigned>(), s->stream));
+  HIPCHK(s->sync_all());
+  if (order) HIPCHK(hipMemcpy(order, s->plan_order.p, (size_t)n * 4, hipMemcpyDeviceToHost));
+  if (dur) HIPCHK(hipMemcpy(dur, s->plan_dur.p, (size_t)n * 4, hipMemcpyDeviceToHost));
+  return ILQG_OK;
+}
 
 int ilqg_solver_set_stream(ilqg_solver* s, void* stream) {
   if (!s) return fail(ILQG_ERR_ARG, "null solver");

@@ -67,9 +67,11 @@ __device__ inline void stage_model(const DevModel& g, const CoopAux& Xg, const W
   X.isanc = reinterpret_cast<const int*>(base + (reinterpret_cast<const unsigned char*>(Xg.isanc) - g.img));
   X.pair = reinterpret_cast<const int*>(base + (reinterpret_cast<const unsigned char*>(Xg.pair) - g.img));
   X.npair = Xg.npair;
-  X.pmask = Xg.pmask ? reinterpret_cast<const unsigned long long*>(
-                           base + (reinterpret_cast<const unsigned char*>(Xg.pmask) - g.img))
-                     : nullptr;
+  X.haspm = Xg.haspm;
+  // (an offset select, not a pointer one: a null LDS pointer cast to flat is
+  // what ROCm's backend miscompiles in the stamps build; unread when !haspm)
+  X.pmask = reinterpret_cast<const unsigned long long*>(
+      base + (Xg.haspm ? reinterpret_cast<const unsigned char*>(Xg.pmask) - g.img : 0));
   TSYNC();
 }
 

@@ -808,6 +808,111 @@ __device__ inline void com_pos(const auto& m, const auto& L, const Team& T) {
   TSYNC();
 }
 
+#ifndef ILQG_COM_U
+#define ILQG_COM_U 0
+#endif
+// com_pos for a compile-time model on one wave with the subtree centres of
+// mass in wave-uniform registers (the rollout's primary chain): every lane
+// forms every body's mass-weighted position, the subtree sums (per component,
+// bodies descending, com_pos' order) and the normalisation, so the three LDS
+// exchange phases before the per-body / per-joint phase disappear; each
+// value is com_pos' expression in com_pos' order.
+template <class MT>
+__device__ inline void com_pos_u(const auto& m, const auto& L, const Team& T) {
+  constexpr int NB = MT::nbody;
+  const real* xipos = T.w + L.xipos;
+  real* scom = T.w + L.scom;
+  real* cinert = T.w + L.cinert;
+  const real* ximat = T.w + L.ximat;
+  real* cdof = T.w + L.cdof;
+  const real* xanchor = T.w + L.xanchor;
+  const real* xaxis = T.w + L.xaxis;
+  const real* xmat = T.w + L.xmat;
+  real xi[NB][3], sc[NB][3];
+  sfor<0, NB>(SLAM(ii) {
+    constexpr int i = SK(ii);
+    const real ms = m.body_mass[i];
+    sfor<0, 3>(SLAM(kk) {
+      xi[i][SK(kk)] = xipos[3 * i + SK(kk)];
+      sc[i][SK(kk)] = xi[i][SK(kk)] * ms;
+    });
+  });
+  sfor<0, NB - 1>(SLAM(ii) {
+    constexpr int i = NB - 1 - SK(ii);
+    constexpr int p = MT::body_parentid[i];
+    sfor<0, 3>(SLAM(kk) { sc[p][SK(kk)] += sc[i][SK(kk)]; });
+  });
+  sfor<0, NB>(SLAM(ii) {
+    constexpr int i = SK(ii);
+    const real stm = m.body_subtreemass[i];
+    const bool tiny = stm < MINVAL;
+    const real inv = 1 / (tiny ? 1.0 : stm);
+    sfor<0, 3>(SLAM(kk) { sc[i][SK(kk)] = tiny ? xi[i][SK(kk)] : sc[i][SK(kk)] * inv; });
+  });
+  // scom out: lane e < 3 NB writes entry e
+  if (T.tid < 3 * NB) {
+    real v = sc[0][0];
+    sfor<1, 3 * NB>(SLAM(ee) { v = T.tid == SK(ee) ? sc[SK(ee) / 3][SK(ee) % 3] : v; });
+    scom[T.tid] = v;
+  }
+  // the subtree centre of a body's root, selected from the registers
+  auto root_com = [&](int b, real (&rc)[3]) __attribute__((always_inline)) {
+    const int rid = m.body_rootid[b];
+    sfor<0, 3>(SLAM(kk) { rc[SK(kk)] = sc[0][SK(kk)]; });
+    sfor<1, NB>(SLAM(bb) {
+      sfor<0, 3>(SLAM(kk) { rc[SK(kk)] = rid == SK(bb) ? sc[SK(bb)][SK(kk)] : rc[SK(kk)]; });
+    });
+  };
+  FOR_T(i, NB) {
+    if (i == 0) {
+      for (int k = 0; k < 10; k++) cinert[k] = 0;
+    } else {
+      real off[3], mat[9], in[3], res[10], rc[3];
+      root_com(i, rc);
+      off[0] = xipos[3 * i] - rc[0];
+      off[1] = xipos[3 * i + 1] - rc[1];
+      off[2] = xipos[3 * i + 2] - rc[2];
+      ldm<9>(mat, ximat + 9 * i);
+      ldm<3>(in, m.body_inertia + 3 * i);
+      inert_com(res, in, mat, off, m.body_mass[i]);
+      for (int k = 0; k < 10; k++) cinert[10 * i + k] = res[k];
+    }
+  }
+  FOR_T(j, MT::njnt) {
+    const int da = 6 * m.jnt_dofadr[j];
+    const int bi = m.jnt_bodyid[j];
+    real rc[3];
+    root_com(bi, rc);
+    real off[3] = {rc[0] - xanchor[3 * j], rc[1] - xanchor[3 * j + 1], rc[2] - xanchor[3 * j + 2]};
+    real out[6];
+    const int type = m.jnt_type[j];
+    int skip = 0;
+    if (type == JNT_FREE) {
+      for (int k = 0; k < 18; k++) cdof[da + k] = 0;
+      for (int i = 0; i < 3; i++) cdof[da + 3 + 7 * i] = 1;
+      skip = 18;
+    }
+    if (type == JNT_FREE || type == JNT_BALL) {
+      for (int i = 0; i < 3; i++) {
+        real axis[3] = {xmat[9 * bi + i], xmat[9 * bi + i + 3], xmat[9 * bi + i + 6]};
+        out[0] = axis[0]; out[1] = axis[1]; out[2] = axis[2];
+        cross3(out + 3, axis, off);
+        for (int k = 0; k < 6; k++) cdof[da + skip + 6 * i + k] = out[k];
+      }
+    } else if (type == JNT_SLIDE) {
+      out[0] = out[1] = out[2] = 0;
+      out[3] = xaxis[3 * j]; out[4] = xaxis[3 * j + 1]; out[5] = xaxis[3 * j + 2];
+      for (int k = 0; k < 6; k++) cdof[da + k] = out[k];
+    } else {
+      real ax[3] = {xaxis[3 * j], xaxis[3 * j + 1], xaxis[3 * j + 2]};
+      out[0] = ax[0]; out[1] = ax[1]; out[2] = ax[2];
+      cross3(out + 3, ax, off);
+      for (int k = 0; k < 6; k++) cdof[da + k] = out[k];
+    }
+  }
+  TSYNC();
+}
+
 __device__ inline void crb(const auto& m, const auto& L, const auto& C, const auto& X,
                            const Team& T) {
   const int nv = m.nv, nb = m.nbody;
@@ -845,11 +950,57 @@ __device__ inline void crb(const auto& m, const auto& L, const auto& C, const au
   TSYNC();
 }
 
+// crb for a compile-time model with the composite inertias in wave-uniform
+// registers (the rollout's primary chain): every lane loads every body's
+// cinert and forms the subtree sums (per component, bodies descending, crb's
+// order), so the copy and tree-sum phases disappear; each dof lane then
+// selects its body's composite inertia.  Same expressions, same order.
+template <class MT>
+__device__ inline void crb_u(const auto& m, const auto& L, const auto& C, const auto& X, const Team& T) {
+  constexpr int NB = MT::nbody, NV = MT::nv;
+  const real* cinert = T.w + L.cinert;
+  real* qM = T.w + L.qM;
+  const real* cdof = T.w + L.cdof;
+  real* buf = T.c + C.buf6;
+  real cr[NB][10];
+  sfor<1, NB>(SLAM(ii) {
+    sfor<0, 10>(SLAM(kk) { cr[SK(ii)][SK(kk)] = cinert[10 * SK(ii) + SK(kk)]; });
+  });
+  sfor<0, NB - 1>(SLAM(ii) {
+    constexpr int i = NB - 1 - SK(ii);
+    constexpr int p = MT::body_parentid[i];
+    if constexpr (p > 0) sfor<0, 10>(SLAM(kk) { cr[p][SK(kk)] += cr[i][SK(kk)]; });
+  });
+  if (T.tid < NV) {
+    const int i = T.tid;
+    const int b = m.dof_bodyid[i];
+    real ci[10], cd[6], r[6];
+    sfor<0, 10>(SLAM(kk) { ci[SK(kk)] = cr[1][SK(kk)]; });
+    sfor<2, NB>(SLAM(bb) {
+      sfor<0, 10>(SLAM(kk) { ci[SK(kk)] = b == SK(bb) ? cr[SK(bb)][SK(kk)] : ci[SK(kk)]; });
+    });
+    ldm<6>(cd, cdof + 6 * i);
+    mul_inert_vec(r, ci, cd);
+    for (int k = 0; k < 6; k++) buf[6 * i + k] = r[k];
+  }
+  TSYNC();
+  FOR_T(e, NV * NV) {
+    int i = e / NV, j = e % NV;
+    if (j <= i) {
+      real v = (i == j) ? m.dof_armature[i] : 0.0;
+      if (X.isanc[e]) v += tdot(cdof + 6 * j, buf + 6 * i, 6);
+      qM[e] = v;
+      qM[j * NV + i] = v;
+    }
+  }
+  TSYNC();
+}
+
 // tree L'DL (oracle factor_ld), parallel over ancestor pairs for each k
 __device__ inline void factor_ld(const auto& m, const auto& X, const Team& T, const real* mat, real* LD,
                                  real* diaginv, real* tmpv) {
   const int nv = m.nv;
-  if (nv <= RMAX && X.pmask) {
+  if (nv <= RMAX && has_pmask(X)) {
     factor_ld_rows(nv, X.pmask, T.tid, mat, LD, diaginv);
     return;
   }
@@ -858,7 +1009,7 @@ __device__ inline void factor_ld(const auto& m, const auto& X, const Team& T, co
     LD[e] = (j <= i) ? mat[e] : 0;
   }
   TSYNC();
-  if (nv > SERIAL_NV && nv <= TEAM_SIZE && X.pmask && T.nt == TEAM_SIZE) {
+  if (nv > SERIAL_NV && nv <= TEAM_SIZE && has_pmask(X) && T.nt == TEAM_SIZE) {
     // lane i owns row i.  For each k (descending) every proper ancestor i of k
     // at once: tmp = LD[k][i] / LD[k][k], LD[i][j] -= tmp * LD[k][j] over j in
     // {i} u anc(i) (descending, as the oracle), then LD[k][i] = tmp.  Within
@@ -899,7 +1050,7 @@ __device__ inline void factor_ld(const auto& m, const auto& X, const Team& T, co
   if (nv <= SERIAL_NV) {
     // small trees: the oracle's loop on lane 0 beats 4 LDS round trips per k
     if (T.tid == 0) {
-      if (X.pmask) {
+      if (has_pmask(X)) {
         // ancestor bitmasks replace the dependent parent-pointer chase
         for (int k = nv - 1; k >= 0; k--) {
           if (LD[k * nv + k] < MINVAL) LD[k * nv + k] = MINVAL;
@@ -957,11 +1108,11 @@ __device__ inline void factor_ld(const auto& m, const auto& X, const Team& T, co
 __device__ inline void solve_ld(const auto& m, const auto& X, const Team& T, const real* LD,
                                 const real* diaginv, real* x) {
   const int nv = m.nv;
-  if (nv <= RMAX && X.pmask) {
+  if (nv <= RMAX && has_pmask(X)) {
     solve_ld_rows(nv, X.pmask, T.tid, LD, diaginv, x);
     return;
   }
-  if (nv > SERIAL_NV && nv <= TEAM_SIZE && X.pmask && T.nt == TEAM_SIZE) {
+  if (nv > SERIAL_NV && nv <= TEAM_SIZE && has_pmask(X) && T.nt == TEAM_SIZE) {
     // lane j owns x[j]; the products LD[i][j] * x[.] are formed by the lane
     // holding the operand (one coalesced row read per step) and applied in the
     // oracle's order: the same operations on the same operands
@@ -993,7 +1144,7 @@ __device__ inline void solve_ld(const auto& m, const auto& X, const Team& T, con
     return;
   }
   if (T.tid == 0) {
-    if (X.pmask) {
+    if (has_pmask(X)) {
       for (int i = nv - 1; i >= 0; i--) {
         real tmp = x[i];
         if (tmp != 0)
@@ -1608,6 +1759,106 @@ __device__ inline void fwd_velocity(const auto& m, const auto& L, const auto& C,
   TSYNC();
 }
 
+#ifndef ILQG_VEL_U
+#define ILQG_VEL_U 0
+#endif
+// fwd_velocity's part 1 (com velocities, cdof_dot, RNE -> qfrc_bias) for a
+// compile-time model whose joints are all hinges and slides, in wave-uniform
+// registers (the rollout's primary chain): every lane loads qvel and cdof once
+// and runs the whole chain -- cvel per component down the tree, cdof_dot,
+// the per-body dof terms, cacc, cfrc, the subtree sums, the bias rows -- with
+// no LDS exchange in between; lane d < nv stores qfrc_bias[d] (cvel, cdof_dot
+// and the RNE scratch have no reader outside this stage).  Every value is
+// fwd_velocity's expression, in its order (the "t = 0; t += x" forms kept).
+template <class MT>
+constexpr bool vel_regs_ok() {
+  if constexpr (StaticModel<MT> && ILQG_VEL_U) {
+    if constexpr (MT::nv <= RMAX && MT::nbody <= 8) {
+      for (int j = 0; j < MT::njnt; j++)
+        if (MT::jnt_type[j] != JNT_SLIDE && MT::jnt_type[j] != JNT_HINGE) return false;
+      return true;
+    }
+  }
+  return false;
+}
+template <class MT>
+__device__ inline void fwd_velocity_u(const auto& m, const auto& L, const Team& T) {
+  constexpr int NV = MT::nv, NB = MT::nbody;
+  const real* cdofw = T.w + L.cdof;
+  const real* cinert = T.w + L.cinert;
+  real qv[NV], cd[NV][6];
+  sfor<0, NV>(SLAM(dd) {
+    qv[SK(dd)] = T.w[L.qvel + SK(dd)];
+    sfor<0, 6>(SLAM(kk) { cd[SK(dd)][SK(kk)] = cdofw[6 * SK(dd) + SK(kk)]; });
+  });
+  // com velocities; cvb[d]: the cvel dof d sees (fwd_velocity's chain)
+  real cvel[NB][6], cvb[NV][6];
+  sfor<0, 6>(SLAM(kk) { cvel[0][SK(kk)] = 0; });
+  sfor<1, NB>(SLAM(ii) {
+    constexpr int i = SK(ii);
+    constexpr int pid = MT::body_parentid[i], bda = MT::body_dofadr[i], nd = MT::body_dofnum[i];
+    sfor<0, 6>(SLAM(kk) {
+      constexpr int k = SK(kk);
+      real cv = cvel[pid][k];
+      sfor<0, nd>(SLAM(jj) {
+        constexpr int d = bda + SK(jj);
+        cvb[d][k] = cv;
+        real t = 0;
+        t += cd[d][k] * qv[d];
+        cv += t;
+      });
+      cvel[i][k] = cv;
+    });
+  });
+  // cdof_dot
+  real cdd[NV][6];
+  sfor<0, NV>(SLAM(dd) { cross_motion(cdd[SK(dd)], cvb[SK(dd)], cd[SK(dd)]); });
+  // RNE: per-body dof terms, cacc down the tree
+  real cacc[NB][6];
+  cacc[0][0] = cacc[0][1] = cacc[0][2] = 0.0;
+  cacc[0][3] = -m.opt_gravity0;
+  cacc[0][4] = -m.opt_gravity1;
+  cacc[0][5] = -m.opt_gravity2;
+  sfor<1, NB>(SLAM(ii) {
+    constexpr int i = SK(ii);
+    constexpr int pid = MT::body_parentid[i], bda = MT::body_dofadr[i], nd = MT::body_dofnum[i];
+    sfor<0, 6>(SLAM(kk) {
+      constexpr int k = SK(kk);
+      real sum = 0;
+      sfor<0, nd>(SLAM(jj) { sum += cdd[bda + SK(jj)][k] * qv[bda + SK(jj)]; });
+      const real rt = nd ? sum : 0;
+      cacc[i][k] = cacc[pid][k] + rt;
+    });
+  });
+  // cfrc per body, subtree sums
+  real cf[NB][6];
+  sfor<1, NB>(SLAM(ii) {
+    constexpr int i = SK(ii);
+    real ci[10], f[6], tmp[6], tmp1[6];
+    sfor<0, 10>(SLAM(kk) { ci[SK(kk)] = cinert[10 * i + SK(kk)]; });
+    mul_inert_vec(f, ci, cacc[i]);
+    mul_inert_vec(tmp, ci, cvel[i]);
+    cross_force(tmp1, cvel[i], tmp);
+    sfor<0, 6>(SLAM(kk) { cf[i][SK(kk)] = f[SK(kk)] + tmp1[SK(kk)]; });
+  });
+  sfor<0, NB - 1>(SLAM(ii) {
+    constexpr int i = NB - 1 - SK(ii);
+    constexpr int p = MT::body_parentid[i];
+    if constexpr (p != 0) sfor<0, 6>(SLAM(kk) { cf[p][SK(kk)] += cf[i][SK(kk)]; });
+  });
+  // qfrc_bias[d] = tdot(cdof_d, cfrc_body(d)) on lane d
+  real b = 0;
+  sfor<0, NV>(SLAM(dd) {
+    constexpr int d = SK(dd);
+    constexpr int bi = MT::dof_bodyid[d];
+    real r = 0;
+    sfor<0, 6>(SLAM(kk) { r += cd[d][SK(kk)] * cf[bi][SK(kk)]; });
+    b = T.tid == d ? r : b;
+  });
+  if (T.tid < NV) T.w[L.qfrc_bias + T.tid] = b;
+  TSYNC();
+}
+
 // -------------------------------------------------- acceleration stage ---
 // act_pre: actuator_force() already ran (two-wave rollout: on the helper wave)
 __device__ inline void fwd_acceleration(const auto& m, const auto& L, const auto& X, const Team& T,
@@ -1677,6 +1928,74 @@ __device__ inline void fwd_acceleration(const auto& m, const auto& L, const auto
 }
 
 // s0 + v[lane 0] + v[lane 1] + ... + v[lane n-1], in that order
+// fwd_acceleration(act_pre = true) for a compile-time model with the dof
+// ancestor masks compiled in (the rollout's primary chain), in wave-uniform
+// registers: qfrc_smooth's rows and the tree L'DL solve of qacc_smooth
+// (solve_ld_rows' sequence, as euler_finish_u runs it) with one LDS read
+// phase and one write.  Returns false, having done nothing, when a body
+// carries xfrc_applied (the general path forms those Jacobian columns).
+template <class MT>
+__device__ inline bool fwd_acceleration_u(const auto& m, const auto& L, const auto& X, const Team& T) {
+  constexpr int NV = MT::nv, NB = MT::nbody;
+  using XT = std::remove_cvref_t<decltype(X)>;
+  (void)X;
+  const real* xf = T.w + L.xfrc_applied;
+  static_assert(6 * NB <= TEAM_SIZE, "one ballot over xfrc_applied");
+  if (__ballot(T.tid >= 6 && T.tid < 6 * NB && xf[T.tid] != 0) != 0ull) return false;
+  const real *qp = T.w + L.qfrc_passive, *qb = T.w + L.qfrc_bias, *qap = T.w + L.qfrc_applied;
+  const real* qa = T.w + L.qfrc_act;
+  const real *LD = T.w + L.qLD, *LDinv = T.w + L.qLDinv;
+  real v[NV], x[NV], dinv[NV], LDr[NV][NV];
+  sfor<0, NV>(SLAM(jj) {
+    constexpr int j = SK(jj);
+    real t = qp[j] - qb[j];
+    t += qap[j];
+    t += qa[j];
+    v[j] = t;
+    x[j] = t;
+    dinv[j] = LDinv[j];
+  });
+  sfor<0, NV>(SLAM(ii) {
+    constexpr int i = SK(ii);
+    sfor<0, i>(SLAM(jj) {
+      constexpr int j = SK(jj);
+      if constexpr ((XT::pmask[i] >> j) & 1) LDr[i][j] = LD[i * NV + j];
+    });
+  });
+  // x[j] -= LD[i][j] x[i] for j in anc(i), i descending, where x[i] != 0
+  sfor<0, NV>(SLAM(ii) {
+    constexpr int i = NV - 1 - SK(ii);
+    const bool nz = x[i] != 0;
+    sfor<0, i>(SLAM(jj) {
+      constexpr int j = SK(jj);
+      if constexpr ((XT::pmask[i] >> j) & 1) {
+        const real u = x[j] - LDr[i][j] * x[i];
+        x[j] = nz ? u : x[j];
+      }
+    });
+  });
+  sfor<0, NV>(SLAM(ii) { x[SK(ii)] *= dinv[SK(ii)]; });
+  // x[i] -= LD[i][j] x[j] for j in anc(i) descending, i ascending
+  sfor<0, NV>(SLAM(ii) {
+    constexpr int i = SK(ii);
+    sfor<0, i>(SLAM(jj) {
+      constexpr int j = i - 1 - SK(jj);
+      if constexpr ((XT::pmask[i] >> j) & 1) x[i] -= LDr[i][j] * x[j];
+    });
+  });
+  real vv = v[0], xv = x[0];
+  sfor<1, NV>(SLAM(ii) {
+    vv = T.tid == SK(ii) ? v[SK(ii)] : vv;
+    xv = T.tid == SK(ii) ? x[SK(ii)] : xv;
+  });
+  if (T.tid < NV) {
+    T.w[L.qfrc_smooth + T.tid] = vv;
+    T.w[L.qacc_smooth + T.tid] = xv;
+  }
+  TSYNC();
+  return true;
+}
+
 __device__ __forceinline__ real lane_sum(real s0, real v, int n) {
   for (int i = 0; i < n; i++) s0 += bcast(v, i);
   return s0;
@@ -3265,7 +3584,7 @@ __device__ inline void factor_m_and_euler(const auto& m, const auto& L, const au
     factor_ld(m, X, T, qM, T.w + L.qLD, T.w + L.qLDinv, T.c + C.ftmp);
     return;
   }
-  if (!(nv <= RMAX && X.pmask)) {
+  if (!(nv <= RMAX && has_pmask(X))) {
     factor_ld(m, X, T, qM, T.w + L.qLD, T.w + L.qLDinv, T.c + C.ftmp);
     euler_prefactor(m, L, C, X, T);
     return;
@@ -3337,7 +3656,9 @@ __device__ inline void step_dual_split(const auto& m, const auto& L, const auto&
   STAMP(24);
   STAMPB(32);
   if (A) {
-    com_pos(m, L, T);
+    using MT = std::remove_cvref_t<decltype(m)>;
+    if constexpr (StaticModel<MT> && ILQG_COM_U) com_pos_u<MT>(m, L, T);
+    else com_pos(m, L, T);
     STAMP(1);
   } else if (B) {
     collision(m, L, C, X, T);
@@ -3348,7 +3669,9 @@ __device__ inline void step_dual_split(const auto& m, const auto& L, const auto&
   STAMPB(34);
   bool rows_done = false;
   if (A) {
-    crb(m, L, C, X, T);
+    using MT = std::remove_cvref_t<decltype(m)>;
+    if constexpr (StaticModel<MT> && ILQG_COM_U) crb_u<MT>(m, L, C, X, T);
+    else crb(m, L, C, X, T);
     STAMP(2);
   } else if (B) {
     mc_contact_jac(m, L, X, T);
@@ -3369,7 +3692,9 @@ __device__ inline void step_dual_split(const auto& m, const auto& L, const auto&
   const int ne5 = T.iw[L.nefc];
   const bool spec = ne5 > 0 && ne5 <= TEAM_SIZE && m.nv <= RMAX;
   if (A) {
-    fwd_velocity(m, L, C, T, 1);
+    using MT = std::remove_cvref_t<decltype(m)>;
+    if constexpr (vel_regs_ok<MT>()) fwd_velocity_u<MT>(m, L, T);
+    else fwd_velocity(m, L, C, T, 1);
     STAMP(6);
   } else if (B) {
     if (!rows_done) {
@@ -3388,7 +3713,10 @@ __device__ inline void step_dual_split(const auto& m, const auto& L, const auto&
   STAMP(27);
   STAMPB(39);
   if (A) {
-    fwd_acceleration(m, L, X, T, true);
+    using MT = std::remove_cvref_t<decltype(m)>;
+    bool acc_done = false;
+    if constexpr (vel_regs_ok<MT>() && euler_regs_ok<MT>()) acc_done = fwd_acceleration_u<MT>(m, L, X, T);
+    if (!acc_done) fwd_acceleration(m, L, X, T, true);
     STAMP(7);
     if (spec) {
       fwd_constraint_fast(m, L, C, X, T, m.opt_iterations, m.opt_tolerance, true);

@@ -188,7 +188,17 @@ struct CoopAux {
   const int* pair;   // 2*npair: geom pairs passing the static collision filters, oracle order
   int npair;
   const unsigned long long* pmask;  // nv: proper-ancestor bitmask of each dof (null if nv > 64)
+  // pmask != null, as a flag: a null test of pmask after stage_model points it
+  // into LDS makes this ROCm's backend emit an illegal is-shared compare
+  // (V_CMP_NE_U32_e32 0, src_shared_base) in the -DILQG_STAMPS build
+  int haspm;
 };
+// has_pmask(X): the generic aux's flag, or the static models' compile-time table
+template <class XT>
+__host__ __device__ __forceinline__ bool has_pmask(const XT& X) {
+  if constexpr (requires { X.haspm; }) return X.haspm != 0;
+  else return static_cast<bool>(X.pmask);
+}
 
 }  // namespace coop
 }  // namespace ilqg

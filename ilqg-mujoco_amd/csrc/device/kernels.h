@@ -82,7 +82,19 @@ struct FdFused {
   double mu;
   double *K, *k, *V, *v;
   RicFlags fl;
+  // ticket schedule (launch_fd_plan): slot -> FD item, null = identity; each
+  // FD item's duration in this launch (s_memrealtime ticks), null = not kept
+  const unsigned* order;
+  unsigned* dur;
 };
+// Plan the fused sweep's ticket order from the previous launch's per-item
+// durations (dur, all zero = no history: identity order).  Items of the first
+// p0 points keep their slots; then, point-major, every (seed, point) with an
+// item longer than kthr x the mean duration: its centre team and its long
+// column teams; then the rest in identity order.  Every column team still
+// follows its centre team, so the deadlock argument is unchanged.
+hipError_t launch_fd_plan(int S, int P, int ntm, int p0, float kthr, const unsigned* dur, unsigned* order,
+                          hipStream_t st);
 
 }  // namespace ilqg
 

@@ -214,6 +214,9 @@ __device__ inline unsigned long long hw_where() {
 #endif
 __device__ inline void fd_fused_body(const auto& m, const auto& L, const auto& C, const auto& X, const Team& T,
                                      const FdFused& a, unsigned u) {
+  // the planned schedule (launch_fd_plan); readfirstlane: the item stays wave-uniform (SGPR)
+  if (a.order) u = __builtin_amdgcn_readfirstlane(a.order[u]);
+  const unsigned long long tstart = __builtin_amdgcn_s_memrealtime();
   STAMP_INIT();
 #ifdef ILQG_STAMPS
   const unsigned long long tteam_ = __builtin_amdgcn_s_memtime();
@@ -340,6 +343,7 @@ __device__ inline void fd_fused_body(const auto& m, const auto& L, const auto& C
   drain_stores();
   TSYNC();
   if (tid == 0) signal_add(done);
+  if (a.dur && tid == 0) a.dur[u] = (unsigned)(__builtin_amdgcn_s_memrealtime() - tstart);
 #ifdef ILQG_STAMPS
   if (tid == 0 && u < (unsigned)TL_N) g_tl[3 * u + 1] = __builtin_amdgcn_s_memrealtime();
   if (tid == 0) atomicMax(&g_fused_diag[4], __builtin_amdgcn_s_memtime());
@@ -409,7 +413,94 @@ __global__ __launch_bounds__(TEAM, FD_WAVES_PER_EU) void k_fd_fused_g(DevModel m
   fd_fused_body(m, L, C, X, T, a, t - a.nB);
 }
 
+// ---- the fused sweep's ticket schedule (launch_fd_plan) -----------------
+// One 1024-thread workgroup.  Items: centre C(s,p) = p S + s (u < S P), column
+// w of (s,p) = S P + (p S + s) ntm + w (fd_decode's identity order).  Groups g =
+// p S + s with p >= p0 are dealt to threads in contiguous runs of G_RUN; three
+// exclusive scans over the groups place section B (long groups: centre + long
+// columns), section C1 (the other centres) and C2 (the other columns).
+constexpr int PLAN_T = 1024;
+__device__ inline unsigned block_excl_scan(unsigned v, unsigned* sh, unsigned& total) {
+  const int t = threadIdx.x;
+  sh[t] = v;
+  __syncthreads();
+  for (int off = 1; off < PLAN_T; off <<= 1) {
+    const unsigned x = t >= off ? sh[t - off] : 0u;
+    __syncthreads();
+    sh[t] += x;
+    __syncthreads();
+  }
+  total = sh[PLAN_T - 1];
+  const unsigned incl = sh[t];
+  __syncthreads();
+  return incl - v;
+}
+
+__global__ __launch_bounds__(PLAN_T) void k_fd_plan(int S, int P, int ntm, int p0, float kthr, const unsigned* dur,
+                                                    unsigned* order) {
+  __shared__ unsigned sh[PLAN_T];
+  __shared__ unsigned long long sum_sh;
+  const int t = threadIdx.x;
+  const unsigned nC = (unsigned)S * P, nI = nC * (1 + ntm);
+  if (p0 > P) p0 = P;
+  if (t == 0) sum_sh = 0;
+  __syncthreads();
+  unsigned long long part = 0;
+  for (unsigned u = t; u < nI; u += PLAN_T) part += dur[u];
+  atomicAdd(&sum_sh, part);
+  __syncthreads();
+  const unsigned long long sum = sum_sh;
+  if (sum == 0) {  // no history: identity
+    for (unsigned u = t; u < nI; u += PLAN_T) order[u] = u;
+    return;
+  }
+  const double thr = (double)kthr * (double)sum / (double)nI;
+  // section A: the first p0 points keep their identity slots
+  const unsigned nA_c = (unsigned)p0 * S, nA_w = nA_c * ntm;
+  for (unsigned u = t; u < nA_c; u += PLAN_T) order[u] = u;
+  for (unsigned j = t; j < nA_w; j += PLAN_T) order[nA_c + j] = nC + j;
+  // groups g0 .. nC-1, G_RUN consecutive per thread
+  const unsigned g0 = nA_c, ng = nC - g0, run = (ng + PLAN_T - 1) / PLAN_T;
+  const unsigned ga = g0 + min(ng, t * run), gb = g0 + min(ng, (t + 1) * run);
+  auto is_long = [&](unsigned u) { return (double)dur[u] > thr; };
+  auto col = [&](unsigned g, int w) { return nC + g * ntm + (unsigned)w; };
+  unsigned cB = 0, cC1 = 0, cC2 = 0;
+  for (unsigned g = ga; g < gb; g++) {
+    int nl = 0;
+    for (int w = 0; w < ntm; w++) nl += is_long(col(g, w));
+    const bool lg = nl > 0 || is_long(g);
+    cB += lg ? 1 + nl : 0;
+    cC1 += lg ? 0 : 1;
+    cC2 += ntm - nl;
+  }
+  unsigned tB, tC1, tC2;
+  unsigned oB = block_excl_scan(cB, sh, tB);
+  unsigned oC1 = block_excl_scan(cC1, sh, tC1);
+  unsigned oC2 = block_excl_scan(cC2, sh, tC2);
+  const unsigned baseB = nA_c + nA_w, baseC1 = baseB + tB, baseC2 = baseC1 + tC1;
+  for (unsigned g = ga; g < gb; g++) {
+    int nl = 0;
+    for (int w = 0; w < ntm; w++) nl += is_long(col(g, w));
+    const bool lg = nl > 0 || is_long(g);
+    if (lg) {
+      order[baseB + oB++] = g;
+      for (int w = 0; w < ntm; w++)
+        if (is_long(col(g, w))) order[baseB + oB++] = col(g, w);
+    } else {
+      order[baseC1 + oC1++] = g;
+    }
+    for (int w = 0; w < ntm; w++)
+      if (!is_long(col(g, w))) order[baseC2 + oC2++] = col(g, w);
+  }
+}
+
 }  // namespace
+
+hipError_t launch_fd_plan(int S, int P, int ntm, int p0, float kthr, const unsigned* dur, unsigned* order,
+                          hipStream_t st) {
+  hipLaunchKernelGGL(k_fd_plan, dim3(1), dim3(PLAN_T), 0, st, S, P, ntm, p0, kthr, dur, order);
+  return hipGetLastError();
+}
 
 size_t coop_lds_bytes(const WsLayout& L, const CoopLayout& C) {
   return (size_t)(L.nd + C.nd + C.imgd) * sizeof(double) + (size_t)(L.ni + C.ni) * sizeof(int);

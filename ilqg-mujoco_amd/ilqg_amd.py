@@ -62,7 +62,7 @@ EXPORTS = [
     "ilqg_forward", "ilqg_fd_sweep", "ilqg_backward", "ilqg_iterate", "ilqg_synchronize",
     "ilqg_solver_stream", "ilqg_solver_device_costs", "ilqg_solver_set_stream", "ilqg_solver_set_timing",
     "ilqg_solver_get_timing",
-    "ilqg_solver_debug_set_fault", "ilqg_solver_device_traj", "ilqg_solver_set_layout", "ilqg_solver_set_value",
+    "ilqg_solver_debug_set_fault", "ilqg_solver_device_traj", "ilqg_solver_set_layout", "ilqg_solver_set_value", "ilqg_solver_debug_plan",
     "ilqg_solver_set_riccati", "ilqg_selftest_div", "ilqg_solver_set_fd_precision",
 ]
 KERNELS = ("rollout", "select", "fd_centre", "fd_cols", "backward", "fd_backward")

@@ -144,6 +144,10 @@ int ilqg_iterate(ilqg_solver* s);   /* forwardPass; setDInit(dArray[N]); backwar
 int ilqg_synchronize(ilqg_solver* s);
 /* test hook: preset the fault report word that ilqg_synchronize reads */
 int ilqg_solver_debug_set_fault(ilqg_solver* s, unsigned value);
+/* test hook: run the fused sweep's ticket planner on the durations the last
+   sweep recorded and copy out the schedule (slot -> FD item) and the
+   durations; nitems = the sweep's FD item count (0: no fused sweep) */
+int ilqg_solver_debug_plan(ilqg_solver* s, unsigned* order, unsigned* dur, int* nitems);
 void* ilqg_solver_stream(ilqg_solver* s); /* hipStream_t */
 /* enqueue subsequent hot-path launches on an external stream (hipStream_t,
    e.g. torch's current stream) instead of the solver's own; NULL restores it */

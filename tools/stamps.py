@@ -50,8 +50,14 @@ for what, fn, rd, rls in (("rollout (1 seed)", g.forward_pass, L.ilqg_debug_stam
     # the barrier waits
     tot = sum(acc[i] for i in list(range(11)) + list(range(11, 24)) + list(range(24, 30)))
     ms = sum(v[0] for v in tm.values())
-    print(f"== {what}: block 0, lane 0, total {tot} ticks (wave-0 stages + barriers); kernel time {ms:.3f} ms "
-          f"-> {tot / (ms * 1e3):.0f} ticks/us if the stages were all of it")
+    if what == "fd sweep":
+        # kernels_fd.hip stamps every 2^ILQG_STAMP_SAMPLE-th workgroup (a sample of
+        # every team role): totals are sums over those teams, cycles/call per call
+        print(f"== {what}: lane 0 of every 64th workgroup (ILQG_STAMP_SAMPLE 6), {tot} ticks summed over the "
+              f"sampled teams; kernel time {ms:.3f} ms; cycles/call are per call of a sampled team")
+    else:
+        print(f"== {what}: block 0, lane 0, total {tot} ticks (wave-0 stages + barriers); kernel time {ms:.3f} ms "
+              f"-> {tot / (ms * 1e3):.0f} ticks/us if the stages were all of it")
     if acc[45]:
         print(f"   Newton (all workgroups): {acc[45]} solves, {acc[44]} iterations, "
               f"{acc[44] / acc[45]:.2f} iterations per solve")
