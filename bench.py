@@ -104,6 +104,7 @@ def cpu_baseline(budget_s, horizon, threads, nalpha, model="hopper", cost=None):
     with open(cost_path, "w") as f:
         json.dump({k: list(v) for k, v in cost.packed(m.nq, m.nv, m.nu).items()}, f)
     state = "cfg-3 state" if model == "hopper" else "cfg-5 state: qpos0, root z = 1.4"
+    state_arg = "cfg3" if model == "hopper" else "cfg5"
     script = os.path.join(ROOT, "oracle", "cpu_bench.py")
     allc = sorted(os.sched_getaffinity(0))
     cores = allc[:threads]
@@ -111,12 +112,13 @@ def cpu_baseline(budget_s, horizon, threads, nalpha, model="hopper", cost=None):
     def pinned(cs):
         return lambda: os.sched_setaffinity(0, cs)
     try:
-        out = subprocess.run([sys.executable, script, "faithful", blob_path, cost_path, str(horizon), str(budget_s)],
+        out = subprocess.run([sys.executable, script, "faithful", blob_path, cost_path, str(horizon), str(budget_s),
+                              state_arg],
                              capture_output=True, text=True, preexec_fn=pinned(cores), timeout=budget_s * 4 + 120)
         ref = json.loads(out.stdout.strip().splitlines()[-1])
         tb = max(3.0, budget_s / 3)
         procs = [subprocess.Popen([sys.executable, script, "tuned", blob_path, cost_path, str(horizon), str(tb),
-                                   str(i), str(nalpha)], stdout=subprocess.PIPE, text=True,
+                                   state_arg, str(i), str(nalpha)], stdout=subprocess.PIPE, text=True,
                                   preexec_fn=pinned([c])) for i, c in enumerate(cores)]
         tuned = [json.loads(p.communicate(timeout=tb * 4 + 120)[0].strip().splitlines()[-1]) for p in procs]
     finally:
@@ -169,6 +171,30 @@ def cpu_baseline(budget_s, horizon, threads, nalpha, model="hopper", cost=None):
                           "runs 16 pinned processes; host_extrapolated = per_core x host_physical_cores is a linear "
                           "extrapolation to every physical core, not a measurement")},
     }
+
+
+def visible_gpus():
+    """GPUs this process may use, counted without initialising HIP: the KFD
+    topology's GPU nodes (nodes with a nonzero simd_count), narrowed by
+    HIP_VISIBLE_DEVICES / ROCR_VISIBLE_DEVICES; None if the topology is absent
+    (each rank then checks its own LOCAL_RANK when it binds its device)."""
+    import glob
+    n = 0
+    for f in glob.glob("/sys/class/kfd/kfd/topology/nodes/*/properties"):
+        try:
+            with open(f) as fh:
+                props = dict(line.split() for line in fh if len(line.split()) == 2)
+        except OSError:
+            continue
+        if int(props.get("simd_count", "0")) > 0:
+            n += 1
+    if n == 0:
+        return None
+    for var in ("HIP_VISIBLE_DEVICES", "ROCR_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES"):
+        v = os.environ.get(var)
+        if v is not None:
+            n = min(n, len([x for x in v.split(",") if x.strip() != ""]))
+    return n
 
 
 def _free_port():
@@ -331,8 +357,10 @@ def main():
     args = ap.parse_args(argv)
 
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
-        if not args.dry_run and torch.cuda.device_count() < args.gpus:  # counting does not initialise HIP
-            sys.exit(f"bench.py: --gpus {args.gpus} but {torch.cuda.device_count()} GPUs visible")
+        # count the devices without touching HIP in this parent (ranks are fresh children)
+        nvis = visible_gpus()
+        if not args.dry_run and nvis is not None and nvis < args.gpus:
+            sys.exit(f"bench.py: --gpus {args.gpus} but {nvis} GPUs visible")
         sys.exit(launch_ranks(args.gpus, argv))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     if world != args.gpus:

@@ -809,7 +809,7 @@ __device__ inline void com_pos(const auto& m, const auto& L, const Team& T) {
 }
 
 #ifndef ILQG_COM_U
-#define ILQG_COM_U 0
+#define ILQG_COM_U 1
 #endif
 // com_pos for a compile-time model on one wave with the subtree centres of
 // mass in wave-uniform registers (the rollout's primary chain): every lane
@@ -1760,7 +1760,7 @@ __device__ inline void fwd_velocity(const auto& m, const auto& L, const auto& C,
 }
 
 #ifndef ILQG_VEL_U
-#define ILQG_VEL_U 0
+#define ILQG_VEL_U 1
 #endif
 // fwd_velocity's part 1 (com velocities, cdof_dot, RNE -> qfrc_bias) for a
 // compile-time model whose joints are all hinges and slides, in wave-uniform
@@ -2885,7 +2885,14 @@ __device__ inline real linesearch_rows(int ne, real g1, real g2, real jr, real j
 }
 
 // fwd_constraint + solver_newton for a compile-time nv <= RMAX and nefc <= 64
-// (dual: the rollout's primary wave, whose helper ran newton_warm_prep)
+// (dual: the rollout's primary wave, whose helper ran newton_warm_prep).
+// Workspace contract: the outputs are qacc, the warm start and the rows'
+// jar; unlike fwd_constraint_fast / fwd_constraint, this solver keeps the
+// constraint forces and states in registers and does NOT write efc_force,
+// efc_state, efc_b or qfrc_constraint back to LDS -- those fields are stale
+// after a compile-time-model solve (nothing reads them after the solve today;
+// a future consumer such as a contact-force cost or sensor must add the
+// write-back).
 template <int NV>
 __device__ inline void fwd_constraint_u(const auto& m, const auto& L, const auto& C, const Team& T, int maxiter,
                                         real tol, bool dual) {

@@ -39,6 +39,17 @@ constexpr unsigned HANDOFF_SPIN_LIMIT = 1u << 22;
 // cycles, [1] of which waiting for records, [2] waits that polled more than
 // once, [3] role-0 start, [4] latest FD team end, [5] role-0 end, [8 + s] role s cycles
 __device__ unsigned long long g_fused_diag[24];
+// per-step completion time (s_memrealtime) of the backward roles of seeds
+// 0..7 inside the fused sweep: [s * 512 + n] for step n < 512
+__device__ unsigned long long g_bstep[8 * 512];
+#define BSTEP_LOG(s, n)                                                                   \
+  do {                                                                                     \
+    if (done && tid == 0 && (s) < 8 && (n) < 512) g_bstep[(s) * 512 + (n)] = __builtin_amdgcn_s_memrealtime(); \
+  } while (0)
+#else
+#define BSTEP_LOG(s, n) \
+  do {                  \
+  } while (0)
 #endif
 
 __device__ __forceinline__ double ld_sc1(const double* p) {

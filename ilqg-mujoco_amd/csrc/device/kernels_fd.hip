@@ -598,10 +598,15 @@ extern "C" int ilqg_debug_timeline(unsigned long long* out, int reset) {
   if (hipMemcpyFromSymbol(out + 3 * ilqg::TL_N, HIP_SYMBOL(ilqg::g_tlb), sizeof(unsigned long long) * 128) !=
       hipSuccess)
     return 3;
+  // then the backward roles' per-step completion times (handoff.h g_bstep)
+  if (hipMemcpyFromSymbol(out + 3 * ilqg::TL_N + 128, HIP_SYMBOL(ilqg::g_bstep), sizeof(unsigned long long) * 8 * 512) !=
+      hipSuccess)
+    return 3;
   if (reset) {
     static unsigned long long z[3 * ilqg::TL_N];
     (void)hipMemcpyToSymbol(HIP_SYMBOL(ilqg::g_tl), z, sizeof(z));
     (void)hipMemcpyToSymbol(HIP_SYMBOL(ilqg::g_tlb), z, sizeof(unsigned long long) * 128);
+    (void)hipMemcpyToSymbol(HIP_SYMBOL(ilqg::g_bstep), z, sizeof(unsigned long long) * 8 * 512);
   }
   return 0;
 }

@@ -523,6 +523,7 @@ __device__ inline void backward_seed_reg(const MD& m, int P, double dt, double m
     xb = xn;
     wsync();
     BSTAMP(6);
+    BSTEP_LOG(s, n);
   }
   const double* vfin = Vv + ((P - 1) & 1) * NX;
   if (P == 1) vfin = Vv;

@@ -43,7 +43,7 @@ def normals(seed, n):
     return _n(seed, n)
 
 
-def setup(blob_path, cost_path, lib, seed):
+def setup(blob_path, cost_path, lib, seed, state):
     with open(blob_path, "rb") as f:
         blob = f.read()
     om = ora.OModel(blob, lib)
@@ -57,10 +57,13 @@ def setup(blob_path, cost_path, lib, seed):
             arr[i] = x
     lib.L.ora_set_cost_desc(desc)
     d = om.make_data()
-    if om.nq != om.nv:
+    if state == "cfg5":
         # cfg 5 (humanoid): qpos0 with the root at z = 1.4 (humanoid.xml:49-50), qvel 0
+        # (one state: a humanoid leg has no per-seed perturbation)
         d.arr("qpos")[2] = 1.4
         return om, d
+    if state != "cfg3":
+        raise ValueError(f"unknown state {state!r} (cfg3 | cfg5)")
     # cfg 3 state (tst/test_derivatives.cpp:38-47) + cfg 4's per-seed perturbation
     d.step(500)
     d.arr("ctrl")[:] -= 0.1
@@ -71,10 +74,10 @@ def setup(blob_path, cost_path, lib, seed):
     return om, d
 
 
-def faithful(blob, cost, H, budget, seed=-1):
+def faithful(blob, cost, H, budget, state, seed=-1):
     kind = "reference" if os.path.exists(ora.REF_SO) else "port"
     lib = ora.ref_lib() if kind == "reference" else ora.oracle_lib()
-    om, d = setup(blob, cost, lib, seed)
+    om, d = setup(blob, cost, lib, seed, state)
     lib.L.ora_set_nthread(0)  # omp_get_num_procs(), capped at 16 (mjderivative.cpp:32,217)
     il = ora.OILQR(om, d, H, cost_fn="ora_cost_desc_fn", use_ref_fd=(kind == "reference"))
     il.set_dinit(d)
@@ -91,9 +94,9 @@ def faithful(blob, cost, H, budget, seed=-1):
                 threads=lib.L.ora_get_nthread(), nproc=os.cpu_count(), cores=len(os.sched_getaffinity(0)))
 
 
-def tuned(blob, cost, H, budget, seed, nalpha):
+def tuned(blob, cost, H, budget, state, seed, nalpha):
     lib = ora.oracle_lib()
-    om, d = setup(blob, cost, lib, seed)
+    om, d = setup(blob, cost, lib, seed, state)
     lib.L.ora_set_nthread(1)
     alphas = [2.0 ** -i for i in range(nalpha)]
     il = ora.OILQR(om, d, H, cost_fn="ora_cost_desc_fn")
@@ -116,9 +119,11 @@ def tuned(blob, cost, H, budget, seed, nalpha):
 
 
 if __name__ == "__main__":
-    mode, blob, cost, H, budget = sys.argv[1], sys.argv[2], sys.argv[3], int(sys.argv[4]), float(sys.argv[5])
+    # cpu_bench.py faithful|tuned BLOB COST H BUDGET STATE(cfg3|cfg5) [SEED [NALPHA]]
+    mode, blob, cost, H, budget, state = (sys.argv[1], sys.argv[2], sys.argv[3], int(sys.argv[4]),
+                                          float(sys.argv[5]), sys.argv[6])
     if mode == "faithful":
-        out = faithful(blob, cost, H, budget, int(sys.argv[6]) if len(sys.argv) > 6 else -1)
+        out = faithful(blob, cost, H, budget, state, int(sys.argv[7]) if len(sys.argv) > 7 else -1)
     else:
-        out = tuned(blob, cost, H, budget, int(sys.argv[6]), int(sys.argv[7]))
+        out = tuned(blob, cost, H, budget, state, int(sys.argv[7]), int(sys.argv[8]))
     print(json.dumps(out), flush=True)

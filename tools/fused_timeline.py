@@ -15,7 +15,7 @@ import workloads  # noqa: E402
 
 TL_N = 65536
 L = ia.lib()
-buf = (ctypes.c_ulonglong * (3 * TL_N + 128))()
+buf = (ctypes.c_ulonglong * (3 * TL_N + 128 + 8 * 512))()
 S = int(sys.argv[1]) if len(sys.argv) > 1 else 8
 m = ia.Model.load(workloads.model_file("hopper"))
 g = ia.ILQR(m, workloads.hopper_dmain(m, S, sigma=0.01), 500, ia.HOPPER_COST,
@@ -34,7 +34,8 @@ nv, nu, P = m.nv, m.nu, 501
 ntm = nu + 2 * nv
 n_items = S * P * (1 + ntm)
 tl = a[: 3 * TL_N].reshape(TL_N, 3)[:n_items]
-tb = a[3 * TL_N:].reshape(64, 2)[:S].astype(np.int64)
+tb = a[3 * TL_N:3 * TL_N + 128].reshape(64, 2)[:S].astype(np.int64)
+bstep = a[3 * TL_N + 128:].reshape(8, 512).astype(np.int64)
 st, en, hw = tl[:, 0].astype(np.int64), tl[:, 1].astype(np.int64), tl[:, 2]
 ok = (st > 0) & (en > 0)
 print(f"S={S}: fused launch {t['fd_backward'][0]:.3f} ms (HIP events); items {n_items}, recorded {ok.sum()}")
@@ -74,6 +75,23 @@ for p in range(P):
     pts.append(us(en[idx].max()))
 pts = np.array(pts)
 print("  seed 0 record complete (us) at points 0,50,...: " + " ".join(f"{pts[p]:.0f}" for p in range(0, P, 50)))
+# the recursion against its records (handoff.h g_bstep): step n of seed s needs
+# record n (and prefetches n + 1); lag = step done - that record complete
+for s_ in range(min(S, 8)):
+    ready = np.array([us(en[[p * S + s_] + [nC + p * S * ntm + s_ * ntm + k for k in range(ntm)]].max())
+                      for p in range(P)])
+    done = bstep[s_, 1:P]
+    if not np.all(done > 0):
+        continue
+    dn = us(done)
+    lag = dn - ready[1:P]
+    last_rec = ready.max()
+    behind = int((dn > last_rec).sum())
+    step_us = np.diff(dn)
+    print(f"  seed {s_} recursion: last record {last_rec:.0f} us, last step {dn[-1]:.0f} us "
+          f"({dn[-1] - last_rec:.0f} us after it, {behind} steps done after it); step time median "
+          f"{np.median(step_us):.2f} us, over the last 50 steps {np.mean(step_us[-50:]):.2f} us; "
+          f"lag behind its record: median {np.median(lag):.0f} us, max {lag.max():.0f} us")
 cu = hw[ok]
 xcc = (cu >> 32) & 0xF
 hwid = cu & 0xFFFFFFFF
