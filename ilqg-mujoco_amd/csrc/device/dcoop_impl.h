@@ -112,6 +112,10 @@ __shared__ unsigned long long s_stamp_acc[STAMP_N], s_stamp_cnt[STAMP_N], s_stam
 #endif
 // below this many dofs the small factorizations run on lane 0 (fewer LDS round trips)
 constexpr int SERIAL_NV = 12;
+// the Newton Hessian's Cholesky in row registers up to 32 dofs (cholesky_rows32)
+#ifndef ILQG_CHOL32
+#define ILQG_CHOL32 1
+#endif
 
 __device__ __forceinline__ real tdot(const real* a, const real* b, int n) {
   real r = 0;
@@ -1197,40 +1201,56 @@ __device__ inline void jac_col(const auto& m, const auto& X, const real* scom, c
   out3[2] = cd[5] + tmp[2];
 }
 
-__device__ inline void collision(const auto& m, const auto& L, const auto& C, const auto& X,
-                                 const Team& T) {
+// collision's narrow phase for pair p (its contacts into pcon, its count into
+// pcnt).  Always inlined: as an outlined call (flat pointer arguments) ROCm's
+// backend emits an illegal is-shared compare (V_CMP_NE_U32_e32 0, src_shared_base)
+__device__ __forceinline__ void collision_pair(const auto& m, const auto& L, const auto& C, const auto& X, const Team& T,
+                                      int p) {
   real* gxpos = T.w + L.gxpos;
   real* gxmat = T.w + L.gxmat;
+  real* pcon = T.w + L.pcon;
+  int* pcnt = T.ci + C.pcnt;
+  int g1 = X.pair[2 * p], g2 = X.pair[2 * p + 1];
+  int n = 0;
+  real margin = maxd(m.geom_margin[g1], m.geom_margin[g2]);
+  bool ok = true;
+  if (m.geom_rbound[g1] > 0 && m.geom_rbound[g2] > 0) {
+    real dd[3] = {gxpos[3 * g1] - gxpos[3 * g2], gxpos[3 * g1 + 1] - gxpos[3 * g2 + 1],
+                    gxpos[3 * g1 + 2] - gxpos[3 * g2 + 2]};
+    if (sqrt(dot3(dd, dd)) > m.geom_rbound[g1] + m.geom_rbound[g2] + margin) ok = false;
+  }
+  if (ok) {
+    int ga = g1, gb = g2;
+    if (m.geom_type[g1] > m.geom_type[g2]) { ga = g2; gb = g1; }
+    real pos1[3], mat1[9], sz1[3], pos2[3], mat2[9], sz2[3];
+    ldm<3>(pos1, gxpos + 3 * ga);
+    ldm<9>(mat1, gxmat + 9 * ga);
+    ldm<3>(sz1, m.geom_size + 3 * ga);
+    ldm<3>(pos2, gxpos + 3 * gb);
+    ldm<9>(mat2, gxmat + 9 * gb);
+    ldm<3>(sz2, m.geom_size + 3 * gb);
+    // contacts straight into the pair's LDS records
+    n = narrow(m, m.geom_type[ga], m.geom_type[gb], pos1, mat1, sz1, pos2, mat2, sz2, margin,
+               LdsConSinkT<real>{pcon + 14 * p});
+  }
+  pcnt[p] = n;
+}
+
+__device__ __forceinline__ void collision_finish(const auto& m, const auto& L, const auto& C, const auto& X,
+                                                const Team& T);
+__device__ inline void collision(const auto& m, const auto& L, const auto& C, const auto& X,
+                                 const Team& T) {
+  FOR_T(p, X.npair) collision_pair(m, L, C, X, T, p);
+  collision_finish(m, L, C, X, T);
+}
+
+// the ordered compaction and the contact records (after every pair's narrow phase)
+__device__ __forceinline__ void collision_finish(const auto& m, const auto& L, const auto& C, const auto& X,
+                                                const Team& T) {
   real* con = T.w + L.con;
   int* coni = T.iw + L.coni;
   real* pcon = T.w + L.pcon;
   int* pcnt = T.ci + C.pcnt;
-  FOR_T(p, X.npair) {
-    int g1 = X.pair[2 * p], g2 = X.pair[2 * p + 1];
-    int n = 0;
-    real margin = maxd(m.geom_margin[g1], m.geom_margin[g2]);
-    bool ok = true;
-    if (m.geom_rbound[g1] > 0 && m.geom_rbound[g2] > 0) {
-      real dd[3] = {gxpos[3 * g1] - gxpos[3 * g2], gxpos[3 * g1 + 1] - gxpos[3 * g2 + 1],
-                      gxpos[3 * g1 + 2] - gxpos[3 * g2 + 2]};
-      if (sqrt(dot3(dd, dd)) > m.geom_rbound[g1] + m.geom_rbound[g2] + margin) ok = false;
-    }
-    if (ok) {
-      int ga = g1, gb = g2;
-      if (m.geom_type[g1] > m.geom_type[g2]) { ga = g2; gb = g1; }
-      real pos1[3], mat1[9], sz1[3], pos2[3], mat2[9], sz2[3];
-      ldm<3>(pos1, gxpos + 3 * ga);
-      ldm<9>(mat1, gxmat + 9 * ga);
-      ldm<3>(sz1, m.geom_size + 3 * ga);
-      ldm<3>(pos2, gxpos + 3 * gb);
-      ldm<9>(mat2, gxmat + 9 * gb);
-      ldm<3>(sz2, m.geom_size + 3 * gb);
-      // contacts straight into the pair's LDS records
-      n = narrow(m, m.geom_type[ga], m.geom_type[gb], pos1, mat1, sz1, pos2, mat2, sz2, margin,
-                 LdsConSinkT<real>{pcon + 14 * p});
-    }
-    pcnt[p] = n;
-  }
   TSYNC();
   // ordered compaction with the oracle's truncation at nconmax
   const int lim = m.nconmax < m.maxcon ? m.nconmax : m.maxcon;
@@ -2082,8 +2102,16 @@ __device__ inline void hessian_factor(const auto& m, const auto& L, const auto& 
   // ascending order (as a ballot when nefc <= 64), inactive rows skipped as
   // the oracle skips them
   const int ntri = nv * (nv + 1) / 2;
-  const bool bal = ne <= 64 && T.nt == 64;
-  const unsigned long long am = bal ? __ballot(T.tid < ne && state[T.tid] != 0) : 0ull;
+  // the active set as ballots of 64 rows (up to HMASK of them, before the
+  // entry loop, with every lane active)
+  constexpr int HMASK = 4;
+  const bool bal = ne <= 64 * HMASK && T.nt == 64;
+  unsigned long long am[HMASK];
+#pragma unroll
+  for (int q = 0; q < HMASK; q++) {
+    const int i = 64 * q + T.tid;
+    am[q] = bal && 64 * q < ne ? __ballot(i < ne && state[i] != 0) : 0ull;
+  }
   FOR_T(e, ntri) {
     int r = (int)((sqrtf(8.0f * (float)e + 1.0f) - 1.0f) * 0.5f);
     while (r * (r + 1) / 2 > e) r--;
@@ -2091,25 +2119,28 @@ __device__ inline void hessian_factor(const auto& m, const auto& L, const auto& 
     const int c = e - r * (r + 1) / 2;
     real h = 0;
     if (bal) {
-      // four active rows' loads in flight at once, the terms added in row order
-      for (unsigned long long mm = am; mm;) {
-        int id[4];
-        real a[4], d[4], b[4];
+      // eight active rows' loads in flight at once, the terms added in row order
 #pragma unroll
-        for (int q = 0; q < 4; q++) {
-          id[q] = mm ? __builtin_ctzll(mm) : -1;
-          mm &= mm - 1;
+      for (int w = 0; w < HMASK; w++) {
+        for (unsigned long long mm = am[w]; mm;) {
+          int id[8];
+          real a[8], d[8], b[8];
+#pragma unroll
+          for (int q = 0; q < 8; q++) {
+            id[q] = mm ? 64 * w + __builtin_ctzll(mm) : -1;
+            mm &= mm - 1;
+          }
+#pragma unroll
+          for (int q = 0; q < 8; q++) {
+            const int i = id[q] < 0 ? id[0] : id[q];
+            a[q] = J[i * nv + r];
+            d[q] = D[i];
+            b[q] = J[i * nv + c];
+          }
+#pragma unroll
+          for (int q = 0; q < 8; q++)
+            if (id[q] >= 0) h += a[q] * d[q] * b[q];
         }
-#pragma unroll
-        for (int q = 0; q < 4; q++) {
-          const int i = id[q] < 0 ? id[0] : id[q];
-          a[q] = J[i * nv + r];
-          d[q] = D[i];
-          b[q] = J[i * nv + c];
-        }
-#pragma unroll
-        for (int q = 0; q < 4; q++)
-          if (id[q] >= 0) h += a[q] * d[q] * b[q];
       }
     } else {
       for (int i = 0; i < ne; i++)
@@ -2122,6 +2153,12 @@ __device__ inline void hessian_factor(const auto& m, const auto& L, const auto& 
     cholesky_rows(nv, T.tid, H);
     return;
   }
+#if ILQG_CHOL32
+  if (nv <= 32 && T.nt == TEAM_SIZE) {
+    cholesky_rows32(nv, T.tid, H);
+    return;
+  }
+#endif
   if (nv <= SERIAL_NV) {
     if (T.tid == 0) {
       for (int j = 0; j < nv; j++) {
@@ -3608,6 +3645,30 @@ __device__ inline void factor_m_and_euler(const auto& m, const auto& L, const au
   factor_ld_rows2(nv, X.pmask, T.tid, qM, T.w + L.qLD, T.w + L.qLDinv, qH, qHLD, qHinv);
 }
 
+#ifndef ILQG_COLL_SPLIT
+#define ILQG_COLL_SPLIT 1
+#endif
+// pairs (compile-time aux) with a plane geom: bit p
+template <class MT, class XT>
+constexpr unsigned long long plane_pair_mask() {
+  unsigned long long mk = 0;
+  for (int p = 0; p < XT::npair && p < 64; p++)
+    if (MT::geom_type[XT::pair[2 * p]] == GEOM_PLANE || MT::geom_type[XT::pair[2 * p + 1]] == GEOM_PLANE)
+      mk |= 1ull << p;
+  return mk;
+}
+template <class MT, class XT>
+constexpr bool coll_split_ok() {
+  if constexpr (StaticModel<MT> && ILQG_COLL_SPLIT) {
+    if constexpr (XT::npair > 0 && XT::npair <= 64) {
+      constexpr unsigned long long pm = plane_pair_mask<MT, XT>();
+      constexpr unsigned long long all = XT::npair == 64 ? ~0ull : (1ull << XT::npair) - 1;
+      return pm != 0 && pm != all;
+    }
+  }
+  return false;
+}
+
 // step_dual for the split layout (L.split: RNE / com-velocity / Euler scratch
 // outside the union) and register-row models, on a THREE-wave team (wave 0
 // the dependency chain, waves 1 and 2 helpers).  Work moves to where a helper
@@ -3624,7 +3685,7 @@ __device__ inline void factor_m_and_euler(const auto& m, const auto& L, const au
 //   phase 5: the primary's acceleration stage and constraint solve find the
 //     Newton warm start ready.
 __device__ inline void step_dual_split(const auto& m, const auto& L, const auto& C, const auto& X, const Team& T,
-                                       int wave, int sid, auto&& pre) {
+                                       int wave, int sid, auto&& pre, auto&& late) {
   const bool A = wave == 0, B = wave == 1;
   int* fq = T.ci + C.ibc + 6;  // quaternions final (primary -> frames helper)
   int* ff = T.ci + C.ibc + 7;  // frame rotations final (helper -> primary)
@@ -3633,7 +3694,10 @@ __device__ inline void step_dual_split(const auto& m, const auto& L, const auto&
   STAMPB(-1);
   const bool bad = any_bad(T, C, T.w + L.qpos, m.nq) || any_bad(T, C, T.w + L.qvel, m.nv);
   if (bad) {
-    if (B) pre();
+    if (B) {
+      pre();
+      late();
+    }
     __syncthreads();
     if (A) reset_data(m, L, T);
     __syncthreads();  // the helpers' phase-1 work reads the reset state
@@ -3667,9 +3731,28 @@ __device__ inline void step_dual_split(const auto& m, const auto& L, const auto&
     if constexpr (StaticModel<MT> && ILQG_COM_U) com_pos_u<MT>(m, L, T);
     else com_pos(m, L, T);
     STAMP(1);
-  } else if (B) {
-    collision(m, L, C, X, T);
-    STAMPB(33);
+  } else {
+    using MT = std::remove_cvref_t<decltype(m)>;
+    using XT = std::remove_cvref_t<decltype(X)>;
+    if constexpr (coll_split_ok<MT, XT>()) {
+      // the narrow phase split by pair kind over the two helpers (no divergent
+      // mix of kernels on one wave): wave 1 the pairs with a plane, wave 2 the
+      // rest; wave 2 hands its counts and candidates to wave 1, which compacts
+      int* fc = T.ci + C.ibc + 4;
+      constexpr unsigned long long pm = plane_pair_mask<MT, XT>();
+      const bool mine = T.tid < XT::npair && (((pm >> T.tid) & 1ull) != 0) == B;
+      if (mine) collision_pair(m, L, C, X, T, T.tid);
+      if (!B) {
+        wave_signal(fc, sid);
+      } else {
+        wave_wait(fc, sid);
+        collision_finish(m, L, C, X, T);
+        STAMPB(33);
+      }
+    } else if (B) {
+      collision(m, L, C, X, T);
+      STAMPB(33);
+    }
   }
   __syncthreads();
   STAMP(25);
@@ -3734,6 +3817,10 @@ __device__ inline void step_dual_split(const auto& m, const auto& L, const auto&
     STAMP(8);
   } else {
     __syncthreads();  // the primary's barrier inside its Newton start
+    // `late` (the caller's work after `pre` that no phase reads: parking the
+    // prefetched record) runs here, where wave 1 has slack, so its loads have
+    // landed long before
+    if (B && !bad) late();
     STAMPB(38);
   }
   __syncthreads();

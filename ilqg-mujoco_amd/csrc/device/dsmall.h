@@ -342,6 +342,44 @@ __device__ inline void cholesky_rows(int nv, int tid, R* H) {
   team_sync();
 }
 
+// The same Cholesky for RMAX < nv <= 32 (the humanoid, nv = 27) with run-time
+// nv: lane t keeps row t in registers for the whole factorization, row j is
+// broadcast entry by entry (v_readlane) as column j needs it, and the
+// diagonal's dot product is lane j's own row dot product -- the oracle's
+// tdot(H_j, H_j, j) and tdot(H_i, H_j, j), ascending from +0.  No LDS round
+// trip or barrier per column (the LDS form: one of each).
+template <class R>
+__device__ inline void cholesky_rows32(int nv, int tid, R* H) {
+  constexpr int NM = 32;
+  const bool own = tid < nv;
+  R r[NM];
+  sfor<0, NM>(SLAM(jj) {
+    constexpr int j = SK(jj);
+    r[j] = (own && j < nv && j <= tid) ? H[tid * nv + j] : (R)0.0;
+  });
+  sfor<0, NM>(SLAM(jc) {
+    constexpr int j = SK(jc);
+    if (j >= nv) return;
+    R s = 0;
+    sfor<0, j>(SLAM(qq) { s += r[SK(qq)] * bcast(r[SK(qq)], j); });
+    R t = r[j];
+    if (j) t -= s;
+    t = bcast(t, j);
+    if (t < MINVAL) t = MINVAL;
+    const R d = sqrt(t);
+    const R tinv = 1 / d;
+    if (tid == j) r[j] = d;
+    if (own && tid > j) r[j] = (r[j] - s) * tinv;
+  });
+  team_sync();
+  if (own) {
+    sfor<0, NM>(SLAM(jj) {
+      if (SK(jj) < nv && SK(jj) <= tid) H[tid * nv + SK(jj)] = r[SK(jj)];
+    });
+  }
+  team_sync();
+}
+
 // search = -(H H')^-1 grad with the Cholesky factor in H's lower triangle;
 // mirrors the lane-0 substitution in coop::solver_newton.
 template <class R>

@@ -144,7 +144,7 @@ __device__ inline void rollout_body(const auto& m, const auto& L, const auto& C,
   };
   if (wave >= 0) {
     // the step ids of the two-wave hand-off flags (step_dual_split) start above 0
-    if (threadIdx.x == 0) T.ci[C.ibc + 6] = T.ci[C.ibc + 7] = 0;
+    if (threadIdx.x == 0) T.ci[C.ibc + 4] = T.ci[C.ibc + 6] = T.ci[C.ibc + 7] = 0;
     __syncthreads();
   }
   for (int n = P - 1; n >= 0; n--) {
@@ -153,13 +153,16 @@ __device__ inline void rollout_body(const auto& m, const auto& L, const auto& C,
       step(m, L, C, X, T);
       park(n);
     } else {
-      auto pre = [&]() {
-        pre_step(n);
-        park(n);
-      };
-      // split layout (compile-time models): the rebalanced two-wave schedule
-      if constexpr (decltype(split)::value) step_dual_split(m, L, C, X, T, wave, P - n, pre);
-      else step_dual(m, L, C, X, T, wave, pre);
+      // split layout (compile-time models): the rebalanced three-wave
+      // schedule, which parks the record in a later phase
+      if constexpr (decltype(split)::value) {
+        step_dual_split(m, L, C, X, T, wave, P - n, [&]() { pre_step(n); }, [&]() { park(n); });
+      } else {
+        step_dual(m, L, C, X, T, wave, [&]() {
+          pre_step(n);
+          park(n);
+        });
+      }
     }
   }
   if (ctl && T.tid == 0 && cost_cand) cost_cand[lane] = c;
