@@ -850,8 +850,10 @@ static hipError_t fused_launch(ilqg_solver* s, const SeedRange& r, int mode) {
   a.V = s->V.as<double>() + s0 * nx * nx;
   a.v = s->v.as<double>() + s0 * nx;
   a.fl = s->flags();
-  // ticket schedule from the previous launch's item durations (ILQG_PLAN=0: identity)
-  if (s->plan_dur.p && getenv_int("ILQG_PLAN", 1)) {
+  // ticket schedule from the previous launch's item durations: opt-in
+  // (ILQG_PLAN=1); measured slower than the point-major order on the bench
+  // workload ("Fused sweep ticket schedule")
+  if (s->plan_dur.p && getenv_int("ILQG_PLAN", 0)) {
     static const float kthr = [] {
       const char* e = getenv("ILQG_PLAN_K");
       return e ? (float)atof(e) : 3.0f;

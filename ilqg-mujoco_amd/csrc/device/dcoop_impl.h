@@ -116,6 +116,11 @@ constexpr int SERIAL_NV = 12;
 #ifndef ILQG_CHOL32
 #define ILQG_CHOL32 1
 #endif
+// the Newton search-direction substitution for RMAX < nv <= 32: 0 chol_solve_wave,
+// 1 chol_solve_rows32 (solution in registers), 2 chol_solve_u2 (compile-time steps)
+#ifndef ILQG_CHOLS
+#define ILQG_CHOLS 2
+#endif
 
 __device__ __forceinline__ real tdot(const real* a, const real* b, int n) {
   real r = 0;
@@ -2149,6 +2154,7 @@ __device__ inline void hessian_factor(const auto& m, const auto& L, const auto& 
     H[r * nv + c] = qM[r * nv + c] + h;
   }
   TSYNC();
+  STAMP(31);
   if (nv <= RMAX) {
     cholesky_rows(nv, T.tid, H);
     return;
@@ -2493,6 +2499,10 @@ __device__ inline void solver_newton(const auto& m, const auto& L, const auto& C
     // search = -H^-1 grad ; line search ; all on lane 0 except the parallel products
     if (nv <= RMAX) {
       chol_solve_rows(nv, T.tid, H, grad, search);
+    } else if (ILQG_CHOLS == 1 && nv <= 32 && T.nt == TEAM_SIZE) {
+      chol_solve_rows32(nv, T.tid, H, grad, search);
+    } else if (ILQG_CHOLS == 2 && nv <= 32 && T.nt == TEAM_SIZE) {
+      chol_solve_u2(nv, T.tid, H, grad, search);
     } else if (nv <= TEAM_SIZE) {
       chol_solve_wave(nv, T.tid, H, grad, search);
     } else {

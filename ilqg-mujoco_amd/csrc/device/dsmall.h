@@ -442,6 +442,9 @@ __device__ __forceinline__ double div_ref_lane_rt(double a, double b, double r, 
   return q;
 }
 __device__ __forceinline__ float div_ref_lane_rt(float a, float b, float, int) { return a / b; }
+// a / b on every lane, b's reciprocal refined ahead (fp64) / plain (fp32)
+__device__ __forceinline__ double div_u(double a, double b, double r) { return div_ref(a, b, r); }
+__device__ __forceinline__ float div_u(float a, float b, float) { return a / b; }
 
 // The same substitution for RMAX < nv <= TEAM_SIZE (the humanoid, nv = 27),
 // with run-time loops: lane t holds row t's running dot product (forward) and
@@ -482,6 +485,102 @@ __device__ inline void chol_solve_wave(int nv, int tid, const R* H, const R* gra
   }
   team_sync();
   if (own) search[tid] = -sb;
+  team_sync();
+}
+
+// chol_solve_wave for RMAX < nv <= 32 with compile-time step indices: the same
+// lanes and operations (lane t: row t's running dot product, column t's
+// product in the backward pass), but every broadcast reads an immediate lane,
+// the next step's matrix entries are loaded a step ahead, and the divisor of
+// each backward step is broadcast from its lane with its reciprocal ready.
+// A handful of VGPRs: no per-row register arrays (register-light for the
+// large generic kernels).
+template <class R>
+__device__ inline void chol_solve_u2(int nv, int tid, const R* H, const R* grad, R* search) {
+  constexpr int NM = 32;
+  const bool own = tid < nv;
+  const R dg = own ? H[tid * nv + tid] : (R)1.0;
+  const R rg = rcp_ref(dg);
+  const R g = own ? grad[tid] : (R)0.0;
+  R acc = 0, sv = 0;
+  R h = own ? H[tid * nv] : (R)0.0;
+  sfor<0, NM>(SLAM(ii) {
+    constexpr int i = SK(ii);
+    if (i >= nv) return;
+    const R hn = (own && i + 1 < nv) ? H[tid * nv + i + 1] : (R)0.0;
+    const R a = bcast(i ? g - acc : g, i);
+    const R si = div_u(a, bcast(dg, i), bcast(rg, i));
+    sv = tid == i ? si : sv;
+    acc += h * si;
+    h = hn;
+  });
+  R sb = 0;
+  R hc = own ? H[tid * nv + nv - 1] : (R)0.0;
+  sfor<0, NM>(SLAM(kk) {
+    constexpr int i = NM - 1 - SK(kk);
+    if (i >= nv) return;
+    const R hcn = (own && i > 0) ? H[tid * nv + i - 1] : (R)0.0;
+    const R pr = (own && tid > i) ? hc * sb : (R)0.0;
+    R t = bcast(sv, i);
+    sfor<i + 1, NM>(SLAM(jj) {
+      constexpr int j = SK(jj);
+      if (j < nv) t -= bcast(pr, j);
+    });
+    const R q = div_u(t, bcast(dg, i), bcast(rg, i));
+    sb = tid == i ? q : sb;
+    hc = hcn;
+  });
+  team_sync();
+  if (own) search[tid] = -sb;
+  team_sync();
+}
+
+
+// The substitution of chol_solve_wave for RMAX < nv <= 32 with the solution
+// wave-uniform in registers.  Forward as there (lane t accumulates row t's dot
+// product as each s[i] is formed; s[i] itself is computed on every lane from
+// the broadcast numerator, so it needs no broadcast of its own).  Backward,
+// the oracle's chain s[i] -= H[j][i] s[j] (j ascending) runs on every lane on
+// uniform operands: H[j][i] by broadcast LDS reads, which depend on nothing
+// on the chain and are issued ahead, so the chain is one subtraction per term
+// and the division's tail per row -- no v_readlane on it.
+template <class R>
+__device__ inline void chol_solve_rows32(int nv, int tid, const R* H, const R* grad, R* search) {
+  constexpr int NM = 32;
+  const bool own = tid < nv;
+  R row[NM];
+  sfor<0, NM>(SLAM(jj) {
+    constexpr int j = SK(jj);
+    row[j] = (own && j < nv && j < tid) ? H[tid * nv + j] : (R)0.0;
+  });
+  const R g = own ? grad[tid] : (R)0.0;
+  R acc = 0, out = 0;
+  R s[NM];
+  sfor<0, NM>(SLAM(ii) {
+    constexpr int i = SK(ii);
+    if (i >= nv) {
+      s[i] = 0;
+      return;
+    }
+    const R d = H[i * nv + i];
+    const R a = bcast(i ? g - acc : g, i);
+    s[i] = div_u(a, d, rcp_ref(d));
+    acc += row[i] * s[i];
+  });
+  sfor<0, NM>(SLAM(kk) {
+    constexpr int i = NM - 1 - SK(kk);
+    if (i >= nv) return;
+    R t = s[i];
+    sfor<i + 1, NM>(SLAM(jj) {
+      constexpr int j = SK(jj);
+      if (j < nv) t -= H[j * nv + i] * s[j];
+    });
+    const R d = H[i * nv + i];
+    s[i] = div_u(t, d, rcp_ref(d));
+    out = tid == i ? s[i] : out;
+  });
+  team_sync();
+  if (own) search[tid] = -out;
   team_sync();
 }
 

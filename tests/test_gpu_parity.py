@@ -401,11 +401,14 @@ def test_riccati_mfma_step(ia, fixture):
     assert all(e <= 1e-12 for e in errs.values()), errs
 
 
-@pytest.mark.parametrize("env", [{}, {"ILQG_FUSED": "0"}])
+@pytest.mark.parametrize("env", [{}, {"ILQG_FUSED": "0"}, {"ILQG_PLAN": "1"}])
 def test_fused_sweep_schedules(ia, ora, env, monkeypatch):
-    """The fused FD sweep + streamed backward pass (k_fd_fused_g) and the
-    two-kernel sweep (ILQG_FUSED=0) give the oracle's iterate bit for bit
-    (3 seeds x 41 points x 16 column teams: the ticket order interleaves seeds)"""
+    """The fused FD sweep + streamed backward pass (k_fd_fused_g), the
+    two-kernel sweep (ILQG_FUSED=0) and the fused sweep with its tickets in the
+    order planned from the previous launch's item durations (ILQG_PLAN=1, the
+    second iteration's order is a non-trivial permutation) give the oracle's
+    iterate bit for bit (3 seeds x 41 points x 16 column teams: the ticket
+    order interleaves seeds)"""
     import workloads
     for k, v in env.items():
         monkeypatch.setenv(k, v)
@@ -428,6 +431,18 @@ def test_fused_sweep_schedules(ia, ora, env, monkeypatch):
         exact(D[s], oa["deriv"], f"seed {s} deriv")
         exact(V[s], oa["V"], f"seed {s} V")
         exact(v[s], oa["v"], f"seed {s} v")
+    if env.get("ILQG_PLAN") == "1":
+        import ctypes
+        n = ctypes.c_int(0)
+        ia._check(ia.lib().ilqg_solver_debug_plan(g._h, None, None, ctypes.byref(n)), "debug_plan")
+        order = np.zeros(n.value, dtype=np.uint32)
+        dur = np.zeros(n.value, dtype=np.uint32)
+        ia._check(ia.lib().ilqg_solver_debug_plan(g._h, order.ctypes.data_as(ctypes.c_void_p),
+                                                  dur.ctypes.data_as(ctypes.c_void_p), ctypes.byref(n)),
+                  "debug_plan")
+        assert np.array_equal(np.sort(order), np.arange(n.value)), "planned order is a permutation"
+        assert not np.array_equal(order, np.arange(n.value)), "the planner reordered the tickets"
+        assert (dur > 0).all(), "every item's duration was recorded"
     # the sweep alone (no backward roles) writes the same records
     g.fd_sweep()
     g.synchronize()

@@ -15,7 +15,7 @@ NAMES = {10: " nt: start (warm/smooth choice, factor)", 0: "kinematics", 1: "com
          36: "B: barrier 3", 37: "B: passive+aref / contact rows+aref", 38: "B: euler prefactor / M and M+hD factors", 39: "B: barrier 4 (A com vel + RNE)",
          40: "B: barrier 6 (end of step)", 41: "B: control law + record", 42: "B: factor_ld(M) / limit rows+passive+act",
          43: "B: barrier 5",
-         29: "A: barrier 5b (Euler factor)", 30: "B: Newton warm-start prep"}
+         29: "A: barrier 5b (Euler factor)", 30: "B: Newton warm-start prep", 31: " nt: hessian build (M + J'DJ)"}
 L = ia.lib()
 acc = (ctypes.c_ulonglong * 48)(); cnt = (ctypes.c_ulonglong * 48)()
 m = ia.Model.load(workloads.model_file(sys.argv[1] if len(sys.argv) > 1 else "hopper"))
@@ -48,7 +48,7 @@ for what, fn, rd, rls in (("rollout (1 seed)", g.forward_pass, L.ilqg_debug_stam
     # wave 0's stamps partition its time: top-level stages, their sub-stages
     # (11-23: kinematics and Newton pieces, which restart the stage clock) and
     # the barrier waits
-    tot = sum(acc[i] for i in list(range(11)) + list(range(11, 24)) + list(range(24, 30)))
+    tot = sum(acc[i] for i in list(range(11)) + list(range(11, 24)) + list(range(24, 30)) + [31])
     ms = sum(v[0] for v in tm.values())
     if what == "fd sweep":
         # kernels_fd.hip stamps every 2^ILQG_STAMP_SAMPLE-th workgroup (a sample of
