@@ -252,6 +252,10 @@ struct ilqg_solver {
   DevBuf traj[5], cand[5], dinit[5];
   DevBuf qfrc_applied, xfrc_applied, K, k, deriv, warm_c, cost_c, V, v, cost_cand, cost_sel, sel, alphas, cost;
   DevBuf cw, sync, fault, plan_dur, plan_order;
+  DevBuf snap;  // the centre teams' position/velocity workspace per point (FdFused.snap)
+  int snapd = 0;
+  DevBuf xq;    // the column halves' qacc exchange (FdFused.halves)
+  int halves = 0;
   std::vector<double> host_alphas;
   bool initialized = false;
   hipStream_t own_stream = nullptr;
@@ -427,7 +431,8 @@ static int round16(int n) { return (n + 15) / 16 * 16; }
 // ctrl columns on teams of their own, min(nu, nv) of them (mjderivative.cpp:78-82)
 static int fd_nut(const HostModel& h) { return std::min(h.nu, h.nv); }
 // sync block: ticket, pad x3, cflag[npts], done[npts] (u32), padded to 16 bytes
-static size_t sync_bytes(size_t npts) { return ((4 + 2 * npts) * 4 + 15) / 16 * 16; }
+// [4 + 3 npts + npts ntm] words: ticket, pad, cflag, done, snapshot flags, column pair counters
+static size_t sync_bytes(size_t npts, size_t ntm) { return ((4 + 3 * npts + npts * ntm) * 4 + 15) / 16 * 16; }
 
 int ilqg_model_static_key(const ilqg_model* m, int* key, int cap, int* n) {
   if (!m || !n) return fail(ILQG_ERR_ARG, "null argument");
@@ -558,11 +563,11 @@ int ilqg_fd_batch(const ilqg_model* mc, int n, const double* qpos, const double*
     const int Dp = round16(D), WCp = round16(h.nv + 1);
     DevBuf cw, sy, fl, outp;
     HIPCHK(cw.alloc((size_t)n * WCp * 8));
-    HIPCHK(sy.alloc(sync_bytes(n)));
+    HIPCHK(sy.alloc(sync_bytes(n, fd_nut(h) + 2 * h.nv)));
     HIPCHK(fl.alloc(16));
     HIPCHK(outp.alloc((size_t)n * Dp * 8));
     HIPCHK(hipMemsetAsync(fl.p, 0, 16, m->stream));
-    HIPCHK(hipMemsetAsync(sy.p, 0, sync_bytes(n), m->stream));
+    HIPCHK(hipMemsetAsync(sy.p, 0, sync_bytes(n, fd_nut(h) + 2 * h.nv), m->stream));
     FdFused a{};
     a.tr = st; a.S = n; a.P = 1; a.nB = 0; a.nv = h.nv; a.nut = fd_nut(h);
     a.Dp = Dp; a.WCp = WCp; a.qfrc_applied = s.qa.as<double>(); a.xfrc_applied = s.xf.as<double>(); a.cost = cd;
@@ -635,11 +640,18 @@ int ilqg_solver_create(const ilqg_model* mc, const ilqg_solver_opts* o, const il
   ALLOC(s->deriv, S * P * s->Dp * 8);
   if (s->fused) {
     ALLOC(s->cw, S * P * s->WCp * 8);
-    ALLOC(s->sync, sync_bytes(S * P));
+    const size_t ntm = (size_t)s->nut + 2 * (size_t)h.nv;
+    ALLOC(s->sync, sync_bytes(S * P, ntm));
+    // every column as two items (FdFused.halves): the qacc exchange
+    s->halves = getenv_int("ILQG_FD_HALVES", 0) ? 1 : 0;  // opt-in: measured slower
+    ALLOC(s->xq, S * P * ntm * 2 * (size_t)h.nv * 8);
     // the ticket schedule and the per-item durations it is planned from (zero: no history)
-    const size_t items = S * P * (1 + (size_t)s->nut + 2 * (size_t)h.nv);
+    const size_t items = S * P * (1 + (s->halves ? 2 : 1) * ntm);
     ALLOC(s->plan_dur, items * 4);
     ALLOC(s->plan_order, items * 4);
+    const ilqg_model* mm = s->model;
+    s->snapd = round16(mm->Lc.nd + mm->C.nd + (mm->Lc.ni + mm->C.ni + 1) / 2);
+    ALLOC(s->snap, S * P * (size_t)s->snapd * 8);
   }
   ALLOC(s->fault, 16);
   ALLOC(s->warm_c, S * P * h.nv * 8);
@@ -823,7 +835,8 @@ static hipError_t fused_launch(ilqg_solver* s, const SeedRange& r, int mode) {
   const ilqg_model* m = s->model;
   const HostModel& h = m->host;
   const size_t s0 = r.s0, P = s->P, nx = s->nx;
-  hipError_t e = hipMemsetAsync(r.sync, 0, sync_bytes((size_t)r.ns * P), r.st);
+  const size_t ntm = (size_t)s->nut + 2 * (size_t)h.nv;
+  hipError_t e = hipMemsetAsync(r.sync, 0, sync_bytes((size_t)r.ns * P, ntm), r.st);
   if (e != hipSuccess) return e;
   // the launch's own fault word (handoff.h); the report word survives until read
   e = hipMemsetAsync(s->fault.as<unsigned>() + 1, 0, sizeof(unsigned), r.st);
@@ -850,6 +863,22 @@ static hipError_t fused_launch(ilqg_solver* s, const SeedRange& r, int mode) {
   a.V = s->V.as<double>() + s0 * nx * nx;
   a.v = s->v.as<double>() + s0 * nx;
   a.fl = s->flags();
+  {
+    // FD teams' issue priority by ticket slot (permille of the FD items; 0 = off)
+    const unsigned nit = (unsigned)(r.ns * s->P * (1 + (s->halves ? 2 : 1) * (s->nut + 2 * h.nv)));
+    const int p1 = getenv_int("ILQG_FD_PRIO1", 0), p2 = getenv_int("ILQG_FD_PRIO2", 0);
+    a.prio1 = p1 > 0 ? (unsigned)((unsigned long long)nit * p1 / 1000) : ~0u;
+    a.prio2 = p2 > 0 ? (unsigned)((unsigned long long)nit * p2 / 1000) : ~0u;
+  }
+  if (s->snap.p && getenv_int("ILQG_FD_SNAP", 1)) {
+    a.snap = s->snap.as<double>() + s0 * P * (size_t)s->snapd;
+    a.snapd = s->snapd;
+  }
+  if (s->halves) {
+    a.halves = 1;
+    a.xq = s->xq.as<double>() + s0 * P * ntm * 2 * h.nv;
+    a.pairc = r.sync + 4 + 3 * (size_t)r.ns * P;
+  }
   // ticket schedule from the previous launch's item durations: opt-in
   // (ILQG_PLAN=1); measured slower than the point-major order on the bench
   // workload ("Fused sweep ticket schedule")
@@ -858,7 +887,7 @@ static hipError_t fused_launch(ilqg_solver* s, const SeedRange& r, int mode) {
       const char* e = getenv("ILQG_PLAN_K");
       return e ? (float)atof(e) : 3.0f;
     }();
-    e = launch_fd_plan(r.ns, s->P, s->nut + 2 * h.nv, getenv_int("ILQG_PLAN_P0", 8), kthr,
+    e = launch_fd_plan(r.ns, s->P, (s->halves ? 2 : 1) * (s->nut + 2 * h.nv), getenv_int("ILQG_PLAN_P0", 8), kthr,
                        s->plan_dur.as<unsigned>(), s->plan_order.as<unsigned>(), r.st);
     if (e != hipSuccess) return e;
     a.order = s->plan_order.as<unsigned>();
@@ -981,7 +1010,8 @@ int ilqg_solver_debug_plan(ilqg_solver* s, unsigned* order, unsigned* dur, int* 
   *nitems = n;
   if (!n || (!order && !dur)) return ILQG_OK;
   HIPCHK(s->sync_all());
-  HIPCHK(launch_fd_plan(s->S, s->P, s->nut + 2 * h.nv, getenv_int("ILQG_PLAN_P0", 8), 3.0f, s->plan_dur.as<unsigned>(),
+  HIPCHK(launch_fd_plan(s->S, s->P, (s->halves ? 2 : 1) * (s->nut + 2 * h.nv), getenv_int("ILQG_PLAN_P0", 8), 3.0f,
+                        s->plan_dur.as<unsigned>(),
                         s->plan_order.as<unsigned>(), s->stream));
   HIPCHK(s->sync_all());
   if (order) HIPCHK(hipMemcpy(order, s->plan_order.p, (size_t)n * 4, hipMemcpyDeviceToHost));

@@ -139,17 +139,43 @@ __device__ inline CostDev stage_cost(const auto& m, const auto& C, const Team& T
   return l;
 }
 
-// cpMjData(d, src) from a trajectory record (src/util.cpp:4-14)
+// cpMjData(d, src) from a trajectory record (src/util.cpp:4-14).  Every global
+// load is issued before the first LDS store (one memory round trip, not one
+// per field: the FD teams start with this, ~64k of them per sweep)
 __device__ inline void load_state(const auto& m, const auto& L, const Team& T, const TrajDev& tr, int pt,
                                   int seed, const double* qfrc_applied, const double* xfrc_applied) {
-  FOR_T(i, m.nq) T.w[L.qpos + i] = tr.qpos[(size_t)pt * m.nq + i];
-  FOR_T(i, m.nv) {
-    T.w[L.qvel + i] = tr.qvel[(size_t)pt * m.nv + i];
-    T.w[L.warm + i] = tr.warm[(size_t)pt * m.nv + i];
-    T.w[L.qfrc_applied + i] = qfrc_applied ? qfrc_applied[(size_t)seed * m.nv + i] : 0.0;
+  const int nq = m.nq, nv = m.nv, nu = m.nu, nx6 = 6 * m.nbody;
+  const int t = T.tid;
+  if (nq <= TEAM && nv <= TEAM && nu <= TEAM && nx6 <= 2 * TEAM && T.nt == TEAM) {
+    const double q = t < nq ? tr.qpos[(size_t)pt * nq + t] : 0.0;
+    const double v = t < nv ? tr.qvel[(size_t)pt * nv + t] : 0.0;
+    const double w = t < nv ? tr.warm[(size_t)pt * nv + t] : 0.0;
+    const double fa = (t < nv && qfrc_applied) ? qfrc_applied[(size_t)seed * nv + t] : 0.0;
+    const double c = t < nu ? tr.ctrl[(size_t)pt * nu + t] : 0.0;
+    const double x0 = (t < nx6 && xfrc_applied) ? xfrc_applied[(size_t)seed * nx6 + t] : 0.0;
+    const double x1 = (t + TEAM < nx6 && xfrc_applied) ? xfrc_applied[(size_t)seed * nx6 + t + TEAM] : 0.0;
+    const double tm = tr.time[pt];
+    if (t < nq) T.w[L.qpos + t] = q;
+    if (t < nv) {
+      T.w[L.qvel + t] = v;
+      T.w[L.warm + t] = w;
+      T.w[L.qfrc_applied + t] = fa;
+    }
+    if (t < nu) T.w[L.ctrl + t] = c;
+    if (t < nx6) T.w[L.xfrc_applied + t] = x0;
+    if (t + TEAM < nx6) T.w[L.xfrc_applied + t + TEAM] = x1;
+    if (t == 0) T.w[L.time] = tm;
+    TSYNC();
+    return;
   }
-  FOR_T(i, m.nu) T.w[L.ctrl + i] = tr.ctrl[(size_t)pt * m.nu + i];
-  FOR_T(i, 6 * m.nbody) T.w[L.xfrc_applied + i] = xfrc_applied ? xfrc_applied[(size_t)seed * 6 * m.nbody + i] : 0.0;
+  FOR_T(i, nq) T.w[L.qpos + i] = tr.qpos[(size_t)pt * nq + i];
+  FOR_T(i, nv) {
+    T.w[L.qvel + i] = tr.qvel[(size_t)pt * nv + i];
+    T.w[L.warm + i] = tr.warm[(size_t)pt * nv + i];
+    T.w[L.qfrc_applied + i] = qfrc_applied ? qfrc_applied[(size_t)seed * nv + i] : 0.0;
+  }
+  FOR_T(i, nu) T.w[L.ctrl + i] = tr.ctrl[(size_t)pt * nu + i];
+  FOR_T(i, nx6) T.w[L.xfrc_applied + i] = xfrc_applied ? xfrc_applied[(size_t)seed * nx6 + i] : 0.0;
   if (T.tid == 0) T.w[L.time] = tr.time[pt];
   TSYNC();
 }

@@ -99,6 +99,13 @@ __device__ inline double det_cos(double x) {
 // flow (two tests and a four-way switch per function, in series).
 __device__ inline void det_sincos(double x, double* s, double* c) {
   const double PIO4 = 7.85398163397448278999e-01;
+  // every active lane within pi/4 (the common case for joint half-angles): the
+  // small-angle kernels are all either function evaluates
+  if (__ballot(!(fabs(x) < PIO4)) == 0ull) {
+    *s = x == 0 ? x : k_sin(x, 0.0, 0);
+    *c = k_cos(x, 0.0);
+    return;
+  }
   double y0, y1;
   const int n = rem_pio2(x, &y0, &y1);
   const double s0 = k_sin(x, 0.0, 0), c0 = k_cos(x, 0.0);

@@ -60,6 +60,12 @@ __device__ __forceinline__ void st_sc1(double* p, double v) {
   __hip_atomic_store((gu64*)(p), (unsigned long long)__double_as_longlong(v), __ATOMIC_RELAXED,
                      __HIP_MEMORY_SCOPE_AGENT);
 }
+__device__ __forceinline__ int ld_sc1_i(const int* p) {
+  return (int)__hip_atomic_load((gu32*)(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void st_sc1_i(int* p, int v) {
+  __hip_atomic_store((gu32*)(p), (unsigned)v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
 // every storing wave, after its sc1 payload stores and before the signal
 __device__ __forceinline__ void drain_stores() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
 

@@ -86,6 +86,20 @@ struct FdFused {
   // FD item's duration in this launch (s_memrealtime ticks), null = not kept
   const unsigned* order;
   unsigned* dur;
+  // issue priority of the FD teams by ticket slot: slots >= prio1 run at
+  // s_setprio 1, >= prio2 at 2 (the backward roles run at 3); ~0u = never
+  unsigned prio1 = ~0u, prio2 = ~0u;
+  // the centre team's workspace after its position and velocity stages, per
+  // point ([S*P][snapd] doubles: the team's LDS doubles, then its ints), which
+  // the qvel and ctrl teams load instead of recomputing those stages; null =
+  // every team computes its own
+  double* snap = nullptr;
+  int snapd = 0;
+  // every column as two items, its + and - evaluations ([S*P][ntm][2][nv]
+  // qacc exchange, [S*P][ntm] pair counters zeroed with sync); 0 = one item
+  int halves = 0;
+  double* xq = nullptr;
+  unsigned* pairc = nullptr;
 };
 // Plan the fused sweep's ticket order from the previous launch's per-item
 // durations (dur, all zero = no history: identity order).  Items of the first

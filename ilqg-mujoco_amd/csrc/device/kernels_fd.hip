@@ -182,9 +182,14 @@ __device__ inline unsigned take_ticket(unsigned* sync) {
 
 // FD item u -> role (0 = C, 1 = V, 2 = Q, 3 = U), seed, point, index; ntm = nu + 2 nv
 // column teams per (seed, point)
-__device__ inline void fd_decode(const FdFused& a, unsigned ntm, unsigned u, int& role, int& s, int& p, int& idx) {
-  const unsigned nC = a.S * a.P, nW = a.S * ntm;
+// (a.halves: every column is two items, its + and - evaluations, adjacent;
+// half = 0 / 1, else -1)
+__device__ inline void fd_decode(const FdFused& a, unsigned ntm, unsigned u, int& role, int& s, int& p, int& idx,
+                                 int& half) {
+  const unsigned nt = a.halves ? 2 * ntm : ntm;
+  const unsigned nC = a.S * a.P, nW = a.S * nt;
   idx = 0;
+  half = -1;
   if (u < nC) {
     role = 0; p = u / a.S; s = u % a.S;
     return;
@@ -192,8 +197,12 @@ __device__ inline void fd_decode(const FdFused& a, unsigned ntm, unsigned u, int
   u -= nC;
   p = u / nW;
   const unsigned o = u % nW;
-  s = o / ntm;
-  const int w = o % ntm;
+  s = o / nt;
+  int w = o % nt;
+  if (a.halves) {
+    half = w & 1;
+    w >>= 1;
+  }
   if (w < a.nut) { role = 3; idx = w; }
   else if (w < a.nut + a.nv) { role = 1; idx = w - a.nut; }
   else { role = 2; idx = w - a.nut - a.nv; }
@@ -203,7 +212,7 @@ __device__ inline void fd_decode(const FdFused& a, unsigned ntm, unsigned u, int
 // diagnostic timeline of the fused sweep: per FD item u (ticket - nB) its
 // start and end (s_memrealtime, 100 MHz) and its XCC / SE / CU; per backward
 // role its start and end (tools/fused_timeline.py)
-constexpr int TL_N = 65536;
+constexpr int TL_N = 131072;
 static __device__ unsigned long long g_tl[3 * TL_N];
 static __device__ unsigned long long g_tlb[2 * 64];
 __device__ inline unsigned long long hw_where() {
@@ -214,6 +223,9 @@ __device__ inline unsigned long long hw_where() {
 #endif
 __device__ inline void fd_fused_body(const auto& m, const auto& L, const auto& C, const auto& X, const Team& T,
                                      const FdFused& a, unsigned u) {
+  // late tickets first in the SIMD's issue arbitration: they set the launch's tail
+  if (u >= a.prio2) __builtin_amdgcn_s_setprio(2);
+  else if (u >= a.prio1) __builtin_amdgcn_s_setprio(1);
   // the planned schedule (launch_fd_plan); readfirstlane: the item stays wave-uniform (SGPR)
   if (a.order) u = __builtin_amdgcn_readfirstlane(a.order[u]);
   const unsigned long long tstart = __builtin_amdgcn_s_memrealtime();
@@ -227,8 +239,9 @@ __device__ inline void fd_fused_body(const auto& m, const auto& L, const auto& C
 #endif
   const int nv = m.nv, nu = m.nu, nq = m.nq;
   const int nctrl = nu < nv ? nu : nv;  // mjderivative.cpp:78-82 (assumes nv >= nu)
-  int role, s, p, idx;
-  fd_decode(a, a.nut + 2 * nv, u, role, s, p, idx);
+  int role, s, p, idx, half;
+  const int ntm = a.nut + 2 * nv;
+  fd_decode(a, ntm, u, role, s, p, idx, half);
   const int pt = s * a.P + p;
   double* dr = a.deriv + (size_t)pt * a.Dp;
   double* cwp = a.cw + (size_t)pt * a.WCp;
@@ -242,7 +255,54 @@ __device__ inline void fd_fused_body(const auto& m, const auto& L, const auto& C
   const int tid = T.tid;
   const int G = 2 * nv * nv + nv * nu;  // cost-gradient entries: qpos, qvel, ctrl
   const double* dq = a.tr.qpos + (size_t)pt * nq;
-  load_state(m, L, T, a.tr, pt, s, a.qfrc_applied, a.xfrc_applied);
+  // the centre's position/velocity workspace snapshot (a.snap): the team's LDS
+  // doubles [w | c] and ints [iw | ci] (contiguous, make_team)
+  const int nwd = L.nd + C.nd, nid = L.ni + C.ni;
+  const bool snap = a.snap && nwd + (nid + 1) / 2 <= a.snapd;
+  double* sp = snap ? a.snap + (size_t)pt * a.snapd : nullptr;
+  unsigned* sflag = a.sync + 4 + 2 * (size_t)a.S * a.P + pt;
+  auto snap_store = [&]() {
+    FOR_T(e, nwd) st_sc1(sp + e, T.w[e]);
+    FOR_T(e, nid) st_sc1_i(reinterpret_cast<int*>(sp + nwd) + e, T.iw[e]);
+    drain_stores();
+    TSYNC();
+    if (tid == 0) signal_set(sflag, 1u);
+  };
+  auto snap_load = [&]() {
+    bw_wait_geq(sflag, 1u, a.fault);
+    // sixteen loads in flight per lane before their LDS stores
+    constexpr int CH = 16;
+    for (int e0 = 0; e0 < nwd; e0 += CH * TEAM) {
+      double v[CH];
+#pragma unroll
+      for (int q = 0; q < CH; q++) {
+        const int e = e0 + q * TEAM + tid;
+        v[q] = e < nwd ? ld_sc1(sp + e) : 0.0;
+      }
+#pragma unroll
+      for (int q = 0; q < CH; q++) {
+        const int e = e0 + q * TEAM + tid;
+        if (e < nwd) T.w[e] = v[q];
+      }
+    }
+    for (int e0 = 0; e0 < nid; e0 += CH * TEAM) {
+      int v[CH];
+#pragma unroll
+      for (int q = 0; q < CH; q++) {
+        const int e = e0 + q * TEAM + tid;
+        v[q] = e < nid ? ld_sc1_i(reinterpret_cast<const int*>(sp + nwd) + e) : 0;
+      }
+#pragma unroll
+      for (int q = 0; q < CH; q++) {
+        const int e = e0 + q * TEAM + tid;
+        if (e < nid) T.iw[e] = v[q];
+      }
+    }
+    TSYNC();
+  };
+  // qvel / ctrl teams with a snapshot take their whole state from it
+  if (!(snap && (role == 1 || role == 3))) load_state(m, L, T, a.tr, pt, s, a.qfrc_applied, a.xfrc_applied);
+  bool announce = true;           // this team signals done[s,p] (a.halves: the column's second half)
   double wc = 0, costCenter = 0;  // centre warm start (lane j holds entry j) and cost
   auto set_warm = [&]() {
     if (tid < nv) warm[tid] = wc;
@@ -256,7 +316,15 @@ __device__ inline void fd_fused_body(const auto& m, const auto& L, const auto& C
   if (role == 0) {
     // centre: mj_forward + nwarmup - 1 = 2 forwardSkip(VEL) (written out: no loop)
     static_assert(FD_NWARMUP == 3, "centre warm-up");
-    forward_skip(m, L, C, X, T, STAGE_NONE, FD_NITER, 0.0);
+    if (snap) {
+      // forward_skip(STAGE_NONE) with the workspace published between its
+      // velocity and acceleration stages
+      forward_posvel(m, L, C, X, T, STAGE_NONE);
+      snap_store();
+      forward_acc(m, L, C, X, T, FD_NITER, 0.0);
+    } else {
+      forward_skip(m, L, C, X, T, STAGE_NONE, FD_NITER, 0.0);
+    }
     forward_skip(m, L, C, X, T, STAGE_VEL, FD_NITER, 0.0);
     forward_skip(m, L, C, X, T, STAGE_VEL, FD_NITER, 0.0);
     wc = tid < nv ? warm[tid] : 0.0;
@@ -266,11 +334,89 @@ __device__ inline void fd_fused_body(const auto& m, const auto& L, const auto& C
     drain_stores();
     TSYNC();
     if (tid == 0) signal_set(cflag, 1u);
+  } else if (half >= 0) {
+    // one evaluation of a column (a.halves): the + half also writes the cost
+    // entry; both publish their qacc, and the second to finish forms the
+    // column (qp - qm) / 2 eps and announces it on done[s,p]
+    const int i = idx;
+    const int col = role == 3 ? i : (role == 1 ? a.nut + i : a.nut + nv + i);
+    const double sg = half ? -FD_EPS : FD_EPS;
+    if (role == 3) {
+      if (snap) snap_load();
+      else forward_posvel(m, L, C, X, T, STAGE_NONE);
+      get_centre();
+      const double u0 = ctrl[i];
+      TSYNC();
+      if (tid == 0) {
+        ctrl[i] = u0 + sg;
+        if (!half) st_sc1(dr + G + 2 * nv + i, (step_cost(m, a.cost, qpos, qvel, ctrl) - costCenter) / FD_EPS);
+      }
+      set_warm();
+      forward_acc(m, L, C, X, T, FD_NITER, 0.0);
+    } else if (role == 1) {
+      if (snap) snap_load();
+      const double v0 = qvel[i];
+      TSYNC();
+      if (tid == 0) qvel[i] = v0 + sg;
+      forward_posvel(m, L, C, X, T, snap ? STAGE_POS : STAGE_NONE);
+      get_centre();
+      if (tid == 0 && !half) st_sc1(dr + G + nv + i, (step_cost(m, a.cost, qpos, qvel, ctrl) - costCenter) / FD_EPS);
+      set_warm();
+      forward_acc(m, L, C, X, T, FD_NITER, 0.0);
+    } else {
+      const int jid = m.dof_jntid[i];
+      int quatadr = -1, dofpos = 0;
+      if (m.jnt_type[jid] == JNT_BALL) {
+        quatadr = m.jnt_qposadr[jid];
+        dofpos = i - m.jnt_dofadr[jid];
+      } else if (m.jnt_type[jid] == JNT_FREE && i >= m.jnt_dofadr[jid] + 3) {
+        quatadr = m.jnt_qposadr[jid] + 3;
+        dofpos = i - m.jnt_dofadr[jid] - 3;
+      }
+      if (tid == 0) {
+        if (quatadr >= 0) {
+          double angvel[3] = {0, 0, 0}, q[4];
+          angvel[dofpos] = sg;
+          ldm<4>(q, qpos + quatadr);
+          quat_integrate(q, angvel, 1);
+          for (int k = 0; k < 4; k++) qpos[quatadr + k] = q[k];
+        } else {
+          qpos[m.jnt_qposadr[jid] + i - m.jnt_dofadr[jid]] += sg;
+        }
+      }
+      forward_posvel(m, L, C, X, T, STAGE_NONE);
+      get_centre();
+      if (tid == 0 && !half) st_sc1(dr + G + i, (step_cost(m, a.cost, qpos, qvel, ctrl) - costCenter) / FD_EPS);
+      set_warm();
+      forward_acc(m, L, C, X, T, FD_NITER, 0.0);
+    }
+    const double mine = tid < nv ? qacc[tid] : 0.0;
+    double* xs = a.xq + ((size_t)pt * ntm + col) * 2 * nv;
+    if (tid < nv) st_sc1(xs + half * nv + tid, mine);
+    drain_stores();
+    TSYNC();
+    unsigned prior = 0;
+    if (tid == 0) prior = __hip_atomic_fetch_add((gu32*)(a.pairc + (size_t)pt * ntm + col), 1u, __ATOMIC_RELAXED,
+                                                 __HIP_MEMORY_SCOPE_AGENT);
+    prior = __builtin_amdgcn_readfirstlane(prior);
+    if (prior == 1u) {
+      const double other = tid < nv ? ld_sc1(xs + (1 - half) * nv + tid) : 0.0;
+      const double qp = half ? other : mine, qm = half ? mine : other;
+      const double dv = (qp - qm) / (2 * FD_EPS);
+      if (tid < nv) {
+        if (role == 3) st_sc1(dr + 2 * nv * nv + i + tid * nu, dv);
+        else if (role == 1) st_sc1(dr + nv * nv + i + tid * nv, dv);
+        else st_sc1(dr + i + tid * nv, dv);
+      }
+    } else {
+      announce = false;
+    }
   } else if (role == 3) {
     // ctrl column idx on its own position/velocity stages (ctrl enters only the
     // acceleration stage, so they equal the centre's)
     const int i = idx;
-    forward_posvel(m, L, C, X, T, STAGE_NONE);
+    if (snap) snap_load();
+    else forward_posvel(m, L, C, X, T, STAGE_NONE);
     get_centre();
     const double u0 = ctrl[i];
     TSYNC();
@@ -288,10 +434,12 @@ __device__ inline void fd_fused_body(const auto& m, const auto& L, const auto& C
   } else if (role == 1) {
     // qvel column idx: + side from a position stage of its own, - side reusing it
     const int i = idx;
+    if (snap) snap_load();
     const double v0 = qvel[i];
     TSYNC();
     if (tid == 0) qvel[i] = v0 + FD_EPS;
-    forward_posvel(m, L, C, X, T, STAGE_NONE);
+    // its position stage is the centre's (qpos unchanged): from the snapshot
+    forward_posvel(m, L, C, X, T, snap ? STAGE_POS : STAGE_NONE);
     get_centre();
     if (tid == 0) st_sc1(dr + G + nv + i, (step_cost(m, a.cost, qpos, qvel, ctrl) - costCenter) / FD_EPS);
     set_warm();
@@ -342,7 +490,7 @@ __device__ inline void fd_fused_body(const auto& m, const auto& L, const auto& C
   }
   drain_stores();
   TSYNC();
-  if (tid == 0) signal_add(done);
+  if (tid == 0 && announce) signal_add(done);
   if (a.dur && tid == 0) a.dur[u] = (unsigned)(__builtin_amdgcn_s_memrealtime() - tstart);
 #ifdef ILQG_STAMPS
   if (tid == 0 && u < (unsigned)TL_N) g_tl[3 * u + 1] = __builtin_amdgcn_s_memrealtime();
@@ -562,7 +710,7 @@ hipError_t launch_fd_cols_coop(const DevModel& m, const WsLayout& L, const CoopL
 
 hipError_t launch_fd_fused_coop(const DevModel& m, const WsLayout& L, const CoopLayout& C, const CoopAux& X,
                                 const FdFused& a, hipStream_t st) {
-  const long items = (long)a.S * a.P * (1 + a.nut + 2 * m.nv);
+  const long items = (long)a.S * a.P * (1 + (a.halves ? 2 : 1) * (a.nut + 2 * m.nv));
   const long blocks = items + a.nB;
   if (items <= 0) return hipSuccess;
   size_t lds = coop_lds_bytes(L, C);

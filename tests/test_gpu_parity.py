@@ -401,14 +401,17 @@ def test_riccati_mfma_step(ia, fixture):
     assert all(e <= 1e-12 for e in errs.values()), errs
 
 
-@pytest.mark.parametrize("env", [{}, {"ILQG_FUSED": "0"}, {"ILQG_PLAN": "1"}])
+@pytest.mark.parametrize("env", [{}, {"ILQG_FUSED": "0"}, {"ILQG_PLAN": "1"}, {"ILQG_FD_HALVES": "1"},
+                                 {"ILQG_FD_SNAP": "0"}, {"ILQG_FD_HALVES": "1", "ILQG_FD_SNAP": "0"}])
 def test_fused_sweep_schedules(ia, ora, env, monkeypatch):
     """The fused FD sweep + streamed backward pass (k_fd_fused_g), the
-    two-kernel sweep (ILQG_FUSED=0) and the fused sweep with its tickets in the
+    two-kernel sweep (ILQG_FUSED=0), the fused sweep with its tickets in the
     order planned from the previous launch's item durations (ILQG_PLAN=1, the
-    second iteration's order is a non-trivial permutation) give the oracle's
-    iterate bit for bit (3 seeds x 41 points x 16 column teams: the ticket
-    order interleaves seeds)"""
+    second iteration's order is a non-trivial permutation), with every column
+    as two teams, its + and - halves (ILQG_FD_HALVES=1) and with the qvel/ctrl
+    teams computing their own position/velocity stages instead of loading the
+    centre's (ILQG_FD_SNAP=0) give the oracle's iterate bit for bit (3 seeds x
+    41 points x 16 column teams: the ticket order interleaves seeds)"""
     import workloads
     for k, v in env.items():
         monkeypatch.setenv(k, v)

@@ -13,7 +13,7 @@ sys.path.insert(0, os.path.join(ROOT, "ilqg-mujoco_amd"))
 import ilqg_amd as ia  # noqa: E402
 import workloads  # noqa: E402
 
-TL_N = 65536
+TL_N = 131072
 L = ia.lib()
 buf = (ctypes.c_ulonglong * (3 * TL_N + 128 + 8 * 512))()
 S = int(sys.argv[1]) if len(sys.argv) > 1 else 8
@@ -32,7 +32,9 @@ L.ilqg_debug_timeline(buf, 0)
 a = np.frombuffer(buf, dtype=np.uint64)
 nv, nu, P = m.nv, m.nu, 501
 ntm = nu + 2 * nv
-n_items = S * P * (1 + ntm)
+HALVES = int(os.environ.get("ILQG_FD_HALVES", "0")) != 0  # every column as two items (+, -)
+ncw = 2 * ntm if HALVES else ntm  # column items per (seed, point)
+n_items = S * P * (1 + ncw)
 tl = a[: 3 * TL_N].reshape(TL_N, 3)[:n_items]
 tb = a[3 * TL_N:3 * TL_N + 128].reshape(64, 2)[:S].astype(np.int64)
 bstep = a[3 * TL_N + 128:].reshape(8, 512).astype(np.int64)
@@ -45,7 +47,9 @@ dur = (en - st) / 100.0
 u = np.arange(n_items)
 nC = S * P
 role = np.where(u < nC, 0, 0)
-w = (u - nC) % (S * ntm) % ntm
+w = (u - nC) % (S * ncw) % ncw
+if HALVES:
+    w = w // 2
 role = np.where(u < nC, 0, np.where(w < nu, 3, np.where(w < nu + nv, 1, 2)))
 names = {0: "C (centre)", 1: "V (qvel col)", 2: "Q (qpos col)", 3: "U (ctrl col)"}
 for r in (0, 3, 1, 2):
@@ -71,14 +75,14 @@ print("  team starts per 50 us: " + " ".join(str(x) for x in starts))
 # per point: time the record is complete (all teams of (s, p) ended), seed 0
 pts = []
 for p in range(P):
-    idx = [p * S + 0] + [nC + p * S * ntm + 0 * ntm + k for k in range(ntm)]
+    idx = [p * S + 0] + [nC + p * S * ncw + 0 * ncw + k for k in range(ncw)]
     pts.append(us(en[idx].max()))
 pts = np.array(pts)
 print("  seed 0 record complete (us) at points 0,50,...: " + " ".join(f"{pts[p]:.0f}" for p in range(0, P, 50)))
 # the recursion against its records (handoff.h g_bstep): step n of seed s needs
 # record n (and prefetches n + 1); lag = step done - that record complete
 for s_ in range(min(S, 8)):
-    ready = np.array([us(en[[p * S + s_] + [nC + p * S * ntm + s_ * ntm + k for k in range(ntm)]].max())
+    ready = np.array([us(en[[p * S + s_] + [nC + p * S * ncw + s_ * ncw + k for k in range(ncw)]].max())
                       for p in range(P)])
     done = bstep[s_, 1:P]
     if not np.all(done > 0):
