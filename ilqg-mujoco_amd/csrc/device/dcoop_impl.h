@@ -1884,6 +1884,135 @@ __device__ inline void fwd_velocity_u(const auto& m, const auto& L, const Team& 
   TSYNC();
 }
 
+#ifndef ILQG_VEL_H
+#define ILQG_VEL_H 1
+#endif
+// fwd_velocity_u's values with its independent work spread over lanes: a
+// wave-uniform stage executes every scalar operation as a full wave
+// instruction, so the ≈700 operations of the velocity stage cost their count
+// in issue cycles.  Here each phase runs one output per lane and the phases
+// exchange through LDS (five wave fences):
+//   1. lane k < 6: component k of the com velocities down the tree (the cvel
+//      each dof sees, cvb, and every body's cvel);
+//   2. lane 6 d + c: component c of cdof_dot[d] = cross_motion(cvb[d], cdof[d]);
+//   3. lane k < 6: component k of the per-body dof terms and cacc down the tree;
+//   4. lane i (body): cfrc_i = I_i cacc_i + cvel_i x* (I_i cvel_i);
+//   5. lane k < 6: the subtree sums; then lane d: qfrc_bias[d] = cdof_d . cfrc_body(d).
+// Every value is the expression fwd_velocity_u evaluates, in its order
+// (cross_motion's terms as a lane-selected pair or pair of pairs: -x*y is
+// -(x*y) exactly, and x - y is x + (-y)).
+template <class MT>
+__device__ inline void fwd_velocity_h(const auto& m, const auto& L, const Team& T) {
+  constexpr int NV = MT::nv, NB = MT::nbody;
+  static_assert(6 * NV <= TEAM_SIZE && NB <= TEAM_SIZE, "one output per lane");
+  const int t = T.tid;
+  real* cvw = T.w + L.cvel;      // [NB][6]
+  real* cvb = T.w + L.s_con;     // [NV][6]: the cvel dof d sees
+  real* cdw = T.w + L.cdof_dot;  // [NV][6]
+  real* cac = T.w + L.s_rne;     // [NB][6]
+  real* cfw = cac + 6 * NB;      // [NB][6]
+  const real* cdofw = T.w + L.cdof;
+  const real* qvw = T.w + L.qvel;
+  real qv[NV];
+  sfor<0, NV>(SLAM(dd) { qv[SK(dd)] = qvw[SK(dd)]; });
+  // 1. com velocities
+  if (t < 6) {
+    const int k = t;
+    real cdk[NV];
+    sfor<0, NV>(SLAM(dd) { cdk[SK(dd)] = cdofw[6 * SK(dd) + k]; });
+    real cvel[NB];
+    cvel[0] = 0;
+    sfor<1, NB>(SLAM(ii) {
+      constexpr int i = SK(ii);
+      constexpr int pid = MT::body_parentid[i], bda = MT::body_dofadr[i], nd = MT::body_dofnum[i];
+      real cv = cvel[pid];
+      sfor<0, nd>(SLAM(jj) {
+        constexpr int d = bda + SK(jj);
+        cvb[6 * d + k] = cv;
+        real tt = 0;
+        tt += cdk[d] * qv[d];
+        cv += tt;
+      });
+      cvel[i] = cv;
+    });
+    sfor<0, NB>(SLAM(ii) { cvw[6 * SK(ii) + k] = cvel[SK(ii)]; });
+  }
+  TSYNC();
+  // 2. cdof_dot: r[c] = (s1 v[a1] x[b1] + s2 v[a2] x[b2]) [+ (s3 .. + s4 ..) for c >= 3]
+  if (t < 6 * NV) {
+    const int d = t / 6, c = t - 6 * (t / 6);
+    // cross_motion's operand indices and signs per component, 4 bits per c
+    constexpr unsigned long long A1 = 0x122122, B1 = 0x334001, A2 = 0x001001, B2 = 0x455122;
+    constexpr unsigned long long A3 = 0x455000, B3 = 0x001000, A4 = 0x334000, B4 = 0x122000;
+    constexpr unsigned N1 = 0b101101, N2 = 0b010010, N3 = 0b101000, N4 = 0b010000;
+    auto f4 = [&](unsigned long long P) { return (int)((P >> (4 * c)) & 15); };
+    const real* v = cvb + 6 * d;
+    const real* x = cdofw + 6 * d;
+    const real p1 = v[f4(A1)] * x[f4(B1)], p2 = v[f4(A2)] * x[f4(B2)];
+    const real p3 = v[f4(A3)] * x[f4(B3)], p4 = v[f4(A4)] * x[f4(B4)];
+    const real s1 = ((N1 >> c) & 1 ? -p1 : p1) + ((N2 >> c) & 1 ? -p2 : p2);
+    const real s2 = ((N3 >> c) & 1 ? -p3 : p3) + ((N4 >> c) & 1 ? -p4 : p4);
+    cdw[t] = c < 3 ? s1 : s1 + s2;
+  }
+  TSYNC();
+  // 3. per-body dof terms and cacc down the tree
+  if (t < 6) {
+    const int k = t;
+    real cdd[NV];
+    sfor<0, NV>(SLAM(dd) { cdd[SK(dd)] = cdw[6 * SK(dd) + k]; });
+    real cacc[NB];
+    cacc[0] = k < 3 ? 0.0 : (k == 3 ? -m.opt_gravity0 : (k == 4 ? -m.opt_gravity1 : -m.opt_gravity2));
+    sfor<1, NB>(SLAM(ii) {
+      constexpr int i = SK(ii);
+      constexpr int pid = MT::body_parentid[i], bda = MT::body_dofadr[i], nd = MT::body_dofnum[i];
+      real sum = 0;
+      sfor<0, nd>(SLAM(jj) { sum += cdd[bda + SK(jj)] * qv[bda + SK(jj)]; });
+      const real rt = nd ? sum : 0;
+      cacc[i] = cacc[pid] + rt;
+    });
+    sfor<0, NB>(SLAM(ii) { cac[6 * SK(ii) + k] = cacc[SK(ii)]; });
+  }
+  TSYNC();
+  // 4. cfrc per body
+  if (t >= 1 && t < NB) {
+    const int i = t;
+    real ci[10], a[6], cv[6], f[6], tmp[6], tmp1[6];
+    ldm<10>(ci, T.w + L.cinert + 10 * i);
+    ldm<6>(a, cac + 6 * i);
+    ldm<6>(cv, cvw + 6 * i);
+    mul_inert_vec(f, ci, a);
+    mul_inert_vec(tmp, ci, cv);
+    cross_force(tmp1, cv, tmp);
+    sfor<0, 6>(SLAM(kk) { cfw[6 * i + SK(kk)] = f[SK(kk)] + tmp1[SK(kk)]; });
+  }
+  TSYNC();
+  // 5. subtree sums (children before parents), then the bias rows
+  if (t < 6) {
+    const int k = t;
+    real cf[NB];
+    sfor<1, NB>(SLAM(ii) { cf[SK(ii)] = cfw[6 * SK(ii) + k]; });
+    sfor<0, NB - 1>(SLAM(ii) {
+      constexpr int i = NB - 1 - SK(ii);
+      constexpr int p = MT::body_parentid[i];
+      if constexpr (p != 0) cf[p] += cf[i];
+    });
+    sfor<1, NB>(SLAM(ii) { cfw[6 * SK(ii) + k] = cf[SK(ii)]; });
+  }
+  TSYNC();
+  if (t < NV) {
+    const int d = t;
+    int bi = 0;
+    sfor<0, NV>(SLAM(dd) { bi = d == SK(dd) ? MT::dof_bodyid[SK(dd)] : bi; });
+    real cd[6], cf[6];
+    ldm<6>(cd, cdofw + 6 * d);
+    ldm<6>(cf, cfw + 6 * bi);
+    real r = 0;
+    sfor<0, 6>(SLAM(kk) { r += cd[SK(kk)] * cf[SK(kk)]; });
+    T.w[L.qfrc_bias + d] = r;
+  }
+  TSYNC();
+}
+
 // -------------------------------------------------- acceleration stage ---
 // act_pre: actuator_force() already ran (two-wave rollout: on the helper wave)
 __device__ inline void fwd_acceleration(const auto& m, const auto& L, const auto& X, const Team& T,
@@ -3086,6 +3215,64 @@ __device__ inline void fwd_constraint_u(const auto& m, const auto& L, const auto
 #endif
 }
 
+#ifndef ILQG_WARM_U
+#define ILQG_WARM_U 1
+#endif
+// newton_warm_prep for compile-time nv <= RMAX in fwd_constraint_u's register
+// forms (its non-dual branch's warm-start values: J w - aref per row, M w,
+// the warm start's constraint cost and J' force, the factor of its Hessian),
+// published where fwd_constraint_u's dual branch reads them: jar and M w in
+// the Newton scratch, J' force in qfrc_constraint, the factor's lower triangle
+// at s_newton + 4 nv, the cost and the active mask in the team scalars
+template <int NV>
+__device__ inline void newton_warm_prep_u(const auto& m, const auto& L, const auto& C, const Team& T) {
+  const int ne = T.iw[L.nefc];
+  real* sn = T.w + L.s_newton;
+  real* jar_l = sn + 4 * NV + NV * NV;
+  const real* qM = T.w + L.qM;
+  const real* J = T.w + L.efc_J;
+  const int r = T.tid;
+  const bool row = r < ne;
+  const real Di = row ? T.w[L.efc_D + r] : 0.0;
+  const real aref = row ? T.w[L.efc_aref + r] : 0.0;
+  real Jr[NV], Mr[NV], warm[NV];
+  sfor<0, NV>(SLAM(jj) {
+    constexpr int j = SK(jj);
+    Jr[j] = row ? J[r * NV + j] : 0.0;
+    Mr[j] = r < NV ? qM[r * NV + j] : 0.0;
+  });
+  ldu(warm, T.w + L.warm);
+  const real jw = row ? dotu(Jr, warm) - aref : 0.0;
+  const real maw = dotu(Mr, warm);
+  const bool actw = row && jw < 0;
+  const unsigned long long mw = __ballot(actw);
+  const real cu_w = lane_sum_mask(0.0, actw ? 0.5 * Di * jw * jw : -0.0, mw);
+  real qc[NV], p[NV];
+  const real f = actw ? -Di * jw : 0.0;
+  sfor<0, NV>(SLAM(jj) { p[SK(jj)] = Jr[SK(jj)] * f; });
+  lane_sums_mask(qc, p, mw);
+  real Hf[NV][NV], rd[NV];
+  hessian_factor_u<NV>(qM, J, T.w + L.efc_D, mw, r, Hf, rd);
+  if (row) jar_l[r] = jw;
+  if (r < NV) sn[r] = maw;
+  real qv = qc[0];
+  sfor<1, NV>(SLAM(jj) { qv = r == SK(jj) ? qc[SK(jj)] : qv; });
+  if (r < NV) T.w[L.qfrc_con + r] = qv;
+  if (r < NV * NV) {
+    const int i = r / NV, j = r % NV;
+    real hv = 0;
+    sfor<0, NV>(SLAM(ii) {
+      sfor<0, SK(ii) + 1>(SLAM(cc) { hv = r == SK(ii) * NV + SK(cc) ? Hf[SK(ii)][SK(cc)] : hv; });
+    });
+    if (j <= i) sn[4 * NV + r] = hv;
+  }
+  if (r == 0) {
+    T.c[C.bc + 4] = cu_w;
+    T.c[C.bc + 5] = __longlong_as_double((long long)mw);
+  }
+  TSYNC();
+}
+
 // dual: the primary wave of a two-wave team whose helper runs newton_warm_prep
 // concurrently; exactly one __syncthreads (after the smooth start's cost)
 __device__ inline void fwd_constraint_fast(const auto& m, const auto& L, const auto& C, const auto& X,
@@ -3655,6 +3842,46 @@ __device__ inline void factor_m_and_euler(const auto& m, const auto& L, const au
   factor_ld_rows2(nv, X.pmask, T.tid, qM, T.w + L.qLD, T.w + L.qLDinv, qH, qHLD, qHinv);
 }
 
+// factor_m_and_euler split for the three-wave step: the factor of M, announced
+// on `fm` (step id sid) as soon as it is formed (phase 4; the primary's
+// acceleration stage waits for it), and the factor of M + h D, which only
+// the integrator reads (phase 5, beside the primary's Newton solve).
+// factor_ld_rows twice is factor_ld_rows2's operations.  Returns whether the
+// second factor is still to be formed (euler_factor_rows).
+__device__ inline bool factor_m_signal(const auto& m, const auto& L, const auto& C, const auto& X, const Team& T,
+                                       bool eul, int* fm, int sid) {
+  const int nv = m.nv;
+  if (!(nv <= RMAX && has_pmask(X))) {
+    factor_m_and_euler(m, L, C, X, T, eul);
+    wave_signal(fm, sid);
+    return false;
+  }
+  factor_ld_rows(nv, X.pmask, T.tid, T.w + L.qM, T.w + L.qLD, T.w + L.qLDinv);
+  wave_signal(fm, sid);
+  return eul && euler_damped(m, T);
+}
+__device__ inline void euler_factor_rows(const auto& m, const auto& L, const auto& X, const Team& T) {
+  const int nv = m.nv;
+  const real* qM = T.w + L.qM;
+  real* s = T.w + L.s_euler;
+  real *qH = s + nv, *qHLD = s + nv + nv * nv, *qHinv = s + nv + 2 * nv * nv;
+  FOR_T(e, nv * nv) {
+    int i = e / nv, j = e % nv;
+    real v = qM[e];
+    if (i == j) v += m.opt_timestep * m.dof_damping[i];
+    qH[e] = v;
+  }
+  TSYNC();
+  factor_ld_rows(nv, X.pmask, T.tid, qH, qHLD, qHinv);
+}
+
+// the acceleration stage in phase 4 (beside the helpers), the factor of M
+// handed over by wave 2 and the factor of M + h D moved to phase 5: bit-exact
+// but measured slower (two factorizations in series on wave 2 cost more than
+// factor_ld_rows2's one pass), so off
+#ifndef ILQG_ACC_P4
+#define ILQG_ACC_P4 0
+#endif
 #ifndef ILQG_COLL_SPLIT
 #define ILQG_COLL_SPLIT 1
 #endif
@@ -3791,11 +4018,24 @@ __device__ inline void step_dual_split(const auto& m, const auto& L, const auto&
   STAMPB(36);
   const int ne5 = T.iw[L.nefc];
   const bool spec = ne5 > 0 && ne5 <= TEAM_SIZE && m.nv <= RMAX;
+  // the acceleration stage beside the helpers' phase-4 work (the factor of M
+  // handed over by wave 2 as soon as it is formed), or in phase 5
+  using MT4 = std::remove_cvref_t<decltype(m)>;
+  constexpr bool acc4 = ILQG_ACC_P4 && vel_regs_ok<MT4>() && euler_regs_ok<MT4>();
+  int* fm = T.ci + C.ibc + 3;  // the factor of M final (wave 2 -> primary)
+  bool acc_done = false;
+  bool euler_late = false;  // wave 2: the factor of M + h D left for phase 5
   if (A) {
     using MT = std::remove_cvref_t<decltype(m)>;
-    if constexpr (vel_regs_ok<MT>()) fwd_velocity_u<MT>(m, L, T);
+    if constexpr (vel_regs_ok<MT>() && ILQG_VEL_H) fwd_velocity_h<MT>(m, L, T);
+    else if constexpr (vel_regs_ok<MT>()) fwd_velocity_u<MT>(m, L, T);
     else fwd_velocity(m, L, C, T, 1);
     STAMP(6);
+    if constexpr (acc4) {
+      wave_wait(fm, sid);
+      acc_done = fwd_acceleration_u<MT>(m, L, X, T);
+      STAMP(7);
+    }
   } else if (B) {
     if (!rows_done) {
       mc_rows(m, L, C, T, nlim, T.iw[L.nefc]);
@@ -3804,18 +4044,28 @@ __device__ inline void step_dual_split(const auto& m, const auto& L, const auto&
     constraint_ref(m, L, T);
     TSYNC();
     STAMPB(37);
-    if (spec) newton_warm_prep(m, L, C, T);
+    if (spec) {
+      using MT = std::remove_cvref_t<decltype(m)>;
+      bool done_u = false;
+      if constexpr (StaticModel<MT>) {
+        if constexpr (ILQG_WARM_U && MT::nv <= RMAX) {
+          newton_warm_prep_u<MT::nv>(m, L, C, T);
+          done_u = true;
+        }
+      }
+      if (!done_u) newton_warm_prep(m, L, C, T);
+    }
     STAMPB(30);
   } else {
-    factor_m_and_euler(m, L, C, X, T, eul);
+    if constexpr (acc4) euler_late = factor_m_signal(m, L, C, X, T, eul, fm, sid);
+    else factor_m_and_euler(m, L, C, X, T, eul);
   }
   __syncthreads();
   STAMP(27);
   STAMPB(39);
   if (A) {
     using MT = std::remove_cvref_t<decltype(m)>;
-    bool acc_done = false;
-    if constexpr (vel_regs_ok<MT>() && euler_regs_ok<MT>()) acc_done = fwd_acceleration_u<MT>(m, L, X, T);
+    if constexpr (!acc4 && vel_regs_ok<MT>() && euler_regs_ok<MT>()) acc_done = fwd_acceleration_u<MT>(m, L, X, T);
     if (!acc_done) fwd_acceleration(m, L, X, T, true);
     STAMP(7);
     if (spec) {
@@ -3831,6 +4081,8 @@ __device__ inline void step_dual_split(const auto& m, const auto& L, const auto&
     // prefetched record) runs here, where wave 1 has slack, so its loads have
     // landed long before
     if (B && !bad) late();
+    // wave 2: the factor of M + h D, read by the integrator in phase 6
+    if (!B && euler_late) euler_factor_rows(m, L, X, T);
     STAMPB(38);
   }
   __syncthreads();
@@ -3942,7 +4194,17 @@ __device__ inline void step_dual(const auto& m, const auto& L, const auto& C, co
     }
     STAMP(8);
   } else {
-    if (spec) newton_warm_prep(m, L, C, T);
+    if (spec) {
+      using MT = std::remove_cvref_t<decltype(m)>;
+      bool done_u = false;
+      if constexpr (StaticModel<MT>) {
+        if constexpr (ILQG_WARM_U && MT::nv <= RMAX) {
+          newton_warm_prep_u<MT::nv>(m, L, C, T);
+          done_u = true;
+        }
+      }
+      if (!done_u) newton_warm_prep(m, L, C, T);
+    }
     STAMPB(30);
     __syncthreads();
     if (eul) euler_prefactor(m, L, C, X, T);
