@@ -12,9 +12,8 @@ shift 2
 mkdir -p $OUT
 LIB=ilqg-mujoco_amd/lib
 if [ "$TESTLIB" != "-" ]; then
-  timeout -k 10 900 env ILQG_LIB=$TESTLIB python -u -m pytest tests/test_gpu_parity.py tests/test_layout.py -m gpu -x -q \
+  timeout -k 10 900 env ILQG_LIB=$TESTLIB python -u -m pytest tests -m gpu -x -q \
     --timeout 300 --timeout-method thread \
-    -k "iterate or bench_workload or step_batch or linesearch or cfg4 or edge or corrected or set_value or multiseed or humanoid or fixed_gain or forward" \
     > $OUT/tests.log 2>&1 || { echo "tests failed"; tail -30 $OUT/tests.log; exit 1; }
   tail -3 $OUT/tests.log
 fi
