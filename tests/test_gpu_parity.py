@@ -402,7 +402,8 @@ def test_riccati_mfma_step(ia, fixture):
 
 
 @pytest.mark.parametrize("env", [{}, {"ILQG_FUSED": "0"}, {"ILQG_PLAN": "1"}, {"ILQG_FD_HALVES": "1"},
-                                 {"ILQG_FD_SNAP": "0"}, {"ILQG_FD_HALVES": "1", "ILQG_FD_SNAP": "0"}])
+                                 {"ILQG_FD_SNAP": "0"}, {"ILQG_FD_HALVES": "1", "ILQG_FD_SNAP": "0"},
+                                 {"ILQG_FD_PRIO1": "500", "ILQG_FD_PRIO2": "800"}])
 def test_fused_sweep_schedules(ia, ora, env, monkeypatch):
     """The fused FD sweep + streamed backward pass (k_fd_fused_g), the
     two-kernel sweep (ILQG_FUSED=0), the fused sweep with its tickets in the
