@@ -270,18 +270,40 @@ FP64_MFMA_PEAK_TFS = 78.6  # AMD spec, FP64 matrix (v_mfma_f64_16x16x4_f64); the
 def run_humanoid_cfg5(args, world, rank, local_rank):
     """BASELINE.json configs[4]: humanoid, H = 200, one seed (qpos0 with the
     root at z = 1.4, humanoid.xml:49-50), fp32 FD (eps 1e-3) with the fp64
-    Riccati recursion on the matrix cores (ilqg_solver_set_riccati MFMA).  A
-    single seed does not shard: at N > 1 every rank runs a replica and value
-    sums them.  A separate line, not the headline."""
+    Riccati recursion on the matrix cores (ilqg_solver_set_riccati MFMA).  On
+    N > 1 GPUs the one seed's FD sweep is point-sharded (--cfg5-shard points,
+    the default): every rank rolls out the same trajectory, differentiates its
+    block of the H + 1 points (ilqg_fd_sweep_range), one RCCL all-gather of the
+    fp64 records (RecordExchange, 3.4 MB) gives every rank all of them, and
+    every rank runs the recursion; value = iterations/s of that one seed
+    (strong scaling).  --cfg5-shard replicas runs N independent replicas
+    instead.  A separate line, not the headline."""
     H = 200
+    P = H + 1
     m = ia.Model.load(workloads.model_file("humanoid"))
     st = m.reset_state(1)
     st.qpos[0, 2] = 1.4
     g = ia.ILQR(m, st, H, ia.HUMANOID_COST, device=local_rank)
     g.set_riccati("mfma")
     g.set_fd_precision("f32")
+    shard = world > 1 and args.cfg5_shard == "points"
+    if shard:
+        from seed_shard import RecordExchange
+        stream = torch.cuda.Stream()
+        g.set_stream(stream.cuda_stream)
+        rx = RecordExchange.for_solver(g, rank, world)
+
+        def one_iter():
+            with torch.cuda.stream(stream):
+                g.forward_pass()
+                g.fd_sweep_range(rx.p0, rx.np)
+                rx.exchange()
+                g.riccati_pass()
+    else:
+        def one_iter():
+            g.iterate()
     for _ in range(args.warmup):
-        g.iterate()
+        one_iter()
     g.synchronize()
     if world > 1:
         dist.barrier()
@@ -290,7 +312,7 @@ def run_humanoid_cfg5(args, world, rank, local_rank):
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        g.iterate()
+        one_iter()
     g.synchronize()
     torch.cuda.synchronize()
     if world > 1:
@@ -303,22 +325,27 @@ def run_humanoid_cfg5(args, world, rank, local_rank):
     fd_ms = sum(kt[k]["avg_ms"] for k in ("fd_centre", "fd_cols") if k in kt)
     bw_ms = kt.get("backward", {}).get("avg_ms", 0.0)
     roll_ms = kt.get("rollout", {}).get("avg_ms", 0.0)
-    fd_tf = P * hf["fd_point"]["flops"] / (fd_ms * 1e-3) / 1e12 if fd_ms else 0.0
+    fd_pts = rx.np if shard else P  # points this rank's FD launch differentiates
+    fd_tf = fd_pts * hf["fd_point"]["flops"] / (fd_ms * 1e-3) / 1e12 if fd_ms else 0.0
     bw_tf = H * hf["riccati_step"]["flops"] / (bw_ms * 1e-3) / 1e12 if bw_ms else 0.0
-    value = world * args.steps / elapsed
+    value = (1 if shard else world) * args.steps / elapsed
     out = {
-        "metric": CFG5_METRIC, "value": value, "unit": "iLQR iterations/s (1 seed per GPU, replicas summed)",
+        "metric": CFG5_METRIC, "value": value,
+        "unit": "iLQR iterations/s (one seed, FD point-sharded over the GPUs)" if shard else
+                "iLQR iterations/s (1 seed per GPU, replicas summed)",
         "n_gpus": world, "steps": args.steps, "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3,
-        "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+        "higher_is_better": True, "scaling": "strong" if shard else "weak", "vs_baseline": None,
         "dtype": "f32 (FD sweep) / f64 (rollout, Riccati)",
         "data": "synthetic (humanoid qpos0, root z = 1.4, qvel 0; state-only quadratic cost)",
         "config": {"workload": "humanoid_H200_cfg5", "model": "humanoid.xml", "horizon": H, "seeds_per_gpu": 1,
                    "fd_precision": "f32 (eps 1e-3)", "riccati": "fp64 MFMA (v_mfma_f64_16x16x4_f64)",
-                   "parallelism": f"replicas x{world} (a single seed does not shard)"},
+                   "parallelism": (f"FD point-sharded x{world} (RCCL all-gather of the fp64 records, "
+                                   f"{P * g.device_deriv()[1] * 8 / 1e6:.1f} MB per iteration)") if shard else
+                                  f"replicas x{world}"},
         "kernels": kt,
         "roofline": {
             "rollout": {"bound": "latency", "us_per_step": roll_ms / P * 1e3},
-            "fd_sweep": {"bound": "fp32-valu", "flops_per_launch": P * hf["fd_point"]["flops"],
+            "fd_sweep": {"bound": "fp32-valu", "flops_per_launch": fd_pts * hf["fd_point"]["flops"],
                          "avg_launch_ms": fd_ms, "achieved_tflops": fd_tf, "peak_tflops": FP32_PEAK_TFS,
                          "frac": fd_tf / FP32_PEAK_TFS,
                          "flops_source": "tests/fixtures/flops.json (instrumented oracle, fp64 op count)"},
@@ -353,6 +380,8 @@ def main():
     ap.add_argument("--dry-run", action="store_true")
     # the headline (cfg 4's per-GPU share) or cfg 5 as a separate line
     ap.add_argument("--workload", choices=("hopper_cfg4", "humanoid_cfg5"), default="hopper_cfg4")
+    # cfg 5 on N > 1 GPUs: the one seed's FD sweep point-sharded, or N replicas
+    ap.add_argument("--cfg5-shard", choices=("points", "replicas"), default="points")
     argv = sys.argv[1:]
     args = ap.parse_args(argv)
 

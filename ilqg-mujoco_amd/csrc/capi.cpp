@@ -251,11 +251,19 @@ struct ilqg_solver {
   hipStream_t stream = nullptr;
   DevBuf traj[5], cand[5], dinit[5];
   DevBuf qfrc_applied, xfrc_applied, K, k, deriv, warm_c, cost_c, V, v, cost_cand, cost_sel, sel, alphas, cost;
-  DevBuf cw, sync, fault, plan_dur, plan_order;
+  DevBuf cw, sync, fault, plan_dur, plan_order, plan_pos;
   DevBuf snap;  // the centre teams' position/velocity workspace per point (FdFused.snap)
   int snapd = 0;
   DevBuf xq;    // the column halves' qacc exchange (FdFused.halves)
   int halves = 0;
+  // schedule knobs, read once at creation (ILQG_FD_SNAP, ILQG_PLAN, ILQG_PLAN_K,
+  // ILQG_PLAN_P0): the launch and the debug_plan hook use the same values
+  bool snap_on = true, snap_poison = false, plan_on = false;
+  float plan_k = 3.0f;
+  int plan_p0 = 8;
+  // debug_plant_schedule: one-shot (slot, item) pairs written into the next
+  // fused launch's ticket map before it is validated
+  std::vector<std::pair<unsigned, unsigned>> plants;
   std::vector<double> host_alphas;
   bool initialized = false;
   hipStream_t own_stream = nullptr;
@@ -644,14 +652,23 @@ int ilqg_solver_create(const ilqg_model* mc, const ilqg_solver_opts* o, const il
     ALLOC(s->sync, sync_bytes(S * P, ntm));
     // every column as two items (FdFused.halves): the qacc exchange
     s->halves = getenv_int("ILQG_FD_HALVES", 0) ? 1 : 0;  // opt-in: measured slower
-    ALLOC(s->xq, S * P * ntm * 2 * (size_t)h.nv * 8);
-    // the ticket schedule and the per-item durations it is planned from (zero: no history)
+    if (s->halves) ALLOC(s->xq, S * P * ntm * 2 * (size_t)h.nv * 8);
+    // the ticket schedule, the per-item durations it is planned from (zero: no
+    // history) and the validator's scratch
     const size_t items = S * P * (1 + (s->halves ? 2 : 1) * ntm);
     ALLOC(s->plan_dur, items * 4);
     ALLOC(s->plan_order, items * 4);
-    const ilqg_model* mm = s->model;
-    s->snapd = round16(mm->Lc.nd + mm->C.nd + (mm->Lc.ni + mm->C.ni + 1) / 2);
-    ALLOC(s->snap, S * P * (size_t)s->snapd * 8);
+    ALLOC(s->plan_pos, items * 4);
+    s->plan_on = getenv_int("ILQG_PLAN", 0) != 0;
+    if (const char* pk = getenv("ILQG_PLAN_K")) s->plan_k = (float)atof(pk);
+    s->plan_p0 = getenv_int("ILQG_PLAN_P0", 8);
+    s->snap_on = getenv_int("ILQG_FD_SNAP", 1) != 0;
+    s->snap_poison = getenv_int("ILQG_SNAP_POISON", 0) != 0;  // tests: see FdFused.poison
+    if (s->snap_on) {
+      const ilqg_model* mm = s->model;
+      s->snapd = round16(mm->Lc.nd + mm->C.nd + (mm->Lc.ni + mm->C.ni + 1) / 2);
+      ALLOC(s->snap, S * P * (size_t)s->snapd * 8);
+    }
   }
   ALLOC(s->fault, 16);
   ALLOC(s->warm_c, S * P * h.nv * 8);
@@ -763,6 +780,14 @@ int ilqg_solver_get_deriv(ilqg_solver* s, double* deriv) {
   return ILQG_OK;
 }
 
+int ilqg_solver_get_deriv_point(ilqg_solver* s, int seed, int point, double* deriv) {
+  if (!s || !deriv || seed < 0 || seed >= s->S || point < 0 || point >= s->P) return fail(ILQG_ERR_ARG, "bad argument");
+  HIPCHK(s->sync_all());
+  HIPCHK(hipMemcpy(deriv, s->deriv.as<double>() + ((size_t)seed * s->P + point) * s->Dp, (size_t)s->D * 8,
+                   hipMemcpyDeviceToHost));
+  return ILQG_OK;
+}
+
 int ilqg_solver_set_deriv(ilqg_solver* s, const double* deriv) {
   if (!s || !deriv) return fail(ILQG_ERR_ARG, "bad argument");
   HIPCHK(s->sync_all());
@@ -870,9 +895,10 @@ static hipError_t fused_launch(ilqg_solver* s, const SeedRange& r, int mode) {
     a.prio1 = p1 > 0 ? (unsigned)((unsigned long long)nit * p1 / 1000) : ~0u;
     a.prio2 = p2 > 0 ? (unsigned)((unsigned long long)nit * p2 / 1000) : ~0u;
   }
-  if (s->snap.p && getenv_int("ILQG_FD_SNAP", 1)) {
+  if (s->snap.p && s->snap_on) {
     a.snap = s->snap.as<double>() + s0 * P * (size_t)s->snapd;
     a.snapd = s->snapd;
+    a.poison = s->snap_poison ? 1 : 0;
   }
   if (s->halves) {
     a.halves = 1;
@@ -882,16 +908,36 @@ static hipError_t fused_launch(ilqg_solver* s, const SeedRange& r, int mode) {
   // ticket schedule from the previous launch's item durations: opt-in
   // (ILQG_PLAN=1); measured slower than the point-major order on the bench
   // workload ("Fused sweep ticket schedule")
-  if (s->plan_dur.p && getenv_int("ILQG_PLAN", 0)) {
-    static const float kthr = [] {
-      const char* e = getenv("ILQG_PLAN_K");
-      return e ? (float)atof(e) : 3.0f;
-    }();
-    e = launch_fd_plan(r.ns, s->P, (s->halves ? 2 : 1) * (s->nut + 2 * h.nv), getenv_int("ILQG_PLAN_P0", 8), kthr,
-                       s->plan_dur.as<unsigned>(), s->plan_order.as<unsigned>(), r.st);
+  // Every map the sweep reads is validated first (launch_fd_order_check): an
+  // invalid one is replaced by the identity and reported by ilqg_synchronize.
+  const int nt = (s->halves ? 2 : 1) * (s->nut + 2 * h.nv);
+  if (s->plan_dur.p && (s->plan_on || !s->plants.empty())) {
+    if (s->plan_on) {
+      e = launch_fd_plan(r.ns, s->P, nt, s->plan_p0, s->plan_k, s->plan_dur.as<unsigned>(),
+                         s->plan_order.as<unsigned>(), r.st);
+      if (e != hipSuccess) return e;
+      a.dur = s->plan_dur.as<unsigned>();
+    } else {
+      std::vector<unsigned> id((size_t)r.ns * P * (1 + nt));
+      for (size_t u = 0; u < id.size(); u++) id[u] = (unsigned)u;
+      e = hipMemcpyAsync(s->plan_order.p, id.data(), id.size() * 4, hipMemcpyHostToDevice, r.st);
+      if (e != hipSuccess) return e;
+      e = hipStreamSynchronize(r.st);  // id is a host temporary
+      if (e != hipSuccess) return e;
+    }
+    for (const auto& pl : s->plants) {
+      e = hipMemcpyAsync(s->plan_order.as<unsigned>() + pl.first, &pl.second, 4, hipMemcpyHostToDevice, r.st);
+      if (e != hipSuccess) return e;
+    }
+    if (!s->plants.empty()) {
+      e = hipStreamSynchronize(r.st);
+      s->plants.clear();
+      if (e != hipSuccess) return e;
+    }
+    e = launch_fd_order_check(r.ns, s->P, nt, s->plan_order.as<unsigned>(), s->plan_pos.as<unsigned>(),
+                              s->fault.as<unsigned>(), r.st);
     if (e != hipSuccess) return e;
     a.order = s->plan_order.as<unsigned>();
-    a.dur = s->plan_dur.as<unsigned>();
   }
   return launch_fd_fused_coop(m->dm, m->Lc, m->C, m->X, a, r.st);
 }
@@ -923,6 +969,51 @@ int ilqg_fd_sweep(ilqg_solver* s) {
                                s->xfrc_applied.as<double>(), s->cview(), s->warm_c.as<double>(),
                                s->cost_c.as<double>(), s->deriv.as<double>(), s->Dp, s->stream);
   }));
+  return ILQG_OK;
+}
+
+// calcMJDerivatives at points p0 .. p0 + np - 1 of every seed: the share of
+// one rank in a point-sharded sweep (a single seed's FD sweep spread over
+// GPUs; the records are then all-gathered and every rank runs the recursion).
+// The unfused kernels of the solver's FD precision, one launch pair per seed;
+// the same records the whole-trajectory sweep writes.
+int ilqg_fd_sweep_range(ilqg_solver* s, int p0, int np) {
+  if (!s || !s->initialized) return fail(ILQG_ERR_ARG, "solver not initialised");
+  if (p0 < 0 || np < 0 || p0 + np > s->P) return fail(ILQG_ERR_ARG, "point range outside the trajectory");
+  if (!np) return ILQG_OK;
+  const ilqg_model* m = s->model;
+  const HostModel& h = m->host;
+  constexpr int kOneSeed = 1 << 30;  // the kernels' seed index pt / P is 0 for every point of the range
+  HIPCHK(s->timed(3, [&] {
+    for (int sd = 0; sd < s->S; sd++) {
+      const size_t pt0 = (size_t)sd * s->P + p0;
+      const TrajDev nom = toff(s->tview(s->traj), pt0, h);
+      const double* qa = s->qfrc_applied.as<double>() + (size_t)sd * h.nv;
+      const double* xa = s->xfrc_applied.as<double>() + (size_t)sd * 6 * h.nbody;
+      double* wc = s->warm_c.as<double>() + pt0 * h.nv;
+      double* cc = s->cost_c.as<double>() + pt0;
+      double* dv = s->deriv.as<double>() + pt0 * s->Dp;
+      hipError_t e;
+      if (s->fdprec == ILQG_FD_F32) {
+        e = launch_fd_sweep_f32(m->dm, m->Lc, m->C, m->X, nom, np, kOneSeed, qa, xa, s->cview(), wc, cc, dv, s->Dp,
+                                ILQG_FD32_EPS, s->stream);
+      } else {
+        e = launch_fd_centre_coop(m->dm, m->Lc, m->C, m->X, nom, np, kOneSeed, qa, xa, s->cview(), wc, cc, s->stream);
+        if (e == hipSuccess)
+          e = launch_fd_cols_coop(m->dm, m->Lc, m->C, m->X, nom, np, kOneSeed, qa, xa, s->cview(), wc, cc, dv, s->Dp,
+                                  s->stream);
+      }
+      if (e != hipSuccess) return e;
+    }
+    return hipSuccess;
+  }));
+  return ILQG_OK;
+}
+
+int ilqg_solver_device_deriv(ilqg_solver* s, double** dptr, int* stride) {
+  if (!s || !dptr) return fail(ILQG_ERR_ARG, "bad argument");
+  *dptr = s->deriv.as<double>();
+  if (stride) *stride = s->Dp;
   return ILQG_OK;
 }
 
@@ -965,6 +1056,9 @@ int ilqg_synchronize(ilqg_solver* s) {
   if (flt) {
     // reported once: cleared by the read (the next launch waits normally)
     HIPCHK(hipMemset(s->fault.p, 0, 4));
+    if (flt == 2u)
+      return fail(ILQG_ERR_HIP, "fused FD sweep: invalid ticket schedule (item out of range, repeated, or a column "
+                                "before its centre); the sweep ran in the identity order");
     return fail(ILQG_ERR_HIP, "fused FD sweep: a hand-off wait timed out");
   }
   return ILQG_OK;
@@ -1010,12 +1104,26 @@ int ilqg_solver_debug_plan(ilqg_solver* s, unsigned* order, unsigned* dur, int* 
   *nitems = n;
   if (!n || (!order && !dur)) return ILQG_OK;
   HIPCHK(s->sync_all());
-  HIPCHK(launch_fd_plan(s->S, s->P, (s->halves ? 2 : 1) * (s->nut + 2 * h.nv), getenv_int("ILQG_PLAN_P0", 8), 3.0f,
-                        s->plan_dur.as<unsigned>(),
-                        s->plan_order.as<unsigned>(), s->stream));
+  HIPCHK(launch_fd_plan(s->S, s->P, (s->halves ? 2 : 1) * (s->nut + 2 * h.nv), s->plan_p0, s->plan_k,
+                        s->plan_dur.as<unsigned>(), s->plan_order.as<unsigned>(), s->stream));
   HIPCHK(s->sync_all());
   if (order) HIPCHK(hipMemcpy(order, s->plan_order.p, (size_t)n * 4, hipMemcpyDeviceToHost));
   if (dur) HIPCHK(hipMemcpy(dur, s->plan_dur.p, (size_t)n * 4, hipMemcpyDeviceToHost));
+  return ILQG_OK;
+}
+
+int ilqg_solver_debug_plant_schedule(ilqg_solver* s, unsigned slot, unsigned item) {
+  if (!s) return fail(ILQG_ERR_ARG, "null solver");
+  if (!s->plan_order.p) return fail(ILQG_ERR_UNSUPPORTED, "no fused sweep on this solver");
+  if ((size_t)slot >= s->plan_order.n / 4) return fail(ILQG_ERR_ARG, "slot out of range");
+  s->plants.emplace_back(slot, item);
+  return ILQG_OK;
+}
+
+int ilqg_solver_set_mu(ilqg_solver* s, double mu) {
+  if (!s || !(mu == mu)) return fail(ILQG_ERR_ARG, "bad argument");
+  HIPCHK(s->sync_all());  // launches already enqueued keep the value they were given
+  s->opts.mu = mu;
   return ILQG_OK;
 }
 

@@ -21,10 +21,11 @@ struct Team {
 // workgroup 0, lane 0, accumulated in LDS (a global read-modify-write per
 // stamp would itself wait on memory) and flushed once at kernel end
 #ifdef ILQG_STAMPS
-#define STAMP_N 44
+#define STAMP_N 60  // ids 0..43 waves 0 and 1, 48..59 wave 2 (44..47: per-kernel counters)
+#define STAMP_NG 64
 // (per translation unit: the rollout and the FD kernels each read their own copy)
-static __device__ unsigned long long g_stamp_acc[48];
-static __device__ unsigned long long g_stamp_cnt[48];
+static __device__ unsigned long long g_stamp_acc[STAMP_NG];
+static __device__ unsigned long long g_stamp_cnt[STAMP_NG];
 static __device__ unsigned long long g_newton_iters;  // all workgroups: Newton iterations
 static __device__ unsigned long long g_newton_calls;  // all workgroups: solver calls
 // line searches of the wave-parallel Newton solver: [0] calls, [1] iterations,
@@ -57,7 +58,7 @@ __device__ __forceinline__ void cnt_flush() {
 #define ILQG_STAMP_SAMPLE 0
 #endif
 #define STAMP_BLOCK() ((blockIdx.x & ((1u << ILQG_STAMP_SAMPLE) - 1u)) == 0)
-__shared__ unsigned long long s_stamp_acc[STAMP_N], s_stamp_cnt[STAMP_N], s_stamp_prev, s_stamp_prevb;
+__shared__ unsigned long long s_stamp_acc[STAMP_N], s_stamp_cnt[STAMP_N], s_stamp_prev, s_stamp_prevb, s_stamp_prevc;
 #define STAMP_AT(lane, prev, id)                                             \
   do {                                                                       \
     if (threadIdx.x == (lane) && STAMP_BLOCK()) {                            \
@@ -72,13 +73,15 @@ __shared__ unsigned long long s_stamp_acc[STAMP_N], s_stamp_cnt[STAMP_N], s_stam
 // wave 0 lane 0; STAMPB: lane 0 of the helper wave of a two-wave team
 #define STAMP(id) STAMP_AT(0, s_stamp_prev, id)
 #define STAMPB(id) STAMP_AT(64, s_stamp_prevb, id)
+// STAMPC: lane 0 of the third wave of a three-wave team (ids 48..59)
+#define STAMPC(id) STAMP_AT(128, s_stamp_prevc, id)
 #define STAMP_INIT()                                                         \
   do {                                                                       \
     if (threadIdx.x == 0) {                                                  \
       for (int i_ = 0; i_ < 10; i_++) s_cnt[i_] = 0;                         \
       if (STAMP_BLOCK()) {                                                   \
         for (int i_ = 0; i_ < STAMP_N; i_++) s_stamp_acc[i_] = s_stamp_cnt[i_] = 0; \
-        s_stamp_prev = s_stamp_prevb = __builtin_amdgcn_s_memtime();         \
+        s_stamp_prev = s_stamp_prevb = s_stamp_prevc = __builtin_amdgcn_s_memtime();         \
       }                                                                      \
     }                                                                        \
   } while (0)
@@ -102,6 +105,7 @@ __shared__ unsigned long long s_stamp_acc[STAMP_N], s_stamp_cnt[STAMP_N], s_stam
   do {            \
   } while (0)
 #define STAMPB(id) STAMP(id)
+#define STAMPC(id) STAMP(id)
 #define STAMP_INIT() STAMP(-1)
 #define STAMP_FLUSH() STAMP(-1)
 #endif
@@ -1006,9 +1010,26 @@ __device__ inline void crb_u(const auto& m, const auto& L, const auto& C, const 
 }
 
 // tree L'DL (oracle factor_ld), parallel over ancestor pairs for each k
+// compile-time models small enough for factor_ld_lanes (nv <= RMAX: the
+// register-row models); ILQG_FLD_LANES=0 keeps the register-row broadcasts
+#ifndef ILQG_FLD_LANES
+#define ILQG_FLD_LANES 1
+#endif
+template <class MT>
+constexpr bool fld_lanes_ok() {
+  if constexpr (StaticModel<MT> && ILQG_FLD_LANES) return MT::nv <= RMAX;
+  return false;
+}
 __device__ inline void factor_ld(const auto& m, const auto& X, const Team& T, const real* mat, real* LD,
                                  real* diaginv, real* tmpv) {
   const int nv = m.nv;
+  using MT = std::remove_cvref_t<decltype(m)>;
+  if constexpr (fld_lanes_ok<MT>()) {
+    // compile-time tree: the factor serially in lane 0's registers
+    const real zero[MT::nv] = {};
+    factor_ld_lanes<std::remove_cvref_t<decltype(X)>, MT::nv>(T.tid, mat, zero, false, LD, diaginv, 0, 0);
+    return;
+  }
   if (nv <= RMAX && has_pmask(X)) {
     factor_ld_rows(nv, X.pmask, T.tid, mat, LD, diaginv);
     return;
@@ -3832,6 +3853,23 @@ __device__ inline void factor_m_and_euler(const auto& m, const auto& L, const au
   }
   real* s = T.w + L.s_euler;
   real *qH = s + nv, *qHLD = s + nv + nv * nv, *qHinv = s + nv + 2 * nv * nv;
+  using MT = std::remove_cvref_t<decltype(m)>;
+  if constexpr (fld_lanes_ok<MT>()) {
+    // lane 0 factors M, lane 1 M + h D (its diagonal formed in registers as
+    // euler_prefactor forms it; the matrix itself is read by nothing else)
+    constexpr int NV = MT::nv;
+    real add[NV];
+    sfor<0, NV>(SLAM(ii) { add[SK(ii)] = m.opt_timestep * m.dof_damping[SK(ii)]; });
+#ifdef ILQG_ASM_MARK
+    asm volatile(";;MARK_F2_BEGIN" ::: "memory");
+#endif
+    factor_ld_lanes<std::remove_cvref_t<decltype(X)>, NV>(T.tid, qM, add, true, T.w + L.qLD, T.w + L.qLDinv,
+                                                          (int)(qHLD - (T.w + L.qLD)), (int)(qHinv - (T.w + L.qLDinv)));
+#ifdef ILQG_ASM_MARK
+    asm volatile(";;MARK_F2_END" ::: "memory");
+#endif
+    return;
+  }
   FOR_T(e, nv * nv) {
     int i = e / nv, j = e % nv;
     real v = qM[e];
@@ -3839,7 +3877,13 @@ __device__ inline void factor_m_and_euler(const auto& m, const auto& L, const au
     qH[e] = v;
   }
   TSYNC();
+#ifdef ILQG_ASM_MARK
+  asm volatile(";;MARK_F2_BEGIN" ::: "memory");
+#endif
   factor_ld_rows2(nv, X.pmask, T.tid, qM, T.w + L.qLD, T.w + L.qLDinv, qH, qHLD, qHinv);
+#ifdef ILQG_ASM_MARK
+  asm volatile(";;MARK_F2_END" ::: "memory");
+#endif
 }
 
 // factor_m_and_euler split for the three-wave step: the factor of M, announced
@@ -3885,6 +3929,9 @@ __device__ inline void euler_factor_rows(const auto& m, const auto& L, const aut
 #ifndef ILQG_COLL_SPLIT
 #define ILQG_COLL_SPLIT 1
 #endif
+#ifndef ILQG_SPLIT3
+#define ILQG_SPLIT3 1
+#endif
 // pairs (compile-time aux) with a plane geom: bit p
 template <class MT, class XT>
 constexpr unsigned long long plane_pair_mask() {
@@ -3929,6 +3976,7 @@ __device__ inline void step_dual_split(const auto& m, const auto& L, const auto&
   const bool eul = m.opt_integrator != 1;
   STAMP(-1);
   STAMPB(-1);
+  STAMPC(-1);
   const bool bad = any_bad(T, C, T.w + L.qpos, m.nq) || any_bad(T, C, T.w + L.qvel, m.nv);
   if (bad) {
     if (B) {
@@ -3951,6 +3999,7 @@ __device__ inline void step_dual_split(const auto& m, const auto& L, const auto&
     if (T.tid == 0) *nlim_sh = nl;
     passive_forces(m, L, T);
     if constexpr (ksplit) kinematics_frames(m, L, T, fq, ff, sid);
+    STAMPC(48);
   } else {
     if (!bad) pre();
     STAMPB(41);
@@ -3963,6 +4012,7 @@ __device__ inline void step_dual_split(const auto& m, const auto& L, const auto&
   const int nlim = *nlim_sh;
   STAMP(24);
   STAMPB(32);
+  STAMPC(49);
   if (A) {
     using MT = std::remove_cvref_t<decltype(m)>;
     if constexpr (StaticModel<MT> && ILQG_COM_U) com_pos_u<MT>(m, L, T);
@@ -3981,6 +4031,7 @@ __device__ inline void step_dual_split(const auto& m, const auto& L, const auto&
       if (mine) collision_pair(m, L, C, X, T, T.tid);
       if (!B) {
         wave_signal(fc, sid);
+        STAMPC(50);
       } else {
         wave_wait(fc, sid);
         collision_finish(m, L, C, X, T);
@@ -3994,7 +4045,16 @@ __device__ inline void step_dual_split(const auto& m, const auto& L, const auto&
   __syncthreads();
   STAMP(25);
   STAMPB(34);
+  STAMPC(51);
   bool rows_done = false;
+  // ILQG_SPLIT3 (the register-row models): the velocity stage, which reads only
+  // com_pos's outputs (cdof, cinert) and the state, runs on wave 2 beside crb;
+  // wave 1 forms the constraint rows and their reference accelerations here
+  // too.  Phase 4 is then the primary's factors of M and M + h D and its
+  // acceleration stage beside wave 1's Newton warm start.
+  using MT3 = std::remove_cvref_t<decltype(m)>;
+  constexpr bool split3 = ILQG_SPLIT3 && !ILQG_ACC_P4 && StaticModel<MT3> && ILQG_VEL_H && vel_regs_ok<MT3>() &&
+                          euler_regs_ok<MT3>();
   if (A) {
     using MT = std::remove_cvref_t<decltype(m)>;
     if constexpr (StaticModel<MT> && ILQG_COM_U) crb_u<MT>(m, L, C, X, T);
@@ -4011,11 +4071,29 @@ __device__ inline void step_dual_split(const auto& m, const auto& L, const auto&
       TSYNC();
       rows_done = true;
     }
-    STAMPB(35);
+    if constexpr (split3) {
+      if (!rows_done) {
+        mc_rows(m, L, C, T, nlim, T.iw[L.nefc]);
+        TSYNC();
+        rows_done = true;
+      }
+      STAMPB(35);
+      constraint_ref(m, L, T);
+      TSYNC();
+      STAMPB(37);
+    } else {
+      STAMPB(35);
+    }
+  } else {
+    if constexpr (split3) {
+      fwd_velocity_h<MT3>(m, L, T);
+      STAMPC(57);
+    }
   }
   __syncthreads();
   STAMP(26);
   STAMPB(36);
+  STAMPC(52);
   const int ne5 = T.iw[L.nefc];
   const bool spec = ne5 > 0 && ne5 <= TEAM_SIZE && m.nv <= RMAX;
   // the acceleration stage beside the helpers' phase-4 work (the factor of M
@@ -4027,23 +4105,32 @@ __device__ inline void step_dual_split(const auto& m, const auto& L, const auto&
   bool euler_late = false;  // wave 2: the factor of M + h D left for phase 5
   if (A) {
     using MT = std::remove_cvref_t<decltype(m)>;
-    if constexpr (vel_regs_ok<MT>() && ILQG_VEL_H) fwd_velocity_h<MT>(m, L, T);
-    else if constexpr (vel_regs_ok<MT>()) fwd_velocity_u<MT>(m, L, T);
-    else fwd_velocity(m, L, C, T, 1);
-    STAMP(6);
-    if constexpr (acc4) {
-      wave_wait(fm, sid);
+    if constexpr (split3) {
+      factor_m_and_euler(m, L, C, X, T, eul);
+      STAMP(3);
       acc_done = fwd_acceleration_u<MT>(m, L, X, T);
       STAMP(7);
+    } else {
+      if constexpr (vel_regs_ok<MT>() && ILQG_VEL_H) fwd_velocity_h<MT>(m, L, T);
+      else if constexpr (vel_regs_ok<MT>()) fwd_velocity_u<MT>(m, L, T);
+      else fwd_velocity(m, L, C, T, 1);
+      STAMP(6);
+      if constexpr (acc4) {
+        wave_wait(fm, sid);
+        acc_done = fwd_acceleration_u<MT>(m, L, X, T);
+        STAMP(7);
+      }
     }
   } else if (B) {
-    if (!rows_done) {
-      mc_rows(m, L, C, T, nlim, T.iw[L.nefc]);
+    if constexpr (!split3) {
+      if (!rows_done) {
+        mc_rows(m, L, C, T, nlim, T.iw[L.nefc]);
+        TSYNC();
+      }
+      constraint_ref(m, L, T);
       TSYNC();
+      STAMPB(37);
     }
-    constraint_ref(m, L, T);
-    TSYNC();
-    STAMPB(37);
     if (spec) {
       using MT = std::remove_cvref_t<decltype(m)>;
       bool done_u = false;
@@ -4058,16 +4145,19 @@ __device__ inline void step_dual_split(const auto& m, const auto& L, const auto&
     STAMPB(30);
   } else {
     if constexpr (acc4) euler_late = factor_m_signal(m, L, C, X, T, eul, fm, sid);
-    else factor_m_and_euler(m, L, C, X, T, eul);
+    else if constexpr (!split3) factor_m_and_euler(m, L, C, X, T, eul);
+    STAMPC(53);
   }
   __syncthreads();
   STAMP(27);
   STAMPB(39);
+  STAMPC(54);
   if (A) {
     using MT = std::remove_cvref_t<decltype(m)>;
-    if constexpr (!acc4 && vel_regs_ok<MT>() && euler_regs_ok<MT>()) acc_done = fwd_acceleration_u<MT>(m, L, X, T);
+    if constexpr (!acc4 && !split3 && vel_regs_ok<MT>() && euler_regs_ok<MT>())
+      acc_done = fwd_acceleration_u<MT>(m, L, X, T);
     if (!acc_done) fwd_acceleration(m, L, X, T, true);
-    STAMP(7);
+    if constexpr (!split3) STAMP(7);
     if (spec) {
       fwd_constraint_fast(m, L, C, X, T, m.opt_iterations, m.opt_tolerance, true);
     } else {
@@ -4088,6 +4178,7 @@ __device__ inline void step_dual_split(const auto& m, const auto& L, const auto&
   __syncthreads();
   STAMP(29);
   STAMPB(43);
+  STAMPC(55);
   if (A) {
     bool reset = false;
     if (any_bad(T, C, T.w + L.qacc, m.nv)) {
@@ -4109,6 +4200,7 @@ __device__ inline void step_dual_split(const auto& m, const auto& L, const auto&
   __syncthreads();
   STAMP(28);
   STAMPB(40);
+  STAMPC(56);
 }
 
 // mj_step by a two-wave team (rollout kernels): wave 0 runs the dependency

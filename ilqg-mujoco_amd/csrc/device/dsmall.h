@@ -257,6 +257,64 @@ __device__ inline void factor_ld_rows2(int nv, const auto& pmask, int tid, const
   team_sync();
 }
 
+// Tree L'DL factorization with compile-time sparsity (XT::pmask[k]: proper
+// ancestors of dof k), one matrix per lane, wholly in that lane's registers:
+// lane 0 factors mat into (LD0, diaginv0); with `two`, lane 1 factors
+// mat + diag(add) into (LD0 + o1, diaginv0 + od1) -- the Euler matrix M + h D,
+// whose diagonal sum is formed here exactly as euler_prefactor forms it.
+// This is the oracle's serial loop (coop::factor_ld, oracle/mjsub.c factor_ld)
+// with every index a constant: no broadcasts, no lane-dependent branches, no
+// SGPR masks (factor_ld_rows2's two-half broadcasts and selects cost ~800
+// wave instructions for the hopper, three quarters of them v_readlane / v_mov /
+// v_cndmask; this is ~300, all arithmetic).  Same operations on the same
+// operands per entry; LD is written in full with a zero upper triangle.
+template <class XT, int NV, class R>
+__device__ inline void factor_ld_lanes(int tid, const R* mat, const R (&add)[NV], bool two, R* LD0, R* diaginv0,
+                                       int o1, int od1) {
+  const bool l1 = two && tid == 1;
+  R a[NV][NV];
+  sfor<0, NV>(SLAM(ii) {
+    constexpr int i = SK(ii);
+    sfor<0, i + 1>(SLAM(jj) { a[i][SK(jj)] = mat[i * NV + SK(jj)]; });
+  });
+  sfor<0, NV>(SLAM(ii) {
+    constexpr int i = SK(ii);
+    const R s = a[i][i] + add[i];
+    a[i][i] = l1 ? s : a[i][i];
+  });
+  team_sync();  // every lane has read mat before LD (may alias it) is written
+  sfor<0, NV>(SLAM(kk) {
+    constexpr int k = NV - 1 - SK(kk);
+    R dk = a[k][k];
+    if (dk < MINVAL) dk = MINVAL;
+    a[k][k] = dk;
+    sfor<0, k>(SLAM(ii) {
+      constexpr int i = k - 1 - SK(ii);
+      if constexpr ((XT::pmask[k] >> i) & 1) {
+        const R tmp = a[k][i] / dk;
+        sfor<0, i + 1>(SLAM(jj) {
+          constexpr int j = i - SK(jj);
+          if constexpr (j == i || ((XT::pmask[i] >> j) & 1)) a[i][j] -= tmp * a[k][j];
+        });
+        a[k][i] = tmp;
+      }
+    });
+  });
+  if (tid == 0 || l1) {
+    const int o = l1 ? o1 : 0, od = l1 ? od1 : 0;
+    sfor<0, NV>(SLAM(ii) {
+      constexpr int i = SK(ii);
+      sfor<0, NV>(SLAM(jj) {
+        constexpr int j = SK(jj);
+        if constexpr (j <= i) LD0[o + i * NV + j] = a[i][j];
+        else LD0[o + i * NV + j] = (R)0;
+      });
+      diaginv0[od + i] = 1 / a[i][i];
+    });
+  }
+  team_sync();
+}
+
 // x <- (L'DL)^-1 x for the factor above; mirrors coop::solve_ld.
 template <class R>
 __device__ inline void solve_ld_rows(int nv, const auto& pmask, int tid, const R* LD, const R* diaginv, R* x) {

@@ -90,11 +90,13 @@ struct FdFused {
   // s_setprio 1, >= prio2 at 2 (the backward roles run at 3); ~0u = never
   unsigned prio1 = ~0u, prio2 = ~0u;
   // the centre team's workspace after its position and velocity stages, per
-  // point ([S*P][snapd] doubles: the team's LDS doubles, then its ints), which
-  // the qvel and ctrl teams load instead of recomputing those stages; null =
-  // every team computes its own
+  // point ([S*P][snapd] doubles: the team's LDS ints, then the doubles the
+  // column teams read, kernels_fd.hip snap_ranges), which the qvel and ctrl
+  // teams load instead of recomputing those stages; null = every team
+  // computes its own
   double* snap = nullptr;
   int snapd = 0;
+  int poison = 0;  // tests (ILQG_SNAP_POISON): every double a snapshot does not carry reads as NaN
   // every column as two items, its + and - evaluations ([S*P][ntm][2][nv]
   // qacc exchange, [S*P][ntm] pair counters zeroed with sync); 0 = one item
   int halves = 0;
@@ -109,6 +111,10 @@ struct FdFused {
 // follows its centre team, so the deadlock argument is unchanged.
 hipError_t launch_fd_plan(int S, int P, int ntm, int p0, float kthr, const unsigned* dur, unsigned* order,
                           hipStream_t st);
+// validates a ticket -> item map (nt items per (seed, point) besides its
+// centre); replaces an invalid one by the identity and sets fault bit 1
+hipError_t launch_fd_order_check(int S, int P, int nt, unsigned* order, unsigned* pos, unsigned* fault,
+                                 hipStream_t st);
 
 }  // namespace ilqg
 

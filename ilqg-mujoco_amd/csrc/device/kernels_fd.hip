@@ -221,13 +221,60 @@ __device__ inline unsigned long long hw_where() {
   return ((unsigned long long)xcc << 32) | hw;
 }
 #endif
+// The workspace doubles a qvel or ctrl FD team reads after taking the centre's
+// state at the end of its velocity stage (the team then runs the velocity
+// stage again, qvel teams, and the acceleration stage + constraint solve):
+// the state block (qpos .. time), xipos, scom / cdof / cinert, qM / qLD /
+// qLDinv / amom (the position stage's outputs the later stages read), the
+// velocity stage's outputs (cvel .. qfrc_con), and the constraint rows
+// [0, nefc) of efc_J / pos / margin / D / KBIP / vel / aref.  Everything else
+// (the other frames, crb, the narrow phase's contacts and candidates, scratch)
+// is dead by then.  tests/test_gpu_parity.py::test_fused_sweep_schedules runs
+// with ILQG_SNAP_POISON=1 (every double not listed reads as NaN).
+constexpr int SNAP_NR = 12;
+__device__ __forceinline__ void snap_ranges(const auto& m, const auto& L, int nefc, int (&o)[SNAP_NR],
+                                            int (&l)[SNAP_NR]) {
+  const int nv = m.nv, nb = m.nbody, nu = m.nu;
+  o[0] = L.qpos;       l[0] = L.time + 1 - L.qpos;
+  o[1] = L.xipos;      l[1] = 3 * nb;
+  o[2] = L.scom;       l[2] = L.cinert + 10 * nb - L.scom;
+  o[3] = L.qM;         l[3] = L.amom + nu * nv - L.qM;
+  o[4] = L.cvel;       l[4] = L.qfrc_con + nv - L.cvel;
+  o[5] = L.efc_J;      l[5] = nefc * nv;
+  o[6] = L.efc_pos;    l[6] = nefc;
+  o[7] = L.efc_margin; l[7] = nefc;
+  o[8] = L.efc_D;      l[8] = nefc;
+  o[9] = L.efc_KBIP;   l[9] = L.kstr * nefc;
+  o[10] = L.efc_vel;   l[10] = nefc;
+  o[11] = L.efc_aref;  l[11] = nefc;
+}
+// LDS double of packed snapshot entry e
+__device__ __forceinline__ int snap_dst(int e, const int (&o)[SNAP_NR], const int (&l)[SNAP_NR]) {
+  int d = 0;
+#pragma unroll
+  for (int r = 0; r < SNAP_NR; r++) {
+    if (e >= 0 && e < l[r]) d = o[r] + e;
+    e -= l[r];
+  }
+  return d;
+}
+
 __device__ inline void fd_fused_body(const auto& m, const auto& L, const auto& C, const auto& X, const Team& T,
                                      const FdFused& a, unsigned u) {
   // late tickets first in the SIMD's issue arbitration: they set the launch's tail
   if (u >= a.prio2) __builtin_amdgcn_s_setprio(2);
   else if (u >= a.prio1) __builtin_amdgcn_s_setprio(1);
   // the planned schedule (launch_fd_plan); readfirstlane: the item stays wave-uniform (SGPR)
-  if (a.order) u = __builtin_amdgcn_readfirstlane(a.order[u]);
+  if (a.order) {
+    u = __builtin_amdgcn_readfirstlane(a.order[u]);
+    // launch_fd_order_check has validated the map; an id out of range is still
+    // never decoded into addresses (a reported fault, not a memory fault)
+    const unsigned nI = (unsigned)a.S * a.P * (1u + (a.halves ? 2u : 1u) * (unsigned)(a.nut + 2 * m.nv));
+    if (u >= nI) {
+      if ((threadIdx.x & (TEAM - 1)) == 0) raise_fault(a.fault);
+      return;
+    }
+  }
   const unsigned long long tstart = __builtin_amdgcn_s_memrealtime();
   STAMP_INIT();
 #ifdef ILQG_STAMPS
@@ -256,14 +303,24 @@ __device__ inline void fd_fused_body(const auto& m, const auto& L, const auto& C
   const int G = 2 * nv * nv + nv * nu;  // cost-gradient entries: qpos, qvel, ctrl
   const double* dq = a.tr.qpos + (size_t)pt * nq;
   // the centre's position/velocity workspace snapshot (a.snap): the team's LDS
-  // doubles [w | c] and ints [iw | ci] (contiguous, make_team)
+  // ints [iw | ci] in full, then only the doubles a qvel or ctrl team reads
+  // after the centre's velocity stage (snap_ranges), the constraint rows cut
+  // to the point's nefc
   const int nwd = L.nd + C.nd, nid = L.ni + C.ni;
-  const bool snap = a.snap && nwd + (nid + 1) / 2 <= a.snapd;
+  const bool snap = a.snap && (nid + 1) / 2 + nwd <= a.snapd;
   double* sp = snap ? a.snap + (size_t)pt * a.snapd : nullptr;
+  double* spd = sp + (nid + 1) / 2;
   unsigned* sflag = a.sync + 4 + 2 * (size_t)a.S * a.P + pt;
+  int ro[SNAP_NR], rl[SNAP_NR];
   auto snap_store = [&]() {
-    FOR_T(e, nwd) st_sc1(sp + e, T.w[e]);
-    FOR_T(e, nid) st_sc1_i(reinterpret_cast<int*>(sp + nwd) + e, T.iw[e]);
+    FOR_T(e, nid) st_sc1_i(reinterpret_cast<int*>(sp) + e, T.iw[e]);
+    snap_ranges(m, L, T.iw[L.nefc], ro, rl);
+    int base = 0;
+#pragma unroll
+    for (int r = 0; r < SNAP_NR; r++) {
+      FOR_T(e, rl[r]) st_sc1(spd + base + e, T.w[ro[r] + e]);
+      base += rl[r];
+    }
     drain_stores();
     TSYNC();
     if (tid == 0) signal_set(sflag, 1u);
@@ -272,30 +329,40 @@ __device__ inline void fd_fused_body(const auto& m, const auto& L, const auto& C
     bw_wait_geq(sflag, 1u, a.fault);
     // sixteen loads in flight per lane before their LDS stores
     constexpr int CH = 16;
-    for (int e0 = 0; e0 < nwd; e0 += CH * TEAM) {
-      double v[CH];
-#pragma unroll
-      for (int q = 0; q < CH; q++) {
-        const int e = e0 + q * TEAM + tid;
-        v[q] = e < nwd ? ld_sc1(sp + e) : 0.0;
-      }
-#pragma unroll
-      for (int q = 0; q < CH; q++) {
-        const int e = e0 + q * TEAM + tid;
-        if (e < nwd) T.w[e] = v[q];
-      }
-    }
     for (int e0 = 0; e0 < nid; e0 += CH * TEAM) {
       int v[CH];
 #pragma unroll
       for (int q = 0; q < CH; q++) {
         const int e = e0 + q * TEAM + tid;
-        v[q] = e < nid ? ld_sc1_i(reinterpret_cast<const int*>(sp + nwd) + e) : 0;
+        v[q] = e < nid ? ld_sc1_i(reinterpret_cast<const int*>(sp) + e) : 0;
       }
 #pragma unroll
       for (int q = 0; q < CH; q++) {
         const int e = e0 + q * TEAM + tid;
         if (e < nid) T.iw[e] = v[q];
+      }
+    }
+    // (a.poison, tests: every double the snapshot does not carry reads as NaN,
+    // so a field missing from snap_ranges changes the records)
+    if (a.poison) {
+      FOR_T(e, nwd) T.w[e] = __builtin_nan("");
+    }
+    TSYNC();
+    snap_ranges(m, L, T.iw[L.nefc], ro, rl);
+    int n = 0;
+#pragma unroll
+    for (int r = 0; r < SNAP_NR; r++) n += rl[r];
+    for (int e0 = 0; e0 < n; e0 += CH * TEAM) {
+      double v[CH];
+#pragma unroll
+      for (int q = 0; q < CH; q++) {
+        const int e = e0 + q * TEAM + tid;
+        v[q] = e < n ? ld_sc1(spd + e) : 0.0;
+      }
+#pragma unroll
+      for (int q = 0; q < CH; q++) {
+        const int e = e0 + q * TEAM + tid;
+        if (e < n) T.w[snap_dst(e, ro, rl)] = v[q];
       }
     }
     TSYNC();
@@ -642,11 +709,59 @@ __global__ __launch_bounds__(PLAN_T) void k_fd_plan(int S, int P, int ntm, int p
   }
 }
 
+// ---- schedule validation (launch_fd_order_check) -------------------------
+// The fused sweep trusts its ticket -> item map twice: an item id out of range
+// would address records and hand-off words past their buffers, and a map that
+// is not a permutation with every column behind its centre could let a team
+// wait on work holding a larger ticket, or announce a record before a missing
+// column is written.  One 1024-thread workgroup checks, before the sweep reads
+// it: every entry < nI, no item twice (so, by counting, a permutation), and
+// slot(centre(s,p)) < slot(column) for every column item.  On failure it sets
+// bit 1 of the fault report word (ilqg_synchronize reports it once) and
+// rewrites the map as the identity, which satisfies all three, so the sweep
+// still runs and its records are the same bits.  pos: nI words of scratch,
+// preset to ~0 on the stream.
+__global__ __launch_bounds__(PLAN_T) void k_fd_order_check(unsigned nC, unsigned nt, unsigned* order, unsigned* pos,
+                                                           unsigned* fault) {
+  __shared__ int bad_sh;
+  const int t = threadIdx.x;
+  const unsigned nI = nC * (1 + nt);
+  if (t == 0) bad_sh = 0;
+  __syncthreads();
+  int bad = 0;
+  for (unsigned u = t; u < nI; u += PLAN_T) {
+    const unsigned v = order[u];
+    if (v >= nI) bad = 1;
+    else if (atomicExch(&pos[v], u) != ~0u) bad = 1;
+  }
+  if (bad) atomicOr(&bad_sh, 1);
+  __threadfence_block();
+  __syncthreads();
+  if (!bad_sh) {
+    for (unsigned v = nC + t; v < nI; v += PLAN_T)
+      if (pos[(v - nC) / nt] >= pos[v]) bad = 1;
+    if (bad) atomicOr(&bad_sh, 1);
+    __syncthreads();
+  }
+  if (bad_sh) {
+    for (unsigned u = t; u < nI; u += PLAN_T) order[u] = u;
+    if (t == 0) atomicOr(fault, 2u);
+  }
+}
+
 }  // namespace
 
 hipError_t launch_fd_plan(int S, int P, int ntm, int p0, float kthr, const unsigned* dur, unsigned* order,
                           hipStream_t st) {
   hipLaunchKernelGGL(k_fd_plan, dim3(1), dim3(PLAN_T), 0, st, S, P, ntm, p0, kthr, dur, order);
+  return hipGetLastError();
+}
+hipError_t launch_fd_order_check(int S, int P, int nt, unsigned* order, unsigned* pos, unsigned* fault,
+                                 hipStream_t st) {
+  const unsigned nC = (unsigned)S * (unsigned)P;
+  hipError_t e = hipMemsetAsync(pos, 0xff, (size_t)nC * (1 + nt) * sizeof(unsigned), st);
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(k_fd_order_check, dim3(1), dim3(PLAN_T), 0, st, nC, (unsigned)nt, order, pos, fault);
   return hipGetLastError();
 }
 
@@ -780,9 +895,9 @@ extern "C" int ilqg_debug_ls_fd(unsigned long long* out5, int reset) {
 }
 // the FD kernels' copy of the stamp counters (tools/stamps.py)
 extern "C" int ilqg_debug_stamps_fd(unsigned long long* acc, unsigned long long* cnt, int reset) {
-  if (hipMemcpyFromSymbol(acc, HIP_SYMBOL(ilqg::coop::g_stamp_acc), sizeof(unsigned long long) * 48) != hipSuccess)
+  if (hipMemcpyFromSymbol(acc, HIP_SYMBOL(ilqg::coop::g_stamp_acc), sizeof(unsigned long long) * STAMP_NG) != hipSuccess)
     return 3;
-  if (hipMemcpyFromSymbol(cnt, HIP_SYMBOL(ilqg::coop::g_stamp_cnt), sizeof(unsigned long long) * 48) != hipSuccess)
+  if (hipMemcpyFromSymbol(cnt, HIP_SYMBOL(ilqg::coop::g_stamp_cnt), sizeof(unsigned long long) * STAMP_NG) != hipSuccess)
     return 3;
   unsigned long long nw[2];
   (void)hipMemcpyFromSymbol(&nw[0], HIP_SYMBOL(ilqg::coop::g_newton_iters), 8);
@@ -790,7 +905,7 @@ extern "C" int ilqg_debug_stamps_fd(unsigned long long* acc, unsigned long long*
   acc[44] = nw[0];
   acc[45] = nw[1];
   if (reset) {
-    unsigned long long z[48] = {0};
+    unsigned long long z[STAMP_NG] = {0};
     (void)hipMemcpyToSymbol(HIP_SYMBOL(ilqg::coop::g_newton_iters), z, 8);
     (void)hipMemcpyToSymbol(HIP_SYMBOL(ilqg::coop::g_newton_calls), z, 8);
     (void)hipMemcpyToSymbol(HIP_SYMBOL(ilqg::coop::g_stamp_acc), z, sizeof(z));

@@ -480,9 +480,9 @@ extern "C" int ilqg_debug_ls_rollout(unsigned long long* out5, int reset) {
   return 0;
 }
 extern "C" int ilqg_debug_stamps(unsigned long long* acc, unsigned long long* cnt, int reset) {
-  if (hipMemcpyFromSymbol(acc, HIP_SYMBOL(ilqg::coop::g_stamp_acc), sizeof(unsigned long long) * 48) != hipSuccess)
+  if (hipMemcpyFromSymbol(acc, HIP_SYMBOL(ilqg::coop::g_stamp_acc), sizeof(unsigned long long) * STAMP_NG) != hipSuccess)
     return 3;
-  if (hipMemcpyFromSymbol(cnt, HIP_SYMBOL(ilqg::coop::g_stamp_cnt), sizeof(unsigned long long) * 48) != hipSuccess)
+  if (hipMemcpyFromSymbol(cnt, HIP_SYMBOL(ilqg::coop::g_stamp_cnt), sizeof(unsigned long long) * STAMP_NG) != hipSuccess)
     return 3;
   unsigned long long nw[2];
   (void)hipMemcpyFromSymbol(&nw[0], HIP_SYMBOL(ilqg::coop::g_newton_iters), 8);
@@ -490,7 +490,7 @@ extern "C" int ilqg_debug_stamps(unsigned long long* acc, unsigned long long* cn
   acc[44] = nw[0];
   acc[45] = nw[1];
   if (reset) {
-    unsigned long long z[48] = {0};
+    unsigned long long z[STAMP_NG] = {0};
     (void)hipMemcpyToSymbol(HIP_SYMBOL(ilqg::coop::g_newton_iters), z, 8);
     (void)hipMemcpyToSymbol(HIP_SYMBOL(ilqg::coop::g_newton_calls), z, 8);
     (void)hipMemcpyToSymbol(HIP_SYMBOL(ilqg::coop::g_stamp_acc), z, sizeof(z));

@@ -331,6 +331,7 @@ struct SolverCore::Impl {
   stepCostFn_t fn = nullptr;
   bool device_cost = false;
   std::vector<double> time, qpos, qvel, warm, ctrl, deriv;
+  bool swept = false;  // deriv holds the records of the trajectory in time..ctrl
 };
 
 SolverCore::SolverCore(mjModel* m, int N, stepCostFn_t fn) : p_(new Impl) {
@@ -419,18 +420,38 @@ void SolverCore::forward(mjData* const* dArray, const mjtNum* K, const mjtNum* k
   check(ilqg_solver_set_gains(p_->s, K, k), "ILQR gains");
   check(ilqg_forward(p_->s), "forwardPass");
   pull_traj(dArray);
+  p_->swept = false;
 }
 
-void SolverCore::backward(mjData* const* dArray, mjtNum* K, mjtNum* k, mjtNum* V, mjtNum* v) {
+void SolverCore::sweep(mjData* const* dArray) {
   Impl& I = *p_;
   push_traj(dArray);
   check(ilqg_fd_sweep(I.s), "calcMJDerivatives sweep");
-  check(ilqg_solver_get_deriv(I.s, I.deriv.data()), "ILQR deriv");
   if (!I.device_cost && I.fn) {
     // cost-gradient entries by host evaluation of the user's callback
+    check(ilqg_solver_get_deriv(I.s, I.deriv.data()), "ILQR deriv");
     for (int n = 0; n < I.P; n++) host_cost_columns(I.m, dArray[n], I.fn, &I.deriv[(size_t)n * I.D]);
     check(ilqg_solver_set_deriv(I.s, I.deriv.data()), "ILQR deriv");
+  } else {
+    // only the records the host reads: initV's (n = 0) and the differentiator's (n = N)
+    check(ilqg_solver_get_deriv_point(I.s, 0, 0, &I.deriv[0]), "ILQR deriv");
+    check(ilqg_solver_get_deriv_point(I.s, 0, I.N, &I.deriv[(size_t)I.N * I.D]), "ILQR deriv");
   }
+  I.swept = true;
+}
+
+bool SolverCore::deriv_current(int n, const mjData* d) const {
+  const Impl& I = *p_;
+  if (!I.swept || n < 0 || n >= I.P) return false;
+  return d->time == I.time[n] && !memcmp(d->qpos, &I.qpos[(size_t)n * I.nq], sizeof(mjtNum) * I.nq) &&
+         !memcmp(d->qvel, &I.qvel[(size_t)n * I.nv], sizeof(mjtNum) * I.nv) &&
+         !memcmp(d->qacc_warmstart, &I.warm[(size_t)n * I.nv], sizeof(mjtNum) * I.nv) &&
+         !memcmp(d->ctrl, &I.ctrl[(size_t)n * I.nu], sizeof(mjtNum) * I.nu);
+}
+
+void SolverCore::riccati(mjtNum mu, mjtNum* K, mjtNum* k, mjtNum* V, mjtNum* v) {
+  Impl& I = *p_;
+  check(ilqg_solver_set_mu(I.s, mu), "ILQR mu");
   // V0 / v0 from initV (virtual, inc/ilqr.h:100-107,142)
   check(ilqg_solver_set_value(I.s, V, v), "ILQR initV");
   check(ilqg_backward(I.s), "backwardPass");

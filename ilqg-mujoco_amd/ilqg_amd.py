@@ -64,6 +64,8 @@ EXPORTS = [
     "ilqg_solver_get_timing",
     "ilqg_solver_debug_set_fault", "ilqg_solver_device_traj", "ilqg_solver_set_layout", "ilqg_solver_set_value", "ilqg_solver_debug_plan",
     "ilqg_solver_set_riccati", "ilqg_selftest_div", "ilqg_solver_set_fd_precision",
+    "ilqg_solver_set_mu", "ilqg_solver_get_deriv_point", "ilqg_solver_debug_plant_schedule",
+    "ilqg_fd_sweep_range", "ilqg_solver_device_deriv",
 ]
 KERNELS = ("rollout", "select", "fd_centre", "fd_cols", "backward", "fd_backward")
 
@@ -393,6 +395,18 @@ class ILQR:
     def fd_sweep(self):
         _check(lib().ilqg_fd_sweep(self._h), "ilqg_fd_sweep")
 
+    def fd_sweep_range(self, p0: int, np_: int):
+        """calcMJDerivatives at points p0 .. p0+np_-1 of every seed (a rank's
+        share of a point-sharded sweep): ilqg_fd_sweep_range"""
+        _check(lib().ilqg_fd_sweep_range(self._h, int(p0), int(np_)), "fd_sweep_range")
+
+    def device_deriv(self):
+        """(device pointer, record stride in doubles) of the resident FD records [S][P][stride]"""
+        p = ctypes.POINTER(ctypes.c_double)()
+        st = ctypes.c_int(0)
+        _check(lib().ilqg_solver_device_deriv(self._h, ctypes.byref(p), ctypes.byref(st)), "device_deriv")
+        return ctypes.cast(p, ctypes.c_void_p).value, st.value
+
     def backward_pass(self):
         """initV + Riccati; the FD sweep it depends on is ilqg_fd_sweep."""
         _check(lib().ilqg_fd_sweep(self._h), "ilqg_fd_sweep")
@@ -431,6 +445,11 @@ class ILQR:
             raise IlqgError(f"V / v must hold {self.S}x{self.nx}x{self.nx} / {self.S}x{self.nx} doubles")
         _check(lib().ilqg_solver_set_value(self._h, _ptr(V), _ptr(v)), "set_value")
 
+    def set_mu(self, mu: float):
+        """Levenberg-Marquardt constant (ILQR::mu, inc/ilqr.h:65,166) for the
+        backward passes enqueued from now on: ilqg_solver_set_mu"""
+        _check(lib().ilqg_solver_set_mu(self._h, ctypes.c_double(mu)), "set_mu")
+
     def set_riccati(self, mode: str):
         """'exact' (bit-identical to the oracle, default) or 'mfma' (matrix-core
         products, fp64; agrees to rounding): ilqg_solver_set_riccati"""
@@ -455,6 +474,12 @@ class ILQR:
     def _debug_set_fault(self, value: int):
         """test hook: preset the hand-off fault report word (ilqg_solver_debug_set_fault)"""
         _check(lib().ilqg_solver_debug_set_fault(self._h, ctypes.c_uint(value)), "debug_set_fault")
+
+    def _debug_plant_schedule(self, slot: int, item: int):
+        """test hook: the next fused sweep's ticket map gets order[slot] = item
+        before the device validates it (ilqg_solver_debug_plant_schedule)"""
+        _check(lib().ilqg_solver_debug_plant_schedule(self._h, ctypes.c_uint(slot), ctypes.c_uint(item)),
+               "debug_plant_schedule")
 
     def device_traj_ptr(self, field: str) -> int:
         """device pointer to the resident nominal trajectory field (seed-major [S][P][...])"""

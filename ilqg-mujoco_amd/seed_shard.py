@@ -1,4 +1,5 @@
-"""Seed sharding and the one exchange step of the multi-GPU design.
+"""Seed sharding and the one exchange step of the multi-GPU design,
+and point sharding of a single seed's FD sweep (cfg 5).
 
 Independent MPC seeds shard across ranks (one process per GPU): rank r owns
 global seeds [r*S, (r+1)*S).  Per iteration the only collective is an
@@ -84,6 +85,74 @@ def first_controls_view(solver, nu: int) -> torch.Tensor:
     S, P = solver.S, solver.P
     full = device_view(solver.device_traj_ptr("ctrl"), S * P * nu).view(S, P, nu)
     return full[:, P - 1, :]
+
+
+# ---- point sharding of one seed's FD sweep (cfg 5: one humanoid seed on 8 GPUs)
+# The FD sweep is independent across the N+1 trajectory points
+# (src/mjderivative.cpp:212-255 runs once per point, inc/ilqr.h:153-154).  Every
+# rank runs the (serial, deterministic) rollout itself, differentiates its
+# contiguous block of points, and one all-gather of the fp64 records gives
+# every rank all of them; every rank then runs the recursion (identical inputs,
+# identical K / k: no broadcast).  Exchange per iteration: S (N+1) Dp doubles
+# (humanoid H = 200: 201 x 2112 x 8 B = 3.4 MB).
+
+def point_range(rank: int, world: int, P: int):
+    """(p0, np) of the contiguous block of points `rank` differentiates: blocks
+    of ceil(P / world) points, the last ones shorter (possibly empty)."""
+    chunk = -(-P // world)
+    p0 = min(P, rank * chunk)
+    return p0, min(P, p0 + chunk) - p0
+
+
+class RecordExchange:
+    """all-gather every rank's block of FD records so that every rank holds the
+    records of all points.
+
+    records: the [S, P, stride] fp64 record array (on the GPU, a zero-copy view
+    of the solver's resident records, ilqg_solver_device_deriv; on CPU any
+    tensor -- the gloo tests); rank / world / group: the point-sharding group.
+    solver: the ILQR writing `records`; torch's stream waits on its launch
+    stream before the gather, and the solver's stream waits on torch's after
+    it (the recursion reads what the gather wrote)."""
+
+    def __init__(self, records: torch.Tensor, rank: int, world: int, group=None, solver=None):
+        S, P, D = records.shape
+        self.records, self.rank, self.world, self.group, self.solver = records, rank, world, group, solver
+        self.chunk = -(-P // world)
+        self.p0, self.np = point_range(rank, world, P)
+        self.send = torch.zeros(S, self.chunk, D, dtype=records.dtype, device=records.device)
+        self.recv = torch.empty(world, S, self.chunk, D, dtype=records.dtype, device=records.device)
+
+    @classmethod
+    def for_solver(cls, solver, rank: int, world: int, group=None):
+        ptr, stride = solver.device_deriv()
+        rec = device_view(ptr, solver.S * solver.P * stride).view(solver.S, solver.P, stride)
+        return cls(rec, rank, world, group, solver)
+
+    def _solver_stream(self):
+        if self.solver is None or not self.records.is_cuda:
+            return None
+        sst = self.solver.stream
+        return torch.cuda.ExternalStream(sst, device=self.records.device) if sst else None
+
+    def exchange(self):
+        """every rank's block -> every rank's `records` (rank order = point order)"""
+        ext = self._solver_stream()
+        cur = torch.cuda.current_stream(self.records.device) if self.records.is_cuda else None
+        if ext is not None and ext.cuda_stream != cur.cuda_stream:
+            cur.wait_stream(ext)
+        self.send[:, :self.np] = self.records[:, self.p0:self.p0 + self.np]
+        if self.world > 1:
+            dist.all_gather_into_tensor(self.recv.view(-1), self.send.view(-1), group=self.group)
+        else:
+            self.recv[0].copy_(self.send)
+        P = self.records.shape[1]
+        for r in range(self.world):
+            p0, n = point_range(r, self.world, P)
+            if n and r != self.rank:
+                self.records[:, p0:p0 + n] = self.recv[r, :, :n]
+        if ext is not None and ext.cuda_stream != cur.cuda_stream:
+            ext.wait_stream(cur)
 
 
 def max_over_ranks(x: float, world: int, device) -> float:

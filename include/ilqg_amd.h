@@ -127,6 +127,8 @@ int ilqg_solver_get_traj(ilqg_solver* s, double* time, double* qpos, double* qve
 int ilqg_solver_set_gains(ilqg_solver* s, const double* K, const double* k);
 int ilqg_solver_get_gains(ilqg_solver* s, double* K, double* k);
 int ilqg_solver_get_deriv(ilqg_solver* s, double* deriv);     /* nseed x (N+1) x D */
+/* one FD record (D doubles) of seed `seed` at point `point` (0 = terminal) */
+int ilqg_solver_get_deriv_point(ilqg_solver* s, int seed, int point, double* deriv);
 /* overwrite the FD records before ilqg_backward, e.g. with cost-gradient
    entries from a host cost callback (stepCostFn_t, inc/mjderivative.h:5) */
 int ilqg_solver_set_deriv(ilqg_solver* s, const double* deriv);
@@ -138,6 +140,12 @@ int ilqg_solver_get_costs(ilqg_solver* s, double* cost, int* selected);
 int ilqg_forward(ilqg_solver* s);   /* forwardPass over all candidates + selection (inc/ilqr.h:116-130) */
 int ilqg_fd_sweep(ilqg_solver* s);  /* calcMJDerivatives at every point of every seed */
 int ilqg_backward(ilqg_solver* s);  /* initV + Riccati n = 1..N (inc/ilqr.h:100-107,133-176) */
+/* calcMJDerivatives at points p0 .. p0+np-1 of every seed (one rank's share
+   of a point-sharded sweep, src/mjderivative.cpp:212-255 per point; records
+   identical to ilqg_fd_sweep's).  With the records of the other points
+   written into the buffer ilqg_solver_device_deriv exposes (an all-gather),
+   ilqg_backward then runs the recursion over all of them. */
+int ilqg_fd_sweep_range(ilqg_solver* s, int p0, int np);
 int ilqg_iterate(ilqg_solver* s);   /* forwardPass; setDInit(dArray[N]); backwardPass (inc/ilqr.h:179-186) */
 /* waits for every launch; returns ILQG_ERR_HIP once if a fused sweep's
    hand-off wait timed out since the last call (the report is cleared by it) */
@@ -148,6 +156,12 @@ int ilqg_solver_debug_set_fault(ilqg_solver* s, unsigned value);
    sweep recorded and copy out the schedule (slot -> FD item) and the
    durations; nitems = the sweep's FD item count (0: no fused sweep) */
 int ilqg_solver_debug_plan(ilqg_solver* s, unsigned* order, unsigned* dur, int* nitems);
+/* test hook: the next fused sweep's ticket map (planned, or the identity) gets
+   order[slot] = item before it is validated (calls accumulate until then).  Every map is checked on the
+   device (items in range, none repeated, every column behind its centre); an
+   invalid one is replaced by the identity, the sweep runs normally, and
+   ilqg_synchronize returns ILQG_ERR_HIP once ("invalid ticket schedule") */
+int ilqg_solver_debug_plant_schedule(ilqg_solver* s, unsigned slot, unsigned item);
 void* ilqg_solver_stream(ilqg_solver* s); /* hipStream_t */
 /* enqueue subsequent hot-path launches on an external stream (hipStream_t,
    e.g. torch's current stream) instead of the solver's own; NULL restores it */
@@ -176,6 +190,10 @@ int ilqg_solver_set_layout(ilqg_solver* s, int layout);
    these V0 (nseed x nx x nx, column-major) and v0 (nseed x nx) instead of the
    terminal point's v = dgdx, V = v'v.  One-shot: later passes use initV. */
 int ilqg_solver_set_value(ilqg_solver* s, const double* V, const double* v);
+/* Levenberg-Marquardt constant mu (the public ILQR::mu, inc/ilqr.h:65, read
+   by every backward step at inc/ilqr.h:166): used by every backward pass
+   enqueued after the call (opts.mu at creation until then).  NaN is refused. */
+int ilqg_solver_set_mu(ilqg_solver* s, double mu);
 /* Riccati recursion (inc/ilqr.h:133-176) engine.  EXACT (default): the
    oracle's loops, bit-identical K, k, V, v (streamed behind the FD sweep on
    cooperative models).  MFMA: every matrix product (B'V, Quu = -2B'VB - 2R,
@@ -202,6 +220,9 @@ int ilqg_solver_set_fd_precision(ilqg_solver* s, int prec);
 /* device pointer to the per-seed selected-candidate cost (nseed doubles), for
    an in-stream collective (RCCL all-gather) without a host round trip */
 int ilqg_solver_device_costs(ilqg_solver* s, double** dptr);
+/* device pointer to the resident FD records, [nseed][N+1][stride] doubles
+   (stride >= D: each record padded to whole 128-byte lines) */
+int ilqg_solver_device_deriv(ilqg_solver* s, double** dptr, int* stride);
 /* device pointer to the resident nominal trajectory (field 0 time, 1 qpos,
    2 qvel, 3 warm, 4 ctrl; seed-major [nseed][N+1][...], point N = the first
    applied control): the multi-GPU MPC broadcast of the winning seed's first

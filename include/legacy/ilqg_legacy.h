@@ -69,11 +69,21 @@ class SolverCore {
   void init(const mjData* dmain, mjData* const* dArray);
   void set_dinit(const mjData* dinit);                    // inc/ilqr.h:110-113
   void forward(mjData* const* dArray, const mjtNum* K, const mjtNum* k);  // inc/ilqr.h:116-130
-  // the Riccati recursion n = 1..N (inc/ilqr.h:144-175) from the V0 / v0 that
-  // initV left in V / v (uploaded, ilqg_solver_set_value); K, k, V, v out
-  void backward(mjData* const* dArray, mjtNum* K, mjtNum* k, mjtNum* V, mjtNum* v);
-  // the FD record (calcMJDerivatives layout) of point n from the last backward
+  // the FD sweep of backwardPass: calcMJDerivatives at every point of dArray
+  // (inc/ilqr.h:153-154 for n = 1..N, :102-103 for initV's n = 0), with the
+  // host cost callback's gradient entries when no device cost is registered
+  void sweep(mjData* const* dArray);
+  // the Riccati recursion n = 1..N (inc/ilqr.h:144-175) with Levenberg-
+  // Marquardt constant mu (read per pass, as ilqr.h:166 reads the member) from
+  // the V0 / v0 that initV left in V / v (uploaded, ilqg_solver_set_value);
+  // K, k, V, v out
+  void riccati(mjtNum mu, mjtNum* K, mjtNum* k, mjtNum* V, mjtNum* v);
+  // the FD record (calcMJDerivatives layout) of point n from the last sweep:
+  // n = 0 and n = N always, every n when a host cost callback is in use
   const mjtNum* deriv(int n) const;
+  // whether the last sweep's record of point n is the linearisation at d's
+  // current state (dArray[n] unchanged since the sweep)
+  bool deriv_current(int n, const mjData* d) const;
 
  private:
   void push_traj(mjData* const* dArray);

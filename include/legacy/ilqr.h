@@ -5,7 +5,7 @@
 //   ILQR<nv,nu,N>(m, dmain, stepCostFn); setDInit(d); iterate();
 //   dArray[N]->ctrl (the first control of the optimised trajectory).
 // The passes run on the GPU (include/ilqg_amd.h, one seed, reference
-// semantics: alpha = 1, mu = 1000).  dArray / K / k / V / v are host mirrors,
+// semantics: alpha = 1; mu is the public member, read by every backwardPass).  dArray / K / k / V / v are host mirrors,
 // uploaded before and refreshed after every pass.  Eigen is not required: the
 // matrices are column-major ilqg_legacy::Mat (Eigen's storage order) and the
 // *_mt maps ilqg_legacy::Map views.
@@ -13,7 +13,9 @@
 // initV is virtual, as in the reference (inc/ilqr.h:100,142): backwardPass
 // calls it, and the V / v it leaves (the terminal FD's v = dgdx, V = v'v by
 // default, or whatever an override sets) seed the device recursion
-// (ilqg_solver_set_value).
+// (ilqg_solver_set_value).  backwardPass runs the FD sweep over every point
+// first (the sweep does not depend on V), so the default initV reads the
+// terminal record the sweep already formed instead of launching its own FD.
 //
 // Unlike the reference, every ILQR instance owns its own state (the
 // reference's function-static references in backwardPass, inc/ilqr.h:137-140,
@@ -68,7 +70,7 @@ class ILQR {
   u_mt* u;
   x_mt* xStar;
   u_mt* uStar;
-  mjtNum mu = 1000.0;  // the device solver is created with this value
+  mjtNum mu = 1000.0;  // inc/ilqr.h:65; uploaded by every backwardPass (ilqr.h:166)
 
   ILQR(mjModel* m, mjData* dmain, stepCostFn_t& stepCostFn) : m(m), core_(m, N, stepCostFn) {
     static_assert(sizeof(K_t) == sizeof(mjtNum) * nu * 2 * nv, "K must be dense");
@@ -101,10 +103,17 @@ class ILQR {
   ILQR(const ILQR&) = delete;
   ILQR& operator=(const ILQR&) = delete;
 
-  // inc/ilqr.h:100-107: FD at the terminal point (on the GPU), v = dgdx, V = v'v
+  // inc/ilqr.h:100-107: FD at the terminal point (on the GPU), v = dgdx, V = v'v.
+  // Inside backwardPass the sweep's record of dArray[0] is that FD (the same
+  // bits); called elsewhere, or after dArray[0] changed, it runs its own.
   virtual void initV() {
     differentiator->setMJData(dArray[0]);
-    differentiator->updateDerivatives();
+    if (core_.deriv_current(0, dArray[0])) {
+      mju_copy(differentiator->deriv, core_.deriv(0), Differentiator<nv, nu>::kD);
+      differentiator->assemble();
+    } else {
+      differentiator->updateDerivatives();
+    }
     for (int i = 0; i < 2 * nv; i++) (*v)(0, i) = (*differentiator->dgdx)(0, i);
     for (int j = 0; j < 2 * nv; j++)
       for (int i = 0; i < 2 * nv; i++) (*V)(i, j) = (*v)(0, i) * (*v)(0, j);
@@ -122,12 +131,14 @@ class ILQR {
     new (uStar) u_mt(dArray[0]->ctrl);
   }
 
-  // inc/ilqr.h:133-176: initV (virtual), then FD + Riccati for n = 1..N on the
-  // device; the differentiator is left at dArray[N] with its A / B, as the
-  // reference's last updateDerivatives leaves it
+  // inc/ilqr.h:133-176: the FD sweep over dArray, initV (virtual), then the
+  // Riccati recursion n = 1..N with the current mu on the device; the
+  // differentiator is left at dArray[N] with its A / B, as the reference's last
+  // updateDerivatives leaves it
   void backwardPass() {
+    core_.sweep(dArray);
     initV();
-    core_.backward(dArray, K[0].data(), k[0].data(), V->data(), v->data());
+    core_.riccati(mu, K[0].data(), k[0].data(), V->data(), v->data());
     differentiator->setMJData(dArray[N]);
     mju_copy(differentiator->deriv, core_.deriv(N), Differentiator<nv, nu>::kD);
     differentiator->assemble();

@@ -524,6 +524,12 @@ void ora_ilqr_forwardPass(ora_ilqr* s) {
   }
 }
 
+/* an FD "driver" that leaves the record as it is: backwardPass over records
+   formed elsewhere (the point-sharded sweep's gathered records, tests) */
+void ora_calc_none(mjModel* m, mjData* d, mjtNum* deriv, stepCostFn_t cost) {
+  (void)m; (void)d; (void)deriv; (void)cost;
+}
+
 void ora_ilqr_fd_point(ora_ilqr* s, int n) {
   s->calc(s->m, s->dArray[n], s->deriv + (size_t)n * s->D, s->cost);
 }

@@ -63,6 +63,7 @@ void ora_ilqr_free(ora_ilqr* s);
 void ora_ilqr_setDInit(ora_ilqr* s, const mjData* dinit);
 void ora_ilqr_forwardPass(ora_ilqr* s);
 void ora_ilqr_fd_point(ora_ilqr* s, int n);
+void ora_calc_none(mjModel* m, mjData* d, mjtNum* deriv, stepCostFn_t cost);
 void ora_ilqr_backwardPass(ora_ilqr* s);
 void ora_ilqr_backwardPass_v0(ora_ilqr* s, const mjtNum* V0, const mjtNum* v0);
 void ora_ilqr_iterate(ora_ilqr* s);

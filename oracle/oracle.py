@@ -306,6 +306,36 @@ class OILQR:
     def _view(self, off_name):
         raise NotImplementedError
 
+    def set_mu(self, mu: float):
+        """the Levenberg-Marquardt constant (ILQR::mu, inc/ilqr.h:65; 1000 at
+        creation), written into the oracle's ora_ilqr struct (ilqr_ora.h)"""
+        class S(ctypes.Structure):
+            _fields_ = [("m", ctypes.c_void_p), ("N", ctypes.c_int), ("nv", ctypes.c_int), ("nu", ctypes.c_int),
+                        ("nx", ctypes.c_int), ("D", ctypes.c_int), ("d", ctypes.c_void_p),
+                        ("dArray", ctypes.c_void_p), ("deriv", _dp), ("V", _dp), ("v", _dp), ("K", _dp),
+                        ("k", _dp), ("mu", ctypes.c_double)]
+        ctypes.cast(self.s, ctypes.POINTER(S)).contents.mu = float(mu)
+
+    def backward_from_records(self, deriv):
+        """backwardPass (initV + the recursion, inc/ilqr.h:100-107,133-176) over
+        the given FD records (P x D) instead of the oracle's own sweep"""
+        class S(ctypes.Structure):
+            _fields_ = [("m", ctypes.c_void_p), ("N", ctypes.c_int), ("nv", ctypes.c_int), ("nu", ctypes.c_int),
+                        ("nx", ctypes.c_int), ("D", ctypes.c_int), ("d", ctypes.c_void_p),
+                        ("dArray", ctypes.c_void_p), ("deriv", _dp), ("V", _dp), ("v", _dp), ("K", _dp),
+                        ("k", _dp), ("mu", ctypes.c_double), ("cost", ctypes.c_void_p),
+                        ("calc", ctypes.c_void_p), ("cout_lines", ctypes.c_long)]
+        st = ctypes.cast(self.s, ctypes.POINTER(S)).contents
+        P = self.N + 1
+        rec = np.ascontiguousarray(deriv, dtype=np.float64).reshape(P, st.D)
+        np.ctypeslib.as_array(st.deriv, shape=(P, st.D))[:] = rec
+        calc = st.calc
+        st.calc = self.lib.fnptr("ora_calc_none").value
+        try:
+            self.lib.L.ora_ilqr_backwardPass(self.s)
+        finally:
+            st.calc = calc
+
     def arrays(self):
         """K (P, nu*nx), k (P, nu), deriv (P, D), V (nx*nx), v (nx) copied out of the C struct."""
         m, P = self.model, self.N + 1

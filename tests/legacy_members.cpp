@@ -8,6 +8,8 @@
 //   legacy_members model.xml members   reference semantics of the members (GPU)
 //   legacy_members model.xml initv N   N iterate() of the initV-override subclass;
 //                                      prints K, k, V, v and the trajectory as hex
+//   legacy_members model.xml mu X N    N iterate() of a plain ILQR whose public mu
+//                                      was set to X first (inc/ilqr.h:65,166); same output
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -138,15 +140,8 @@ int members(mjModel* m, mjData* d0) {
   return fails ? 1 : 0;
 }
 
-int initv(mjModel* m, mjData* d0, int iters) {
-  stepCostFn_t fn = stepCost;
-  FixedTerminal<kNv, kNu, kN> il(m, d0, fn);
-  il.setDInit(d0);
-  for (int i = 0; i < iters; i++) il.iterate();
-  if (il.calls != iters) {
-    fprintf(stderr, "FAIL: backwardPass called initV %d times for %d iterations\n", il.calls, iters);
-    return 1;
-  }
+template <class IL>
+void dump(const mjModel* m, IL& il) {
   for (int n = 0; n <= kN; n++) hex("K", il.K[n].data(), kNu * 2 * kNv);
   for (int n = 0; n <= kN; n++) hex("k", il.k[n].data(), kNu);
   hex("V", il.V->data(), 4 * kNv * kNv);
@@ -156,14 +151,35 @@ int initv(mjModel* m, mjData* d0, int iters) {
     hex("qvel", il.dArray[n]->qvel, m->nv);
     hex("ctrl", il.dArray[n]->ctrl, m->nu);
   }
+}
+
+int initv(mjModel* m, mjData* d0, int iters) {
+  stepCostFn_t fn = stepCost;
+  FixedTerminal<kNv, kNu, kN> il(m, d0, fn);
+  il.setDInit(d0);
+  for (int i = 0; i < iters; i++) il.iterate();
+  if (il.calls != iters) {
+    fprintf(stderr, "FAIL: backwardPass called initV %d times for %d iterations\n", il.calls, iters);
+    return 1;
+  }
+  dump(m, il);
   return 0;
 }
 
+int mu(mjModel* m, mjData* d0, mjtNum value, int iters) {
+  stepCostFn_t fn = stepCost;
+  ILQR<kNv, kNu, kN> il(m, d0, fn);
+  il.mu = value;  // the public member, read by every backwardPass
+  il.setDInit(d0);
+  for (int i = 0; i < iters; i++) il.iterate();
+  dump(m, il);
+  return 0;
+}
 }  // namespace
 
 int main(int argc, const char** argv) {
   if (argc < 3) {
-    fprintf(stderr, "usage: legacy_members model.xml members|initv [iters]\n");
+    fprintf(stderr, "usage: legacy_members model.xml members | initv [iters] | mu value [iters]\n");
     return 2;
   }
   mj_activate("mjkey.txt");
@@ -173,7 +189,9 @@ int main(int argc, const char** argv) {
   if (m->nv != kNv || m->nu != kNu) mju_error("legacy_members drives the inverted pendulum (nv=2, nu=1)");
   mjData* d = mj_makeData(m);
   for (int i = 0; i < 10; i++) mj_step(m, d);  // inverted_pendulum.cpp:12-13
-  int rc = !strcmp(argv[2], "members") ? members(m, d) : initv(m, d, argc > 3 ? atoi(argv[3]) : 1);
+  int rc = !strcmp(argv[2], "members") ? members(m, d)
+           : !strcmp(argv[2], "mu")    ? mu(m, d, argc > 3 ? atof(argv[3]) : 1000.0, argc > 4 ? atoi(argv[4]) : 1)
+                                       : initv(m, d, argc > 3 ? atoi(argv[3]) : 1);
   mj_deleteData(d);
   mj_deleteModel(m);
   return rc;

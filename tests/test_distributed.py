@@ -203,3 +203,87 @@ def test_winner_broadcast_on_subgroup_gloo(tmp_path):
         x = np.load(tmp_path / f"g{r}.npz")
         assert int(x["best"]) == 2
         assert np.array_equal(x["u"], [20.0, -1.0])  # global rank 2's seed 0
+
+
+# ---- point sharding of one seed's FD sweep (cfg 5's single humanoid seed on
+# N GPUs): every rank rolls out the same trajectory, differentiates its block
+# of points, all-gathers the records (RecordExchange) and runs the recursion.
+# The FD engine here is the oracle (the product has no CPU path); the host
+# logic -- point blocks, the gather into every rank's record array, the
+# recursion over the gathered records -- is the one the GPU run uses.
+H_PT = 4  # 5 points: blocks of 3 + 2 (world 2) and 2 + 2 + 1 (world 3)
+
+
+def _humanoid_oracle():
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import ilqg_amd as ia
+    import oracle as ora
+    import workloads
+    m = ia.Model.load(workloads.model_file("humanoid"))
+    om = ora.OModel(m.blob())
+    om.lib.L.ora_set_cost_desc(ora.CostDesc.from_cost(ia.HUMANOID_COST, m.nq, m.nv, m.nu))
+    om.lib.L.ora_set_nthread(1)
+    d = om.make_data()
+    q = d.arr("qpos")
+    q[2] = 1.4  # cfg 5's state (bench.py run_humanoid_cfg5)
+    il = ora.OILQR(om, d, H_PT, cost_fn="ora_cost_desc_fn")
+    il.set_dinit(d)
+    il.forward_pass()
+    il.set_dinit(il_state(om, il, H_PT))
+    return ora, om, il
+
+
+def il_state(om, il, n):
+    t = il.traj()
+    d = om.make_data()
+    d.set_state(time=t["time"][n], qpos=t["qpos"][n], qvel=t["qvel"][n], warm=t["warm"][n], ctrl=t["ctrl"][n])
+    return d
+
+
+def _worker_points(rank, world, port, outdir):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from seed_shard import RecordExchange, point_range
+        ora, om, il = _humanoid_oracle()
+        P = H_PT + 1
+        D = om.D
+        stride = D + 3  # padded records, as the solver's [S][P][Dp]
+        rec = torch.full((1, P, stride), float("nan"), dtype=torch.float64)
+        p0, n = point_range(rank, world, P)
+        for p in range(p0, p0 + n):
+            rec[0, p, :D] = torch.from_numpy(ora.calc_derivatives(om, il_state(om, il, p), "ora_cost_desc_fn"))
+        RecordExchange(rec, rank, world).exchange()
+        il.backward_from_records(rec[0, :, :D].numpy())
+        a = il.arrays()
+        np.savez(os.path.join(outdir, f"p{rank}.npz"), rec=rec[0, :, :D].numpy().copy(), K=a["K"], k=a["k"],
+                 V=a["V"], v=a["v"], p0=p0, n=n)
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_point_sharded_fd_gloo(tmp_path, world):
+    """one humanoid seed (cfg 5), H = 4, its FD sweep point-sharded over
+    `world` gloo ranks: every rank ends with the 1-rank records, K, k, V, v
+    bit for bit, and the blocks tile the trajectory"""
+    mp.spawn(_worker_points, args=(world, _free_port(), str(tmp_path)), nprocs=world, join=True)
+    ora, om, il = _humanoid_oracle()
+    il.backward_pass()
+    ref = il.arrays()
+    r = [np.load(tmp_path / f"p{i}.npz") for i in range(world)]
+    assert [int(x["p0"]) for x in r] == sorted(int(x["p0"]) for x in r)
+    assert sum(int(x["n"]) for x in r) == H_PT + 1
+    for x in r:
+        assert np.array_equal(x["rec"], ref["deriv"])
+        for key in ("K", "k", "V", "v"):
+            assert np.array_equal(x[key], ref[key]), key
+
+
+def test_point_range_tiles():
+    from seed_shard import point_range
+    for P in (1, 5, 201, 501):
+        for world in (1, 2, 3, 8):
+            blocks = [point_range(r, world, P) for r in range(world)]
+            covered = [p for p0, n in blocks for p in range(p0, p0 + n)]
+            assert covered == list(range(P))

@@ -401,9 +401,11 @@ def test_riccati_mfma_step(ia, fixture):
     assert all(e <= 1e-12 for e in errs.values()), errs
 
 
-@pytest.mark.parametrize("env", [{}, {"ILQG_FUSED": "0"}, {"ILQG_PLAN": "1"}, {"ILQG_FD_HALVES": "1"},
+@pytest.mark.parametrize("env", [{}, {"ILQG_FUSED": "0"}, {"ILQG_PLAN": "1"}, {"ILQG_PLAN": "1", "ILQG_FD_HALVES": "1"},
+                                 {"ILQG_FD_HALVES": "1"},
                                  {"ILQG_FD_SNAP": "0"}, {"ILQG_FD_HALVES": "1", "ILQG_FD_SNAP": "0"},
-                                 {"ILQG_FD_PRIO1": "500", "ILQG_FD_PRIO2": "800"}])
+                                 {"ILQG_FD_PRIO1": "500", "ILQG_FD_PRIO2": "800"},
+                                 {"ILQG_SNAP_POISON": "1"}, {"ILQG_SNAP_POISON": "1", "ILQG_FD_HALVES": "1"}])
 def test_fused_sweep_schedules(ia, ora, env, monkeypatch):
     """The fused FD sweep + streamed backward pass (k_fd_fused_g), the
     two-kernel sweep (ILQG_FUSED=0), the fused sweep with its tickets in the
@@ -412,7 +414,10 @@ def test_fused_sweep_schedules(ia, ora, env, monkeypatch):
     as two teams, its + and - halves (ILQG_FD_HALVES=1) and with the qvel/ctrl
     teams computing their own position/velocity stages instead of loading the
     centre's (ILQG_FD_SNAP=0) give the oracle's iterate bit for bit (3 seeds x
-    41 points x 16 column teams: the ticket order interleaves seeds)"""
+    41 points x 16 column teams: the ticket order interleaves seeds).  With
+    ILQG_SNAP_POISON=1 every workspace double the centre snapshot does not
+    carry reads as NaN in the teams that load it: the trimmed snapshot holds
+    everything they read"""
     import workloads
     for k, v in env.items():
         monkeypatch.setenv(k, v)
@@ -447,10 +452,91 @@ def test_fused_sweep_schedules(ia, ora, env, monkeypatch):
         assert np.array_equal(np.sort(order), np.arange(n.value)), "planned order is a permutation"
         assert not np.array_equal(order, np.arange(n.value)), "the planner reordered the tickets"
         assert (dur > 0).all(), "every item's duration was recorded"
+        # the deadlock-freedom invariant: every column item (each half, with
+        # ILQG_FD_HALVES) holds a later ticket than its centre C(s,p) = p S + s
+        nC = S * P
+        nt = n.value // nC - 1
+        pos = np.empty(n.value, dtype=np.int64)
+        pos[order] = np.arange(n.value)
+        cols = np.arange(nC, n.value)
+        assert (pos[(cols - nC) // nt] < pos[cols]).all(), "a column is scheduled before its centre"
     # the sweep alone (no backward roles) writes the same records
     g.fd_sweep()
     g.synchronize()
     exact(g.deriv(), D, "fd_sweep alone vs iterate's fused records")
+
+
+@pytest.mark.parametrize("bad", ["out_of_range", "repeated", "column_first"])
+def test_invalid_schedule_is_reported(ia, ora, bad):
+    """A fused sweep's ticket -> item map is validated on the device before the
+    sweep reads it (launch_fd_order_check): an entry out of range, a repeated
+    item, or a column ahead of its centre is replaced by the identity map,
+    ilqg_synchronize reports ILQG_ERR_HIP once ("invalid ticket schedule")
+    instead of the process dying on a memory fault or a hand-off deadlock,
+    and the records stay the oracle's bit for bit -- on that iteration and the
+    next (test hook ilqg_solver_debug_plant_schedule)"""
+    import workloads
+    m, om = setup(ia, ora, "hopper", ia.HOPPER_COST)
+    S, H = 2, 20
+    P = H + 1
+    dmain = workloads.hopper_dmain(m, S, sigma=0.01)
+    g = ia.ILQR(m, dmain, H, ia.HOPPER_COST)
+    nC = S * P
+    # slot nC holds item nC (the first column of C(0, 0)) in the identity map
+    plants = {"out_of_range": [(nC, 1 << 30)], "repeated": [(nC, nC + 1)],
+              "column_first": [(0, nC), (nC, 0)]}[bad]  # a permutation, C(0, 0) behind its column
+    for slot, item in plants:
+        g._debug_plant_schedule(slot, item)
+    g.iterate()
+    with pytest.raises(ia.IlqgError, match="invalid ticket schedule"):
+        g.synchronize()
+    g.synchronize()  # reported once
+    g.iterate()
+    g.synchronize()
+    (K, k), D = g.gains(), g.deriv()
+    for s in range(S):
+        oa = _oracle_ilqr(ora, om, _state_dict(dmain, s), H, "ora_cost_desc_fn", 2).arrays()
+        exact(D[s], oa["deriv"], f"seed {s} deriv")
+        exact(K[s], oa["K"], f"seed {s} K")
+        exact(k[s], oa["k"], f"seed {s} k")
+
+
+@pytest.mark.parametrize("name,prec", [("hopper", "f64"), ("humanoid", "f32")])
+def test_fd_sweep_range_blocks(ia, ora, name, prec):
+    """ilqg_fd_sweep_range (one rank's block of a point-sharded sweep, cfg 5 on
+    N GPUs): the blocks of a 3-way split together write exactly the records of
+    the whole-trajectory sweep, and the recursion over them (after the
+    single-rank RecordExchange over the solver's resident records) gives the
+    gains of the unsharded iteration"""
+    import workloads
+    from seed_shard import RecordExchange, point_range
+    m = ia.Model.load(workloads.model_file(name))
+    if name == "hopper":
+        dmain, H, cost = workloads.hopper_dmain(m, 2, sigma=0.01), 30, ia.HOPPER_COST
+    else:
+        dmain, H, cost = m.reset_state(1), 12, ia.HUMANOID_COST
+        dmain.qpos[0, 2] = 1.4
+    g = ia.ILQR(m, dmain, H, cost)
+    if prec == "f32":
+        g.set_fd_precision("f32")
+    g.forward_pass()
+    g.fd_sweep()
+    g.riccati_pass()
+    g.synchronize()
+    D_full, (K_full, k_full) = g.deriv(), g.gains()
+    P = H + 1
+    g.set_deriv(np.full_like(D_full, np.nan))
+    for r in range(3):
+        p0, n = point_range(r, 3, P)
+        g.fd_sweep_range(p0, n)
+    g.synchronize()
+    exact(g.deriv(), D_full, "3 blocks vs the whole sweep")
+    RecordExchange.for_solver(g, 0, 1).exchange()
+    g.riccati_pass()
+    g.synchronize()
+    K, k = g.gains()
+    exact(K, K_full, "K")
+    exact(k, k_full, "k")
 
 
 def test_bench_workload_bitexact(ia, ora):

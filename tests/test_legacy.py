@@ -194,3 +194,33 @@ def test_initv_override_drives_recursion(ora, iters):
     for _ in range(iters):
         il2.iterate()
     assert not np.array_equal(il2.arrays()["K"], a["K"])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("iters", [1, 2])
+def test_legacy_mu_is_live(ora, iters):
+    """the public ILQR::mu (inc/ilqr.h:65) is read by every backward pass
+    (inc/ilqr.h:166): a caller setting il.mu = 10 before iterate() gets the
+    oracle's recursion at mu = 10 bit for bit, and mu = 1000 gives other gains"""
+    import ilqg_amd as ia
+    m = ia.Model.load(model_path("inverted_pendulum"))
+    om = ora.OModel(m.blob())
+    d = om.make_data()
+    d.step(10)
+    runs = {}
+    for mu in (10.0, 1000.0):
+        r = subprocess.run([MEMBERS, model_path("inverted_pendulum"), "mu", repr(mu), str(iters)], capture_output=True,
+                           text=True, timeout=600)
+        assert r.returncode == 0, r.stderr
+        got = _hex_rows(r.stdout)
+        il = ora.OILQR(om, d, 20, cost_fn="ora_cost_pendulum")
+        il.set_mu(mu)
+        il.set_dinit(d)
+        for _ in range(iters):
+            il.iterate()
+        a, t = il.arrays(), il.traj()
+        assert np.array_equal(got["K"], a["K"]) and np.array_equal(got["k"], a["k"]), mu
+        assert np.array_equal(got["V"][0], a["V"]) and np.array_equal(got["v"][0], a["v"]), mu
+        assert np.array_equal(got["qpos"], t["qpos"]) and np.array_equal(got["ctrl"], t["ctrl"]), mu
+        runs[mu] = got
+    assert not np.array_equal(runs[10.0]["K"], runs[1000.0]["K"])

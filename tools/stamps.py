@@ -16,8 +16,13 @@ NAMES = {10: " nt: start (warm/smooth choice, factor)", 0: "kinematics", 1: "com
          40: "B: barrier 6 (end of step)", 41: "B: control law + record", 42: "B: factor_ld(M) / limit rows+passive+act",
          43: "B: barrier 5",
          29: "A: barrier 5b (Euler factor)", 30: "B: Newton warm-start prep", 31: " nt: hessian build (M + J'DJ)"}
+# the third wave of a three-wave rollout team (STAMPC, its own clock): partitions that wave's time
+W2 = {48: "W2: limit rows+passive+frames", 49: "W2: barrier 1", 50: "W2: collision (non-plane pairs)",
+      51: "W2: barrier 2", 52: "W2: barrier 3 (idle in phase 3)", 53: "W2: factors of M and M+hD",
+      54: "W2: barrier 4", 55: "W2: barrier 5 (idle in phase 5)", 56: "W2: barrier 6 (end of step)",
+      57: "W2: velocity stage (phase 3)"}
 L = ia.lib()
-acc = (ctypes.c_ulonglong * 48)(); cnt = (ctypes.c_ulonglong * 48)()
+acc = (ctypes.c_ulonglong * 64)(); cnt = (ctypes.c_ulonglong * 64)()
 m = ia.Model.load(workloads.model_file(sys.argv[1] if len(sys.argv) > 1 else "hopper"))
 if m.nq != m.nv:  # humanoid, cfg 5's state (tools/cfg5_probe.py)
     dmain = m.reset_state(1)
@@ -68,6 +73,12 @@ for what, fn, rd, rls in (("rollout (1 seed)", g.forward_pass, L.ilqg_debug_stam
     for i in range(44):
         if cnt[i]:
             print(f"  {NAMES[i]:24s} calls {cnt[i]:6d}  cycles/call {acc[i]/cnt[i]:9.0f}  share {acc[i]/max(tot,1):6.1%}")
+    tot2 = sum(acc[i] for i in W2)
+    if tot2:
+        print(f"   wave 2 (own clock): {tot2} ticks, {tot2 / max(acc[47], 1):.1%} of the block's lifetime")
+        for i in W2:
+            if cnt[i]:
+                print(f"  {W2[i]:24s} calls {cnt[i]:6d}  cycles/call {acc[i]/cnt[i]:9.0f}  share {acc[i]/tot2:6.1%}")
 
 BN = ["stage1 sym/A/B/q/c/r", "stage2 T1=B'V", "stage3 Mm,T3,w,ldlt,col", "stage4 K,k solves",
       "stage5 ABK,T6,y,kR", "stage6 T4", "stage7 Vn", "stage8 z,vn,K/k out", "V copy + prefetch store"]
