@@ -267,6 +267,15 @@ struct ilqg_solver {
   std::vector<double> host_alphas;
   bool initialized = false;
   hipStream_t own_stream = nullptr;
+  // pipelined iterate (one candidate per seed, unfused sweep): the rollout in
+  // chunks of pipe_chunk points, the FD sweep of each finished chunk on
+  // fd_stream behind it (ILQG_PIPE_CHUNK, read at creation; 0 = off)
+  int pipe_chunk = 0;
+  bool pipe_flat = false;  // ILQG_PIPE_FLAT: equal chunks to the end (A/B)
+  static constexpr int kFdStreams = 3;  // chunk c's sweep on fd_stream[c % 3]: the launches' tails overlap
+  hipStream_t fd_stream[kFdStreams] = {};
+  std::vector<hipEvent_t> pipe_ev;
+  DevBuf carry[5];  // the chunked rollout's state between launches, [S][...]
   // (A split variant -- the Riccati recursion as a launch of its own on a second
   // stream, streaming a concurrent sweep launch's records -- deadlocked when the
   // two streams shared a hardware queue: HIP does not guarantee that two
@@ -316,7 +325,12 @@ struct ilqg_solver {
                    c + 3 * nq + 3 * nv, c + 3 * nq + 3 * nv + nu, c + 3 * nq + 3 * nv + 2 * nu};
   }
   // every stream the solver launches on
-  hipError_t sync_all() { return hipStreamSynchronize(stream); }
+  hipError_t sync_all() {
+    hipError_t e = hipStreamSynchronize(stream);
+    for (auto fs : fd_stream)
+      if (e == hipSuccess && fs) e = hipStreamSynchronize(fs);
+    return e;
+  }
   ~ilqg_solver() {
     (void)sync_all();
     for (auto& v : ev)
@@ -325,6 +339,9 @@ struct ilqg_solver {
         (void)hipEventDestroy(p.second);
       }
     for (auto e : event_pool) (void)hipEventDestroy(e);
+    for (auto e : pipe_ev) (void)hipEventDestroy(e);
+    for (auto fs : fd_stream)
+      if (fs) (void)hipStreamDestroy(fs);
     if (own_stream) (void)hipStreamDestroy(own_stream);
   }
 };
@@ -671,6 +688,40 @@ int ilqg_solver_create(const ilqg_model* mc, const ilqg_solver_opts* o, const il
     }
   }
   ALLOC(s->fault, 16);
+  s->pipe_chunk = getenv_int("ILQG_PIPE_CHUNK", 16);
+  s->pipe_flat = getenv_int("ILQG_PIPE_FLAT", 0) != 0;
+  if (s->A == 1 && s->pipe_chunk > 0 && s->pipe_chunk < (int)P) {
+    // the sweep streams leave CUs to the rollout: a rollout chunk's workgroup
+    // (the humanoid's: 147 KB of LDS, a CU to itself) waited up to 13 ms for
+    // sweep teams to free a whole CU (rocprofv3 kernel trace); one CU per seed,
+    // spread over the chip, is never given to the sweep
+    int ncu = 0;
+    e = hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, o->device);
+    if (e != hipSuccess) return fail_free(e, "hipDeviceGetAttribute");
+    // (ILQG_PIPE_KEEP: how many; ILQG_PIPE_LOW=1: the lowest-numbered ones)
+    const int keep = std::min(getenv_int("ILQG_PIPE_KEEP", (int)S), ncu / 4);
+    const bool low = getenv_int("ILQG_PIPE_LOW", 0) != 0;
+    std::vector<uint32_t> fmask((ncu + 31) / 32, 0);
+    for (int c = 0, j = 0; c < ncu; c++) {
+      const bool r = low ? c < keep : (j < keep && (long)c * keep / ncu >= j);  // spread: over every XCD
+      if (r) j++;
+      else fmask[c / 32] |= 1u << (c % 32);
+    }
+    for (auto& fs : s->fd_stream) {
+      e = keep > 0 ? hipExtStreamCreateWithCUMask(&fs, (uint32_t)fmask.size(), fmask.data())
+                   : hipStreamCreateWithFlags(&fs, hipStreamNonBlocking);
+      if (e != hipSuccess) return fail_free(e, "hipStreamCreate");
+    }
+    for (int f = 0; f < 5; f++) ALLOC(s->carry[f], S * fld[f] * 8);
+    const int nch = ((int)P + s->pipe_chunk - 1) / s->pipe_chunk + 32 + ilqg_solver::kFdStreams;
+    s->pipe_ev.resize(nch, nullptr);
+    for (auto& ev : s->pipe_ev) {
+      e = hipEventCreateWithFlags(&ev, hipEventDisableTiming);
+      if (e != hipSuccess) return fail_free(e, "hipEventCreate");
+    }
+  } else {
+    s->pipe_chunk = 0;
+  }
   ALLOC(s->warm_c, S * P * h.nv * 8);
   ALLOC(s->cost_c, S * P * 8);
   ALLOC(s->V, S * s->nx * s->nx * 8);
@@ -825,6 +876,8 @@ static TrajDev toff(TrajDev t, size_t pts, const HostModel& h) {
 }
 
 // rollout of every (seed, alpha) candidate of the range, then selection + setDInit
+static hipError_t rollout_launch(ilqg_solver* s, const SeedRange& r, RollChunk ch);
+static hipError_t fd_range_launch(ilqg_solver* s, int p0, int np, hipStream_t st);
 static hipError_t forward_range(ilqg_solver* s, const SeedRange& r) {
   const ilqg_model* m = s->model;
   const HostModel& h = m->host;
@@ -837,15 +890,78 @@ static hipError_t forward_range(ilqg_solver* s, const SeedRange& r) {
   const double* qa = s->qfrc_applied.as<double>() + s0 * h.nv;
   const double* xf = s->xfrc_applied.as<double>() + s0 * 6 * h.nbody;
   double* cc = s->cost_cand.as<double>() + s0 * A;
-  hipError_t e = s->timed(0, [&] {
-    return launch_rollout_coop(m->dm, m->Lc, m->C, m->X, r.ns, s->A, s->P, nom, outv, multi ? 1 : 0, K, k,
-                               s->alphas.as<double>(), di, qa, xf, 0, s->cview(), cc, r.st);
-  }, r.st);
+  hipError_t e = rollout_launch(s, r, RollChunk{});
   if (e != hipSuccess) return e;
   return s->timed(1, [&] {
     return launch_select(m->dm, r.ns, s->A, s->P, s->opts.select_mode, multi ? 1 : 0, cc, s->sel.as<int>() + s0,
                          s->cost_sel.as<double>() + s0, outv, nom, di, r.st);
   }, r.st);
+}
+
+// the rollout of every (seed, alpha) candidate of the range over ch's points
+static hipError_t rollout_launch(ilqg_solver* s, const SeedRange& r, RollChunk ch) {
+  const ilqg_model* m = s->model;
+  const HostModel& h = m->host;
+  const size_t s0 = r.s0, P = s->P, A = s->A, nx = s->nx;
+  TrajDev nom = toff(s->tview(s->traj), s0 * P, h), di = toff(s->tview(s->dinit), s0, h);
+  const bool multi = s->A > 1;
+  TrajDev outv = multi ? toff(s->tview(s->cand), s0 * A * P, h) : nom;
+  const double* K = s->K.as<double>() + s0 * P * h.nu * nx;
+  const double* k = s->k.as<double>() + s0 * P * h.nu;
+  const double* qa = s->qfrc_applied.as<double>() + s0 * h.nv;
+  const double* xf = s->xfrc_applied.as<double>() + s0 * 6 * h.nbody;
+  double* cc = s->cost_cand.as<double>() + s0 * A;
+  if (ch.n_hi >= 0) ch.carry = toff(s->tview(s->carry), s0 * A, h);
+  return s->timed(0, [&] {
+    return launch_rollout_coop(m->dm, m->Lc, m->C, m->X, r.ns, s->A, s->P, nom, outv, multi ? 1 : 0, K, k,
+                               s->alphas.as<double>(), di, qa, xf, 0, s->cview(), cc, r.st, ch);
+  }, r.st);
+}
+
+// iterate() with one candidate per seed and the unfused sweep: the rollout in
+// chunks of pipe_chunk points (descending, as the rollout runs), and behind
+// each chunk, on fd_stream, the FD sweep of the points it finished -- every
+// point's record depends only on its own trajectory entry, so the sweep runs
+// under the (latency-bound, one-workgroup-per-seed) rollout instead of after
+// it; then selection / setDInit and the recursion once every record is in.
+// The same launches' work as ilqg_forward + ilqg_fd_sweep + ilqg_backward:
+// the same bits (tests/test_gpu_parity.py::test_pipelined_iterate).
+static int iterate_pipelined(ilqg_solver* s) {
+  const ilqg_model* m = s->model;
+  const SeedRange r = whole(s);
+  const int P = s->P, C = s->pipe_chunk;
+  int ev = 0;
+  // chunks of C points, halving toward the end (the last chunks' sweeps are
+  // what the recursion waits for: a small chunk's sweep takes about one
+  // team's latency)
+  for (int hi = P - 1, n; hi >= 0; hi -= n) {
+    const int rem = hi + 1;
+    n = rem >= 2 * C ? C : (rem + 1) / 2;
+    if (n < 1) n = 1;
+    if (s->pipe_flat) n = C;
+    const int lo = hi - n + 1 > 0 ? hi - n + 1 : 0;
+    RollChunk ch;
+    ch.n_hi = hi;
+    ch.n_lo = lo;
+    HIPCHK(rollout_launch(s, r, ch));
+    HIPCHK(hipEventRecord(s->pipe_ev[ev], s->stream));
+    hipStream_t fs = s->fd_stream[ev % ilqg_solver::kFdStreams];
+    HIPCHK(hipStreamWaitEvent(fs, s->pipe_ev[ev], 0));
+    ev++;
+    HIPCHK(s->timed(3, [&] { return fd_range_launch(s, lo, hi - lo + 1, fs); }, fs));
+  }
+  // selection + setDInit (one candidate: the rollout wrote the nominal trajectory)
+  const TrajDev nom = s->tview(s->traj), di = s->tview(s->dinit);
+  HIPCHK(s->timed(1, [&] {
+    return launch_select(m->dm, s->S, s->A, s->P, s->opts.select_mode, 0, s->cost_cand.as<double>(),
+                         s->sel.as<int>(), s->cost_sel.as<double>(), nom, nom, di, s->stream);
+  }));
+  for (auto fs : s->fd_stream) {
+    HIPCHK(hipEventRecord(s->pipe_ev[ev], fs));
+    HIPCHK(hipStreamWaitEvent(s->stream, s->pipe_ev[ev], 0));
+    ev++;
+  }
+  return ilqg_backward(s);
 }
 
 int ilqg_forward(ilqg_solver* s) {
@@ -977,36 +1093,38 @@ int ilqg_fd_sweep(ilqg_solver* s) {
 // GPUs; the records are then all-gathered and every rank runs the recursion).
 // The unfused kernels of the solver's FD precision, one launch pair per seed;
 // the same records the whole-trajectory sweep writes.
+static hipError_t fd_range_launch(ilqg_solver* s, int p0, int np, hipStream_t st) {
+  const ilqg_model* m = s->model;
+  const HostModel& h = m->host;
+  constexpr int kOneSeed = 1 << 30;  // the kernels' seed index pt / P is 0 for every point of the range
+  for (int sd = 0; sd < s->S; sd++) {
+    const size_t pt0 = (size_t)sd * s->P + p0;
+    const TrajDev nom = toff(s->tview(s->traj), pt0, h);
+    const double* qa = s->qfrc_applied.as<double>() + (size_t)sd * h.nv;
+    const double* xa = s->xfrc_applied.as<double>() + (size_t)sd * 6 * h.nbody;
+    double* wc = s->warm_c.as<double>() + pt0 * h.nv;
+    double* cc = s->cost_c.as<double>() + pt0;
+    double* dv = s->deriv.as<double>() + pt0 * s->Dp;
+    hipError_t e;
+    if (s->fdprec == ILQG_FD_F32) {
+      e = launch_fd_sweep_f32(m->dm, m->Lc, m->C, m->X, nom, np, kOneSeed, qa, xa, s->cview(), wc, cc, dv, s->Dp,
+                              ILQG_FD32_EPS, st);
+    } else {
+      e = launch_fd_centre_coop(m->dm, m->Lc, m->C, m->X, nom, np, kOneSeed, qa, xa, s->cview(), wc, cc, st);
+      if (e == hipSuccess)
+        e = launch_fd_cols_coop(m->dm, m->Lc, m->C, m->X, nom, np, kOneSeed, qa, xa, s->cview(), wc, cc, dv, s->Dp,
+                                st);
+    }
+    if (e != hipSuccess) return e;
+  }
+  return hipSuccess;
+}
+
 int ilqg_fd_sweep_range(ilqg_solver* s, int p0, int np) {
   if (!s || !s->initialized) return fail(ILQG_ERR_ARG, "solver not initialised");
   if (p0 < 0 || np < 0 || p0 + np > s->P) return fail(ILQG_ERR_ARG, "point range outside the trajectory");
   if (!np) return ILQG_OK;
-  const ilqg_model* m = s->model;
-  const HostModel& h = m->host;
-  constexpr int kOneSeed = 1 << 30;  // the kernels' seed index pt / P is 0 for every point of the range
-  HIPCHK(s->timed(3, [&] {
-    for (int sd = 0; sd < s->S; sd++) {
-      const size_t pt0 = (size_t)sd * s->P + p0;
-      const TrajDev nom = toff(s->tview(s->traj), pt0, h);
-      const double* qa = s->qfrc_applied.as<double>() + (size_t)sd * h.nv;
-      const double* xa = s->xfrc_applied.as<double>() + (size_t)sd * 6 * h.nbody;
-      double* wc = s->warm_c.as<double>() + pt0 * h.nv;
-      double* cc = s->cost_c.as<double>() + pt0;
-      double* dv = s->deriv.as<double>() + pt0 * s->Dp;
-      hipError_t e;
-      if (s->fdprec == ILQG_FD_F32) {
-        e = launch_fd_sweep_f32(m->dm, m->Lc, m->C, m->X, nom, np, kOneSeed, qa, xa, s->cview(), wc, cc, dv, s->Dp,
-                                ILQG_FD32_EPS, s->stream);
-      } else {
-        e = launch_fd_centre_coop(m->dm, m->Lc, m->C, m->X, nom, np, kOneSeed, qa, xa, s->cview(), wc, cc, s->stream);
-        if (e == hipSuccess)
-          e = launch_fd_cols_coop(m->dm, m->Lc, m->C, m->X, nom, np, kOneSeed, qa, xa, s->cview(), wc, cc, dv, s->Dp,
-                                  s->stream);
-      }
-      if (e != hipSuccess) return e;
-    }
-    return hipSuccess;
-  }));
+  HIPCHK(s->timed(3, [&] { return fd_range_launch(s, p0, np, s->stream); }));
   return ILQG_OK;
 }
 
@@ -1035,6 +1153,7 @@ int ilqg_backward(ilqg_solver* s) {
 
 int ilqg_iterate(ilqg_solver* s) {
   if (!s || !s->initialized) return fail(ILQG_ERR_ARG, "solver not initialised");
+  if (!s->fused && s->pipe_chunk > 0) return iterate_pipelined(s);
   int rc = ilqg_forward(s);
   if (rc) return rc;
   if (s->fused) {

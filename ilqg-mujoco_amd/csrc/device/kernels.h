@@ -16,6 +16,17 @@ struct TrajDev {
   double* ctrl;
 };
 
+// a rollout launch over points n_hi .. n_lo (descending) of the horizon: the
+// whole trajectory (n_hi < 0, the default), or one chunk of a chunked rollout
+// whose FD sweep runs behind it (ilqg_iterate's pipelined path).  A chunk that
+// does not start at point P-1 takes its state from carry[candidate] and adds
+// to the candidate's cost already in cost_cand; one that does not end at
+// point 0 leaves its state in carry[candidate].
+struct RollChunk {
+  TrajDev carry{};
+  int n_hi = -1, n_lo = 0;
+};
+
 // device cost descriptor (all 9 arrays present, zero where unused)
 struct CostDev {
   const double *wq, *tq, *lq, *wv, *tv, *lv, *wu, *tu, *lu;
@@ -142,7 +153,7 @@ hipError_t launch_rollout_coop(const DevModel& m, const WsLayout& L, const coop:
                                const coop::CoopAux& X, int S, int A, int P, TrajDev nominal, TrajDev out,
                                int out_is_cand, const double* K, const double* k, const double* alphas, TrajDev dinit,
                                const double* qfrc_applied, const double* xfrc_applied, int passive, CostDev cost,
-                               double* cost_cand, hipStream_t st);
+                               double* cost_cand, hipStream_t st, RollChunk ch = RollChunk{});
 // n independent states, one wavefront each: nstep mj_step (in place)
 hipError_t launch_step_coop(const DevModel& m, const WsLayout& L, const coop::CoopLayout& C, const coop::CoopAux& X,
                             TrajDev stt, int n, int nstep, const double* qfrc_applied, const double* xfrc_applied,

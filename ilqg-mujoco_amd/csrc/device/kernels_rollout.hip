@@ -24,7 +24,7 @@ namespace ilqg {
 namespace {
 
 __device__ inline void rollout_body(const auto& m, const auto& L, const auto& C, const auto& X, const Team& T,
-                                int S, int A, int P, TrajDev nom, TrajDev out, int out_is_cand, const double* K, const double* k, const double* alphas, TrajDev dinit, const double* qfrc_applied, const double* xfrc_applied, int passive, CostDev cost, double* cost_cand, int wave, auto split) {
+                                int S, int A, int P, TrajDev nom, TrajDev out, int out_is_cand, const double* K, const double* k, const double* alphas, TrajDev dinit, const double* qfrc_applied, const double* xfrc_applied, int passive, CostDev cost, double* cost_cand, RollChunk ch, int wave, auto split) {
   // wave < 0: one-wave team; 0/1: primary/helper wave of a two-wave team (step_dual)
   const bool prim = wave <= 0;
   STAMP_INIT();
@@ -34,7 +34,11 @@ __device__ inline void rollout_body(const auto& m, const auto& L, const auto& C,
   const int lane = blockIdx.x;
   const int s = lane / A, a = lane % A;
   const int nq = m.nq, nv = m.nv, nu = m.nu, nx = 2 * nv;
-  load_state(m, L, T, dinit, s, s, qfrc_applied, xfrc_applied);
+  // the points this launch rolls over (RollChunk): n_hi .. n_lo, descending
+  const int nhi = ch.n_hi >= 0 ? ch.n_hi : P - 1, nlo = ch.n_hi >= 0 ? ch.n_lo : 0;
+  const bool resume = nhi < P - 1;
+  if (resume) load_state(m, L, T, ch.carry, lane, s, qfrc_applied, xfrc_applied);
+  else load_state(m, L, T, dinit, s, s, qfrc_applied, xfrc_applied);
   const CostDev cl = stage_cost(m, C, T, cost);
   double* qpos = T.w + L.qpos;
   double* qvel = T.w + L.qvel;
@@ -69,7 +73,7 @@ __device__ inline void rollout_body(const auto& m, const auto& L, const auto& C,
   // larger records are not prefetched: park() copies them from global memory directly
   const bool pfok = R <= PFR * TEAM_SIZE;
   if (!passive) {
-    FOR_T(t, R) rec[t] = fetch((size_t)s * P + (P - 1), t);
+    FOR_T(t, R) rec[t] = fetch((size_t)s * P + nhi, t);
     TSYNC();
   }
   const double alpha = alphas ? alphas[a] : 1.0;
@@ -78,6 +82,7 @@ __device__ inline void rollout_body(const auto& m, const auto& L, const auto& C,
   // of a two-wave team (beside the primary's kinematics), else the only wave
   const bool ctl = wave < 0 || wave == 1;
   double c = 0;
+  if (resume && ctl && T.tid == 0 && cost_cand) c = cost_cand[lane];
   // control law u = u* + alpha k + K (x - x*) for point n, its record and cost
   // (ilqr.h:116-133); the next point's nominal record is prefetched first
   auto pre_step = [&](int n) {
@@ -147,7 +152,7 @@ __device__ inline void rollout_body(const auto& m, const auto& L, const auto& C,
     if (threadIdx.x == 0) T.ci[C.ibc + 3] = T.ci[C.ibc + 4] = T.ci[C.ibc + 6] = T.ci[C.ibc + 7] = 0;
     __syncthreads();
   }
-  for (int n = P - 1; n >= 0; n--) {
+  for (int n = nhi; n >= nlo; n--) {
     if (wave < 0) {
       pre_step(n);
       step(m, L, C, X, T);
@@ -166,6 +171,19 @@ __device__ inline void rollout_body(const auto& m, const auto& L, const auto& C,
     }
   }
   if (ctl && T.tid == 0 && cost_cand) cost_cand[lane] = c;
+  if (nlo > 0) {
+    // the state the next chunk starts from (point nlo - 1, before its control)
+    if (wave >= 0) __syncthreads();
+    if (prim) {
+      FOR_T(i, nq) ch.carry.qpos[(size_t)lane * nq + i] = qpos[i];
+      FOR_T(i, nv) {
+        ch.carry.qvel[(size_t)lane * nv + i] = qvel[i];
+        ch.carry.warm[(size_t)lane * nv + i] = warm[i];
+      }
+      FOR_T(i, nu) ch.carry.ctrl[(size_t)lane * nu + i] = ctrl[i];
+      if (T.tid == 0) ch.carry.time[lane] = T.w[L.time];
+    }
+  }
 #ifdef ILQG_STAMPS
   if (prim && T.tid == 0 && blockIdx.x == 0) {
     g_stamp_acc[46] += __builtin_amdgcn_s_memrealtime() - rt0;
@@ -175,41 +193,41 @@ __device__ inline void rollout_body(const auto& m, const auto& L, const auto& C,
   STAMP_FLUSH();
 }
 
-__global__ __launch_bounds__(TEAM) void k_rollout_coop(DevModel mg, WsLayout L, CoopLayout C, CoopAux Xg, int S, int A, int P, TrajDev nom, TrajDev out, int out_is_cand, const double* K, const double* k, const double* alphas, TrajDev dinit, const double* qfrc_applied, const double* xfrc_applied, int passive, CostDev cost, double* cost_cand) {
+__global__ __launch_bounds__(TEAM) void k_rollout_coop(DevModel mg, WsLayout L, CoopLayout C, CoopAux Xg, int S, int A, int P, TrajDev nom, TrajDev out, int out_is_cand, const double* K, const double* k, const double* alphas, TrajDev dinit, const double* qfrc_applied, const double* xfrc_applied, int passive, CostDev cost, double* cost_cand, RollChunk ch) {
   Team T = make_team(L, C);
   DevModel m;
   CoopAux X;
   stage_model(mg, Xg, L, C, T, m, X);
-  rollout_body(m, L, C, X, T, S, A, P, nom, out, out_is_cand, K, k, alphas, dinit, qfrc_applied, xfrc_applied, passive, cost, cost_cand, -1, std::false_type{});
+  rollout_body(m, L, C, X, T, S, A, P, nom, out, out_is_cand, K, k, alphas, dinit, qfrc_applied, xfrc_applied, passive, cost, cost_cand, ch, -1, std::false_type{});
 }
 
 // model-specific instance (static_models.h): compile-time sizes, tables and LDS layout
 template <class SM, class SX>
-__global__ __launch_bounds__(TEAM) void k_rollout_s(DevModel mg, int S, int A, int P, TrajDev nom, TrajDev out, int out_is_cand, const double* K, const double* k, const double* alphas, TrajDev dinit, const double* qfrc_applied, const double* xfrc_applied, int passive, CostDev cost, double* cost_cand) {
+__global__ __launch_bounds__(TEAM) void k_rollout_s(DevModel mg, int S, int A, int P, TrajDev nom, TrajDev out, int out_is_cand, const double* K, const double* k, const double* alphas, TrajDev dinit, const double* qfrc_applied, const double* xfrc_applied, int passive, CostDev cost, double* cost_cand, RollChunk ch) {
   static constexpr WsLayout L = make_layout(SM{}, SX::npair);
   static constexpr CoopLayout C = make_coop_layout(SM{}, SX::npair);
   static constexpr SX X{};
   Team T = make_team(L, C);
   SM m;
   stage_model_sep(mg, T, m);
-  rollout_body(m, L, C, X, T, S, A, P, nom, out, out_is_cand, K, k, alphas, dinit, qfrc_applied, xfrc_applied, passive, cost, cost_cand, -1, std::false_type{});
+  rollout_body(m, L, C, X, T, S, A, P, nom, out, out_is_cand, K, k, alphas, dinit, qfrc_applied, xfrc_applied, passive, cost, cost_cand, ch, -1, std::false_type{});
 }
 
 // two-wave teams (step_dual): 128 threads per (seed, candidate)
-__global__ __launch_bounds__(2 * TEAM) void k_rollout2_coop(DevModel mg, WsLayout L, CoopLayout C, CoopAux Xg, int S, int A, int P, TrajDev nom, TrajDev out, int out_is_cand, const double* K, const double* k, const double* alphas, TrajDev dinit, const double* qfrc_applied, const double* xfrc_applied, int passive, CostDev cost, double* cost_cand) {
+__global__ __launch_bounds__(2 * TEAM) void k_rollout2_coop(DevModel mg, WsLayout L, CoopLayout C, CoopAux Xg, int S, int A, int P, TrajDev nom, TrajDev out, int out_is_cand, const double* K, const double* k, const double* alphas, TrajDev dinit, const double* qfrc_applied, const double* xfrc_applied, int passive, CostDev cost, double* cost_cand, RollChunk ch) {
   Team T = make_team(L, C);
   DevModel m;
   CoopAux X;
   stage_model(mg, Xg, L, C, T, m, X);
   rollout_body(m, L, C, X, T, S, A, P, nom, out, out_is_cand, K, k, alphas, dinit, qfrc_applied, xfrc_applied,
-               passive, cost, cost_cand, (int)(threadIdx.x / TEAM), std::false_type{});
+               passive, cost, cost_cand, ch, (int)(threadIdx.x / TEAM), std::false_type{});
 }
 // three-wave teams for the compile-time register-row models (step_dual_split),
 // two-wave otherwise
 template <class SM>
 constexpr int rollout_waves() { return SM::nv <= RMAX ? 3 : 2; }
 template <class SM, class SX>
-__global__ __launch_bounds__(3 * TEAM) void k_rollout2_s(DevModel mg, int S, int A, int P, TrajDev nom, TrajDev out, int out_is_cand, const double* K, const double* k, const double* alphas, TrajDev dinit, const double* qfrc_applied, const double* xfrc_applied, int passive, CostDev cost, double* cost_cand) {
+__global__ __launch_bounds__(3 * TEAM) void k_rollout2_s(DevModel mg, int S, int A, int P, TrajDev nom, TrajDev out, int out_is_cand, const double* K, const double* k, const double* alphas, TrajDev dinit, const double* qfrc_applied, const double* xfrc_applied, int passive, CostDev cost, double* cost_cand, RollChunk ch) {
   static constexpr WsLayout L = make_layout(SM{}, SX::npair, true);
   static constexpr CoopLayout C = make_coop_layout(SM{}, SX::npair);
   static constexpr SX X{};
@@ -217,7 +235,7 @@ __global__ __launch_bounds__(3 * TEAM) void k_rollout2_s(DevModel mg, int S, int
   SM m;
   stage_model_sep(mg, T, m);
   rollout_body(m, L, C, X, T, S, A, P, nom, out, out_is_cand, K, k, alphas, dinit, qfrc_applied, xfrc_applied,
-               passive, cost, cost_cand, (int)(threadIdx.x / TEAM), std::bool_constant<SM::nv <= RMAX>{});
+               passive, cost, cost_cand, ch, (int)(threadIdx.x / TEAM), std::bool_constant<SM::nv <= RMAX>{});
 }
 
 // ---- batch physics (ilqg_step_batch / ilqg_forward_batch): one wavefront per state
@@ -358,7 +376,7 @@ hipError_t launch_rollout_coop(const DevModel& m, const WsLayout& L, const CoopL
                                int A, int P, TrajDev nominal, TrajDev out, int out_is_cand, const double* K,
                                const double* k, const double* alphas, TrajDev dinit, const double* qfrc_applied,
                                const double* xfrc_applied, int passive, CostDev cost, double* cost_cand,
-                               hipStream_t st) {
+                               hipStream_t st, RollChunk ch) {
   const size_t lds = rollout_lds(coop_lds_bytes(L, C));
   hipError_t e;
   if (use_dual()) {
@@ -370,7 +388,7 @@ hipError_t launch_rollout_coop(const DevModel& m, const WsLayout& L, const CoopL
     hipLaunchKernelGGL((k_rollout2_s<stat::SMT, stat::SXT>), dim3(S * A),                                       \
                        dim3(rollout_waves<stat::SMT>() * TEAM), lds2, st, m, S, A, P,                            \
                        nominal, out, out_is_cand, K, k, alphas, dinit, qfrc_applied, xfrc_applied, passive, cost, \
-                       cost_cand);                                                                              \
+                       cost_cand, ch);                                                                              \
     return hipGetLastError();                                                                                   \
   }
     switch (m.static_id) {
@@ -382,7 +400,7 @@ hipError_t launch_rollout_coop(const DevModel& m, const WsLayout& L, const CoopL
     e = allow_lds(k_rollout2_coop, lds);
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(k_rollout2_coop, dim3(S * A), dim3(2 * TEAM), lds, st, m, L, C, X, S, A, P, nominal, out,
-                       out_is_cand, K, k, alphas, dinit, qfrc_applied, xfrc_applied, passive, cost, cost_cand);
+                       out_is_cand, K, k, alphas, dinit, qfrc_applied, xfrc_applied, passive, cost, cost_cand, ch);
     return hipGetLastError();
   }
 #define ILQG_CASE(id, SMT, SXT)                                                                                 \
@@ -391,7 +409,7 @@ hipError_t launch_rollout_coop(const DevModel& m, const WsLayout& L, const CoopL
     if (e != hipSuccess) return e;                                                                              \
     hipLaunchKernelGGL((k_rollout_s<stat::SMT, stat::SXT>), dim3(S * A), dim3(TEAM), lds, st, m, S, A, P,        \
                        nominal, out, out_is_cand, K, k, alphas, dinit, qfrc_applied, xfrc_applied, passive, cost, \
-                       cost_cand);                                                                              \
+                       cost_cand, ch);                                                                              \
     return hipGetLastError();
   switch (m.static_id) {
     ILQG_STATIC_MODELS(ILQG_CASE)
@@ -402,7 +420,7 @@ hipError_t launch_rollout_coop(const DevModel& m, const WsLayout& L, const CoopL
   e = allow_lds(k_rollout_coop, coop_lds_bytes(L, C));
   if (e != hipSuccess) return e;
   hipLaunchKernelGGL(k_rollout_coop, dim3(S * A), dim3(TEAM), coop_lds_bytes(L, C), st, m, L, C, X, S, A, P, nominal,
-                     out, out_is_cand, K, k, alphas, dinit, qfrc_applied, xfrc_applied, passive, cost, cost_cand);
+                     out, out_is_cand, K, k, alphas, dinit, qfrc_applied, xfrc_applied, passive, cost, cost_cand, ch);
   return hipGetLastError();
 }
 

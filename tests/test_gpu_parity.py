@@ -539,6 +539,46 @@ def test_fd_sweep_range_blocks(ia, ora, name, prec):
     exact(k, k_full, "k")
 
 
+@pytest.mark.parametrize("name,prec,chunk", [("humanoid", "f32", 7), ("humanoid", "f64", 5), ("hopper", "f64", 16)])
+def test_pipelined_iterate(ia, ora, name, prec, chunk, monkeypatch):
+    """ilqg_iterate with one candidate per seed and the unfused sweep rolls out
+    in chunks (ILQG_PIPE_CHUNK points each) with the FD sweep of every finished
+    chunk on a second stream behind it: the trajectory, records, gains and
+    value are the unchunked iteration's bit for bit (cfg 5: humanoid, fp32 FD,
+    MFMA recursion; the hopper through the unfused path, ILQG_FUSED=0, also
+    against the oracle)"""
+    import workloads
+    if name == "hopper":
+        monkeypatch.setenv("ILQG_FUSED", "0")
+        m, om = setup(ia, ora, name, ia.HOPPER_COST)
+        dmain, H, cost = workloads.hopper_dmain(m, 2, sigma=0.01), 40, ia.HOPPER_COST
+    else:
+        m = ia.Model.load(workloads.model_file(name))
+        dmain, H, cost = m.reset_state(1), 24, ia.HUMANOID_COST
+        dmain.qpos[0, 2] = 1.4
+    out = {}
+    for ch in (0, chunk):
+        monkeypatch.setenv("ILQG_PIPE_CHUNK", str(ch))
+        g = ia.ILQR(m, dmain, H, cost)
+        if prec == "f32":
+            g.set_fd_precision("f32")
+        if name == "humanoid":
+            g.set_riccati("mfma")
+        for _ in range(2):
+            g.iterate()
+        g.synchronize()
+        t = g.traj()
+        out[ch] = (t.qpos, t.qvel, t.ctrl, g.deriv(), *g.gains(), *g.value(), g.costs()[0])
+    for a, b, what in zip(out[0], out[chunk], ("qpos", "qvel", "ctrl", "deriv", "K", "k", "V", "v", "costs")):
+        exact(b, a, what)
+    if name == "hopper":
+        P = H + 1
+        for s in range(2):
+            il = _oracle_ilqr(ora, om, _state_dict(dmain, s), H, "ora_cost_desc_fn", 2)
+            exact(out[chunk][4][s], il.arrays()["K"], f"seed {s} K vs oracle")
+            exact(out[chunk][0][s * P:(s + 1) * P], il.traj()["qpos"], f"seed {s} qpos vs oracle")
+
+
 def test_bench_workload_bitexact(ia, ora):
     """The exact timed workload of bench.py (cfg 4's per-GPU share: hopper H=500,
     8 seeds x 8 line-search candidates alpha = 2^-i, select='min_cost'), three

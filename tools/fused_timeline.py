@@ -104,4 +104,8 @@ sh = (hwid >> 12) & 1
 se = (hwid >> 13) & 0x7
 key = xcc * 1000 + se * 100 + sh * 16 + cu_id
 print(f"  distinct (xcc, se, sh, cu) used: {len(np.unique(key))}; xcc histogram {np.bincount(xcc.astype(np.int64))}")
+if os.environ.get("TL_SAVE"):
+    # raw per-item start / end (us from the first start) and role, for offline schedule studies
+    np.savez(os.environ["TL_SAVE"], start=us(st), end=us(en), ok=ok, role=role, S=S, P=P, ncw=ncw,
+             tb=np.array([[us(tb[s_, 0]), us(tb[s_, 1])] for s_ in range(S)]))
 del g
