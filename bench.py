@@ -325,7 +325,10 @@ def run_humanoid_cfg5(args, world, rank, local_rank):
     fd_ms = sum(kt[k]["avg_ms"] for k in ("fd_centre", "fd_cols") if k in kt)
     bw_ms = kt.get("backward", {}).get("avg_ms", 0.0)
     roll_ms = kt.get("rollout", {}).get("avg_ms", 0.0)
-    fd_pts = rx.np if shard else P  # points this rank's FD launch differentiates
+    # points one FD launch differentiates: this rank's block, over the chunks
+    # of the pipelined iteration (ILQG_PIPE_CHUNK: one sweep launch per chunk)
+    fd_launches = max((kt.get("fd_cols", {}).get("launches", 0) or kt.get("fd_centre", {}).get("launches", 0)), 1)
+    fd_pts = (rx.np if shard else P) / max(fd_launches / args.steps, 1.0)
     fd_tf = fd_pts * hf["fd_point"]["flops"] / (fd_ms * 1e-3) / 1e12 if fd_ms else 0.0
     bw_tf = H * hf["riccati_step"]["flops"] / (bw_ms * 1e-3) / 1e12 if bw_ms else 0.0
     value = (1 if shard else world) * args.steps / elapsed

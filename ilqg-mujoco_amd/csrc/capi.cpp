@@ -699,8 +699,13 @@ int ilqg_solver_create(const ilqg_model* mc, const ilqg_solver_opts* o, const il
     e = hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, o->device);
     if (e != hipSuccess) return fail_free(e, "hipDeviceGetAttribute");
     // (ILQG_PIPE_KEEP: how many; ILQG_PIPE_LOW=1: the lowest-numbered ones)
-    const int keep = std::min(getenv_int("ILQG_PIPE_KEEP", (int)S), ncu / 4);
-    const bool low = getenv_int("ILQG_PIPE_LOW", 0) != 0;
+    // Default: the lowest ncu / 8 CUs -- one XCD's worth, so the rollout keeps an
+    // L2 of its own (the humanoid reads its model image from global memory
+    // every step): cfg 5 rollout chunks 212 -> 177 us per step beside the
+    // sweep (profiles/r05_cfg5_pipeline.txt; one CU per seed spread over the
+    // chip did not help)
+    const int keep = std::min(getenv_int("ILQG_PIPE_KEEP", std::max((int)S, ncu / 8)), ncu / 4);
+    const bool low = getenv_int("ILQG_PIPE_LOW", 1) != 0;
     std::vector<uint32_t> fmask((ncu + 31) / 32, 0);
     for (int c = 0, j = 0; c < ncu; c++) {
       const bool r = low ? c < keep : (j < keep && (long)c * keep / ncu >= j);  // spread: over every XCD

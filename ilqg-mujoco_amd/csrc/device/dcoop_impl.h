@@ -3886,6 +3886,110 @@ __device__ inline void factor_m_and_euler(const auto& m, const auto& L, const au
 #endif
 }
 
+// The primary's phase 4 under ILQG_SPLIT3 in one pass of registers: lane 0
+// factors M and, with that factor still in its registers, solves qacc_smooth =
+// M^-1 qfrc_smooth; lane 1 factors M + h D (Euler with damping).  The same
+// operations as factor_m_and_euler (factor_ld_lanes' loop) followed by
+// fwd_acceleration_u (the tree solve of solve_ld_rows' sequence), without the
+// factor's round trip through LDS between them.  Returns false, having done
+// nothing, when a body carries xfrc_applied (the general path runs).
+#ifndef ILQG_FACC
+#define ILQG_FACC 1
+#endif
+template <class MT>
+__device__ inline bool factor_acc_u(const auto& m, const auto& L, const auto& X, const Team& T, bool eul) {
+  constexpr int NV = MT::nv, NB = MT::nbody;
+  using XT = std::remove_cvref_t<decltype(X)>;
+  (void)X;
+  const real* xf = T.w + L.xfrc_applied;
+  static_assert(6 * NB <= TEAM_SIZE, "one ballot over xfrc_applied");
+  if (__ballot(T.tid >= 6 && T.tid < 6 * NB && xf[T.tid] != 0) != 0ull) return false;
+  const bool two = eul && euler_damped(m, T);
+  const bool l1 = two && T.tid == 1;
+  const real *qp = T.w + L.qfrc_passive, *qb = T.w + L.qfrc_bias, *qap = T.w + L.qfrc_applied;
+  const real* qa = T.w + L.qfrc_act;
+  const real* qM = T.w + L.qM;
+  real v[NV], a[NV][NV];
+  sfor<0, NV>(SLAM(jj) {
+    constexpr int j = SK(jj);
+    real t = qp[j] - qb[j];
+    t += qap[j];
+    t += qa[j];
+    v[j] = t;
+  });
+  sfor<0, NV>(SLAM(ii) {
+    constexpr int i = SK(ii);
+    sfor<0, i + 1>(SLAM(jj) { a[i][SK(jj)] = qM[i * NV + SK(jj)]; });
+    const real s_ = a[i][i] + m.opt_timestep * m.dof_damping[i];
+    a[i][i] = l1 ? s_ : a[i][i];
+  });
+  // the factor (factor_ld_lanes' loop)
+  sfor<0, NV>(SLAM(kk) {
+    constexpr int k = NV - 1 - SK(kk);
+    real dk = a[k][k];
+    if (dk < MINVAL) dk = MINVAL;
+    a[k][k] = dk;
+    sfor<0, k>(SLAM(ii) {
+      constexpr int i = k - 1 - SK(ii);
+      if constexpr ((XT::pmask[k] >> i) & 1) {
+        const real tmp = a[k][i] / dk;
+        sfor<0, i + 1>(SLAM(jj) {
+          constexpr int j = i - SK(jj);
+          if constexpr (j == i || ((XT::pmask[i] >> j) & 1)) a[i][j] -= tmp * a[k][j];
+        });
+        a[k][i] = tmp;
+      }
+    });
+  });
+  real dinv[NV];
+  sfor<0, NV>(SLAM(ii) { dinv[SK(ii)] = 1 / a[SK(ii)][SK(ii)]; });
+  // qacc_smooth = (L'DL)^-1 qfrc_smooth (fwd_acceleration_u's sequence), lane 0's factor
+  real x[NV];
+  sfor<0, NV>(SLAM(jj) { x[SK(jj)] = v[SK(jj)]; });
+  sfor<0, NV>(SLAM(ii) {
+    constexpr int i = NV - 1 - SK(ii);
+    const bool nz = x[i] != 0;
+    sfor<0, i>(SLAM(jj) {
+      constexpr int j = SK(jj);
+      if constexpr ((XT::pmask[i] >> j) & 1) {
+        const real u = x[j] - a[i][j] * x[i];
+        x[j] = nz ? u : x[j];
+      }
+    });
+  });
+  sfor<0, NV>(SLAM(ii) { x[SK(ii)] *= dinv[SK(ii)]; });
+  sfor<0, NV>(SLAM(ii) {
+    constexpr int i = SK(ii);
+    sfor<0, i>(SLAM(jj) {
+      constexpr int j = i - 1 - SK(jj);
+      if constexpr ((XT::pmask[i] >> j) & 1) x[i] -= a[i][j] * x[j];
+    });
+  });
+  // lane 0: the factor of M and both accelerations; lane 1: the factor of M + h D
+  if (T.tid == 0 || l1) {
+    real* s_ = T.w + L.s_euler;
+    real* LD = l1 ? s_ + NV + NV * NV : T.w + L.qLD;
+    real* Dinv = l1 ? s_ + NV + 2 * NV * NV : T.w + L.qLDinv;
+    sfor<0, NV>(SLAM(ii) {
+      constexpr int i = SK(ii);
+      sfor<0, NV>(SLAM(jj) {
+        constexpr int j = SK(jj);
+        if constexpr (j <= i) LD[i * NV + j] = a[i][j];
+        else LD[i * NV + j] = (real)0;
+      });
+      Dinv[i] = dinv[i];
+    });
+  }
+  if (T.tid == 0) {
+    sfor<0, NV>(SLAM(ii) {
+      T.w[L.qfrc_smooth + SK(ii)] = v[SK(ii)];
+      T.w[L.qacc_smooth + SK(ii)] = x[SK(ii)];
+    });
+  }
+  TSYNC();
+  return true;
+}
+
 // factor_m_and_euler split for the three-wave step: the factor of M, announced
 // on `fm` (step id sid) as soon as it is formed (phase 4; the primary's
 // acceleration stage waits for it), and the factor of M + h D, which only
@@ -4106,9 +4210,12 @@ __device__ inline void step_dual_split(const auto& m, const auto& L, const auto&
   if (A) {
     using MT = std::remove_cvref_t<decltype(m)>;
     if constexpr (split3) {
-      factor_m_and_euler(m, L, C, X, T, eul);
-      STAMP(3);
-      acc_done = fwd_acceleration_u<MT>(m, L, X, T);
+      if constexpr (ILQG_FACC) acc_done = factor_acc_u<MT>(m, L, X, T, eul);
+      if (!acc_done) {
+        factor_m_and_euler(m, L, C, X, T, eul);
+        STAMP(3);
+        acc_done = fwd_acceleration_u<MT>(m, L, X, T);
+      }
       STAMP(7);
     } else {
       if constexpr (vel_regs_ok<MT>() && ILQG_VEL_H) fwd_velocity_h<MT>(m, L, T);

@@ -105,6 +105,10 @@ __device__ inline void backward_seed_mfma(const MD& m, int nq, int nv, int nu, i
   __shared__ int trn[NU_MAX], perm[NU_MAX];  // STATIC_LDS_BYTES
   double* T4 = A;
   double* Vn = V;
+#ifdef ILQG_STAMPS
+  unsigned long long bst_prev = 0;  // BSTAMP (riccati.hip): per-stage cycles, diagnostic build
+#endif
+  BSTAMP(-1);
 
   // initV at the terminal point dArray[0] (inc/ilqr.h:100-107)
   {
@@ -163,12 +167,14 @@ __device__ inline void backward_seed_mfma(const MD& m, int nq, int nv, int nu, i
     __syncthreads();
     for (int i = tid; i < nx; i += THREADS) Vs[i + i * LX] += mu;
     __syncthreads();
+    BSTAMP(0);
     // stage 2: T1 = B' Vs (nu x nx)
     product(
         nu, nx, nx, [&](int a, int k) { return (a < nu && k < nx) ? B[k + a * LX] : 0.0; },
         [&](int k, int j) { return (k < nx && j < nx) ? Vs[k + j * LX] : 0.0; },
         [&](int a, int j, double x) { X1[a + j * LU] = x; }, wave, lane);
     __syncthreads();
+    BSTAMP(1);
     // stage 3: Mm = -2 T1 B - 2 R ; T3 = T1 A ; w = v + 2 Vs c
     auto gT1 = [&](int a, int k) { return (a < nu && k < nx) ? X1[a + k * LU] : 0.0; };
     product(
@@ -183,6 +189,7 @@ __device__ inline void backward_seed_mfma(const MD& m, int nq, int nv, int nu, i
       w[i] = v[i] + 2 * sm;
     }
     __syncthreads();
+    BSTAMP(2);
     // stage 4: LDLT of Mm (wave 0); col = B'w + r beside it (wave 1)
     if (wave == 0) ldlt_factor_wave(nu, Mm, trn, tmp, lane);
     for (int a = tid - 64; a >= 0 && a < nu; a += THREADS) {
@@ -191,6 +198,7 @@ __device__ inline void backward_seed_mfma(const MD& m, int nq, int nv, int nu, i
       col[a] = sm + r[a];
     }
     __syncthreads();
+    BSTAMP(3);
     // stage 5: K = ldlt.solve(2 T3) column-parallel (in place), k = ldlt.solve(B'w + r)
     // (columns dealt over the four waves: one solve per lane, every SIMD busy;
     // the vector in registers, ldlt_solve_reg)
@@ -208,6 +216,7 @@ __device__ inline void backward_seed_mfma(const MD& m, int nq, int nv, int nu, i
       ldlt_solve_reg(nu, Mm, perm, j < nx ? Y1 + j * LU : kl, j < nx + 1);
     }
     __syncthreads();
+    BSTAMP(4);
     // stage 6: ABK = A + B K ; T6 = K'R ; y = B k + c ; kR = k'R
     auto gK = [&](int a, int j) { return (a < nu && j < nx) ? Y1[a + j * LU] : 0.0; };
     product(
@@ -228,12 +237,14 @@ __device__ inline void backward_seed_mfma(const MD& m, int nq, int nv, int nu, i
       kR[b] = sm;
     }
     __syncthreads();
+    BSTAMP(5);
     // stage 7: T4 = ABK' Vs (into A's buffer: A is dead)
     product(
         nx, nx, nx, [&](int i, int k) { return (i < nx && k < nx) ? ABK[k + i * LX] : 0.0; },
         [&](int k, int j) { return (k < nx && j < nx) ? Vs[k + j * LX] : 0.0; },
         [&](int i, int j, double x) { T4[i + j * LX] = x; }, wave, lane);
     __syncthreads();
+    BSTAMP(6);
     // stage 8: V_new = (T4 ABK + q q') + T6 K (into V's buffer: V is dead)
     {
       const int mt = (nx + 15) / 16;
@@ -253,6 +264,7 @@ __device__ inline void backward_seed_mfma(const MD& m, int nq, int nv, int nu, i
       }
     }
     __syncthreads();
+    BSTAMP(7);
     // stage 9: z = (2y)' V_new ; v_new (reads the NEW V, quirk Q14)
     for (int j = tid; j < nx; j += THREADS) {
       double sm = 0;
@@ -276,6 +288,7 @@ __device__ inline void backward_seed_mfma(const MD& m, int nq, int nv, int nu, i
     }
     for (int a = tid; a < nu; a += THREADS) kg[pc * nu + a] = kl[a];
     __syncthreads();
+    BSTAMP(8);
     for (int i = tid; i < nx; i += THREADS) v[i] = vn[i];
     if (n + 1 < P) {
 #pragma unroll
@@ -285,6 +298,7 @@ __device__ inline void backward_seed_mfma(const MD& m, int nq, int nv, int nu, i
       }
     }
     __syncthreads();
+    BSTAMP(9);
   }
   if (Vg)
     for (int e = tid; e < nx * nx; e += THREADS) {

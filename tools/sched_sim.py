@@ -17,6 +17,8 @@ Orders:
                 point-major
   lpt-oracle    centres, then columns longest-first by their true duration
                 (a bound no predictor reaches)
+  split-long    identity, with the columns of long-centre points as two
+                halves of 0.68 x the column each (the measured cost of a half)
 """
 import heapq
 import sys
@@ -72,6 +74,9 @@ def main():
     mk3, _ = simulate(lpt, dur, dep, nC, slots)
     print(f"lpt-oracle: makespan {mk3:.0f} us")
     print(f"bound: total team-us / slots = {dur.sum() / slots:.0f} us")
+    for thr in (150, 300, 500, 800):
+        mk4, work = split_long(sys.argv[1], thr, slots)
+        print(f"split-long thr {thr:4d} us: makespan {mk4:.0f} us, team-us x{work:.3f}")
 
 
 def sim_centre_long(dur, dep, nC, ncw, slots, thr):
@@ -128,6 +133,30 @@ def sim_centre_long(dur, dep, nC, ncw, slots, thr):
                 heapq.heappush(prio, (end[item], nC + item * ncw + w))
         heapq.heappush(free, (end[item], k))
     return end.max()
+
+
+def split_long(path, thr, slots, frac=0.68):
+    """identity order, but the columns of points whose centre ran longer than
+    thr us run as two halves of frac x the column's duration each (measured:
+    a half costs 0.6-0.7 of the whole column, DESIGN.md 'Column halves')"""
+    d = np.load(path)
+    st, en, ok = d["start"], d["end"], d["ok"]
+    S, P, ncw = int(d["S"]), int(d["P"]), int(d["ncw"])
+    nC = S * P
+    dur = np.where(ok, en - st, np.median(en - st))
+    items, deps = list(dur[:nC]), list(range(nC))
+    for u in range(nC, len(dur)):
+        g = (u - nC) // ncw
+        if dur[g] > thr:
+            items += [frac * dur[u], frac * dur[u]]
+            deps += [g, g]
+        else:
+            items.append(dur[u])
+            deps.append(g)
+    items, deps = np.array(items), np.array(deps)
+    mk, _ = simulate(np.arange(len(items)), items, deps, nC, slots)
+    return mk, items.sum() / dur.sum()
+
 
 
 if __name__ == "__main__":

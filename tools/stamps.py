@@ -21,6 +21,7 @@ W2 = {48: "W2: limit rows+passive+frames", 49: "W2: barrier 1", 50: "W2: collisi
       51: "W2: barrier 2", 52: "W2: barrier 3 (idle in phase 3)", 53: "W2: factors of M and M+hD",
       54: "W2: barrier 4", 55: "W2: barrier 5 (idle in phase 5)", 56: "W2: barrier 6 (end of step)",
       57: "W2: velocity stage (phase 3)"}
+MFMA = len(sys.argv) > 2 and sys.argv[2] == "mfma"  # the backward section on the MFMA engine
 L = ia.lib()
 acc = (ctypes.c_ulonglong * 64)(); cnt = (ctypes.c_ulonglong * 64)()
 m = ia.Model.load(workloads.model_file(sys.argv[1] if len(sys.argv) > 1 else "hopper"))
@@ -82,12 +83,16 @@ for what, fn, rd, rls in (("rollout (1 seed)", g.forward_pass, L.ilqg_debug_stam
 
 BN = ["stage1 sym/A/B/q/c/r", "stage2 T1=B'V", "stage3 Mm,T3,w,ldlt,col", "stage4 K,k solves",
       "stage5 ABK,T6,y,kR", "stage6 T4", "stage7 Vn", "stage8 z,vn,K/k out", "V copy + prefetch store"]
+if MFMA:
+    g.set_riccati("mfma")
+    BN = ["1 sym/A/B/q/c/r", "2 T1=B'Vs (mfma)", "3 Mm,T3 (mfma), w", "4 LDLT(Quu), col", "5 perm, K,k solves",
+          "6 ABK,T6 (mfma), y, kR", "7 T4 (mfma)", "8 Vn (mfma)", "9 z, vn, K/k out", "10 v copy, record"]
 acc = (ctypes.c_ulonglong * 16)(); cnt = (ctypes.c_ulonglong * 16)()
 L.ilqg_debug_bstamps(acc, cnt, 1)
 g.backward_pass(); g.synchronize()
 L.ilqg_debug_bstamps(acc, cnt, 1)
-tot = sum(acc[i] for i in range(9))
+tot = sum(acc[i] for i in range(len(BN)))
 print(f"== backward: block 0, lane 0, total {tot} cycles, {tot / max(cnt[0], 1):.0f} per step")
-for i in range(9):
+for i in range(len(BN)):
     if cnt[i]:
         print(f"  {BN[i]:26s} calls {cnt[i]:6d}  cycles/call {acc[i]/cnt[i]:9.0f}  share {acc[i]/max(tot,1):6.1%}")
