@@ -373,6 +373,8 @@ def main():
     ap.add_argument("--seeds-per-gpu", type=int, default=8)
     ap.add_argument("--alphas", type=int, default=8)
     ap.add_argument("--horizon", type=int, default=500)
+    ap.add_argument("--groups", type=int, default=1,
+                    help="seed groups per GPU (ilqg_solver_set_groups): the seeds software-pipelined as G ranges")
     ap.add_argument("--cpu-budget", type=float, default=15.0)
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -434,6 +436,8 @@ def main():
         solver.set_stream(stream.cuda_stream)
         if args.layout != "reference":
             solver.set_layout(args.layout)
+        if args.groups > 1:
+            solver.set_groups(args.groups)
         exchange = CostExchange(device_view(solver.device_costs_ptr(), S), world, solver=solver)
 
     def one_step():
@@ -483,7 +487,8 @@ def main():
             dist.destroy_process_group()
         return
     # roofline of the dominant kernel (largest device time in the timed region)
-    abytes = algorithmic_bytes(m, S, A, P)
+    # per launch: with seed groups every hot-path launch covers S / G seeds
+    abytes = {k: v / args.groups for k, v in algorithmic_bytes(m, S, A, P).items()}
     per_kernel = {k: {"ms_total": v[0], "launches": v[1], "avg_ms": (v[0] / v[1] if v[1] else 0.0)}
                   for k, v in ktime.items()}
     # fd_backward: the fused FD sweep with the Riccati recursion streamed behind it
@@ -496,7 +501,7 @@ def main():
     traffic = pmc_traffic(dom)
 
     # the binding roof: FP64 VALU (algorithmic flops / launch time vs the vector peak)
-    aflops = algorithmic_flops(S, A, P)
+    aflops = {k: v / args.groups for k, v in algorithmic_flops(S, A, P).items()}
     valu = {k: {"flops_per_launch": f, "avg_launch_ms": gtime[k] / max(1, per_kernel[k]["launches"]),
                 "achieved_tflops": f / (gtime[k] / max(1, per_kernel[k]["launches"]) * 1e-3) / 1e12
                 if per_kernel[k]["launches"] else 0.0} for k, f in aflops.items()}
@@ -519,7 +524,7 @@ def main():
         "config": {"workload": f"hopper_H{H}_{S}seeds_x_{A}alphas_per_gpu", "model": "hopper.xml",
                    "horizon": H, "seeds_per_gpu": S, "linesearch_candidates": A, "global_seeds": world * S,
                    "parallelism": f"seed-sharded x{world} (RCCL all-gather of per-seed costs)",
-                   "layout": args.layout},
+                   "layout": args.layout, "seed_groups": args.groups},
         "roofline": {"bound": "hbm", "kernel": dom, "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic["bytes"],
                      "traffic_file": traffic["file"], "traffic_src_sha": traffic["src_sha"],

@@ -276,6 +276,28 @@ struct ilqg_solver {
   hipStream_t fd_stream[kFdStreams] = {};
   std::vector<hipEvent_t> pipe_ev;
   DevBuf carry[5];  // the chunked rollout's state between launches, [S][...]
+  // seed groups (ilqg_solver_set_groups): the seeds as G contiguous ranges,
+  // software-pipelined.  Group g has a rollout stream (CU-masked to an XCD of
+  // its own: one rollout workgroup per CU) and a sweep stream (every CU but the
+  // other groups' rollout XCDs); its rollout of iteration n waits for its own
+  // sweep of n - 1 and for group g - 1's rollout of n.  In steady state a
+  // group's fused sweep runs beside the next group's rollout, which uses a
+  // quarter of the chip.  Launches, operands and results are the per-group
+  // ones of the ungrouped iterate: the same bits.
+  static constexpr int kMaxGroups = 4;
+  int ngroups = 1;
+  bool grp_join = true;  // the next grouped iterate waits for the solver's stream first
+  hipStream_t grp_roll[kMaxGroups] = {}, grp_fd[kMaxGroups] = {};
+  hipEvent_t grp_sel[kMaxGroups] = {}, grp_done[kMaxGroups] = {}, grp_zero[kMaxGroups] = {},
+            grp_fdend[kMaxGroups] = {};
+  // ILQG_GROUP_BW (default 1, read by set_groups): each group's recursion as a
+  // launch of its own beside its sweep (riccati_mw.h, one lane per matrix
+  // entry) where the model has that kernel; 0: streamed inside the fused sweep
+  bool grp_mw = false;
+  DevBuf grp_sync;  // one hand-off block per group
+  size_t grp_sync_stride = 0;
+  int grp_xcd = 1;  // ILQG_GROUP_XCD: 1 a whole XCD per group rollout, 0 spread over every XCD (A/B)
+  int grp_rcus = 0;  // CUs per group rollout mask (0: unmasked streams)
   // (A split variant -- the Riccati recursion as a launch of its own on a second
   // stream, streaming a concurrent sweep launch's records -- deadlocked when the
   // two streams shared a hardware queue: HIP does not guarantee that two
@@ -329,7 +351,25 @@ struct ilqg_solver {
     hipError_t e = hipStreamSynchronize(stream);
     for (auto fs : fd_stream)
       if (e == hipSuccess && fs) e = hipStreamSynchronize(fs);
+    for (int g = 0; g < kMaxGroups; g++) {
+      if (e == hipSuccess && grp_roll[g]) e = hipStreamSynchronize(grp_roll[g]);
+      if (e == hipSuccess && grp_fd[g]) e = hipStreamSynchronize(grp_fd[g]);
+    }
     return e;
+  }
+  void free_groups() {
+    for (int g = 0; g < kMaxGroups; g++) {
+      if (grp_roll[g]) (void)hipStreamDestroy(grp_roll[g]);
+      if (grp_fd[g]) (void)hipStreamDestroy(grp_fd[g]);
+      if (grp_sel[g]) (void)hipEventDestroy(grp_sel[g]);
+      if (grp_done[g]) (void)hipEventDestroy(grp_done[g]);
+      if (grp_zero[g]) (void)hipEventDestroy(grp_zero[g]);
+      if (grp_fdend[g]) (void)hipEventDestroy(grp_fdend[g]);
+      grp_roll[g] = grp_fd[g] = nullptr;
+      grp_sel[g] = grp_done[g] = grp_zero[g] = grp_fdend[g] = nullptr;
+    }
+    grp_sync.release();
+    ngroups = 1;
   }
   ~ilqg_solver() {
     (void)sync_all();
@@ -342,6 +382,7 @@ struct ilqg_solver {
     for (auto e : pipe_ev) (void)hipEventDestroy(e);
     for (auto fs : fd_stream)
       if (fs) (void)hipStreamDestroy(fs);
+    free_groups();
     if (own_stream) (void)hipStreamDestroy(own_stream);
   }
 };
@@ -687,7 +728,7 @@ int ilqg_solver_create(const ilqg_model* mc, const ilqg_solver_opts* o, const il
       ALLOC(s->snap, S * P * (size_t)s->snapd * 8);
     }
   }
-  ALLOC(s->fault, 16);
+  ALLOC(s->fault, 2 * ilqg_solver::kMaxGroups * sizeof(unsigned));  // one fault block (handoff.h) per seed group
   s->pipe_chunk = getenv_int("ILQG_PIPE_CHUNK", 16);
   s->pipe_flat = getenv_int("ILQG_PIPE_FLAT", 0) != 0;
   if (s->A == 1 && s->pipe_chunk > 0 && s->pipe_chunk < (int)P) {
@@ -874,8 +915,9 @@ struct SeedRange {
   int s0, ns;
   hipStream_t st;
   unsigned* sync;  // the range's own hand-off block (fused sweep)
+  int grp = 0;     // its fault block: s->fault + 2 grp (seed groups)
 };
-static SeedRange whole(ilqg_solver* s) { return {0, s->S, s->stream, s->sync.as<unsigned>()}; }
+static SeedRange whole(ilqg_solver* s) { return {0, s->S, s->stream, s->sync.as<unsigned>(), 0}; }
 static TrajDev toff(TrajDev t, size_t pts, const HostModel& h) {
   return TrajDev{t.time + pts, t.qpos + pts * h.nq, t.qvel + pts * h.nv, t.warm + pts * h.nv, t.ctrl + pts * h.nu};
 }
@@ -971,22 +1013,29 @@ static int iterate_pipelined(ilqg_solver* s) {
 
 int ilqg_forward(ilqg_solver* s) {
   if (!s || !s->initialized) return fail(ILQG_ERR_ARG, "solver not initialised");
+  s->grp_join = true;
   HIPCHK(forward_range(s, whole(s)));
   return ILQG_OK;
 }
 
 // the fused sweep over a seed range: its hand-off words zeroed on the stream first
 // mode: 0 the sweep alone, 1 the sweep with the backward roles streamed behind it
-static hipError_t fused_launch(ilqg_solver* s, const SeedRange& r, int mode) {
+// the range's hand-off words and its launch fault word (handoff.h; the report
+// word survives until read), zeroed on the range's stream
+static hipError_t fused_zero(ilqg_solver* s, const SeedRange& r) {
+  const size_t ntm = (size_t)s->nut + 2 * (size_t)s->model->host.nv;
+  hipError_t e = hipMemsetAsync(r.sync, 0, sync_bytes((size_t)r.ns * s->P, ntm), r.st);
+  if (e != hipSuccess) return e;
+  return hipMemsetAsync(s->fault.as<unsigned>() + 2 * r.grp + 1, 0, sizeof(unsigned), r.st);
+}
+static hipError_t fused_launch(ilqg_solver* s, const SeedRange& r, int mode, bool zero = true) {
   const ilqg_model* m = s->model;
   const HostModel& h = m->host;
   const size_t s0 = r.s0, P = s->P, nx = s->nx;
   const size_t ntm = (size_t)s->nut + 2 * (size_t)h.nv;
-  hipError_t e = hipMemsetAsync(r.sync, 0, sync_bytes((size_t)r.ns * P, ntm), r.st);
+  hipError_t e = zero ? fused_zero(s, r) : hipSuccess;
   if (e != hipSuccess) return e;
-  // the launch's own fault word (handoff.h); the report word survives until read
-  e = hipMemsetAsync(s->fault.as<unsigned>() + 1, 0, sizeof(unsigned), r.st);
-  if (e != hipSuccess) return e;
+  unsigned* fault = s->fault.as<unsigned>() + 2 * r.grp;
   FdFused a{};
   a.tr = toff(s->tview(s->traj), s0 * P, h);
   a.S = r.ns;
@@ -1002,7 +1051,7 @@ static hipError_t fused_launch(ilqg_solver* s, const SeedRange& r, int mode) {
   a.cw = s->cw.as<double>() + s0 * P * s->WCp;
   a.deriv = s->deriv.as<double>() + s0 * P * s->Dp;
   a.sync = r.sync;
-  a.fault = s->fault.as<unsigned>();
+  a.fault = fault;
   a.mu = s->opts.mu;
   a.K = s->K.as<double>() + s0 * P * h.nu * nx;
   a.k = s->k.as<double>() + s0 * P * h.nu;
@@ -1032,7 +1081,8 @@ static hipError_t fused_launch(ilqg_solver* s, const SeedRange& r, int mode) {
   // Every map the sweep reads is validated first (launch_fd_order_check): an
   // invalid one is replaced by the identity and reported by ilqg_synchronize.
   const int nt = (s->halves ? 2 : 1) * (s->nut + 2 * h.nv);
-  if (s->plan_dur.p && (s->plan_on || !s->plants.empty())) {
+  // (one ticket map per solver: seed groups run the identity order)
+  if (s->plan_dur.p && (s->plan_on || !s->plants.empty()) && s->ngroups == 1) {
     if (s->plan_on) {
       e = launch_fd_plan(r.ns, s->P, nt, s->plan_p0, s->plan_k, s->plan_dur.as<unsigned>(),
                          s->plan_order.as<unsigned>(), r.st);
@@ -1055,8 +1105,8 @@ static hipError_t fused_launch(ilqg_solver* s, const SeedRange& r, int mode) {
       s->plants.clear();
       if (e != hipSuccess) return e;
     }
-    e = launch_fd_order_check(r.ns, s->P, nt, s->plan_order.as<unsigned>(), s->plan_pos.as<unsigned>(),
-                              s->fault.as<unsigned>(), r.st);
+    e = launch_fd_order_check(r.ns, s->P, nt, s->plan_order.as<unsigned>(), s->plan_pos.as<unsigned>(), fault,
+                              r.st);
     if (e != hipSuccess) return e;
     a.order = s->plan_order.as<unsigned>();
   }
@@ -1065,6 +1115,7 @@ static hipError_t fused_launch(ilqg_solver* s, const SeedRange& r, int mode) {
 
 int ilqg_fd_sweep(ilqg_solver* s) {
   if (!s || !s->initialized) return fail(ILQG_ERR_ARG, "solver not initialised");
+  s->grp_join = true;
   const ilqg_model* m = s->model;
   TrajDev nom = s->tview(s->traj);
   const int npts = s->S * s->P;
@@ -1129,6 +1180,7 @@ int ilqg_fd_sweep_range(ilqg_solver* s, int p0, int np) {
   if (!s || !s->initialized) return fail(ILQG_ERR_ARG, "solver not initialised");
   if (p0 < 0 || np < 0 || p0 + np > s->P) return fail(ILQG_ERR_ARG, "point range outside the trajectory");
   if (!np) return ILQG_OK;
+  s->grp_join = true;
   HIPCHK(s->timed(3, [&] { return fd_range_launch(s, p0, np, s->stream); }));
   return ILQG_OK;
 }
@@ -1142,6 +1194,7 @@ int ilqg_solver_device_deriv(ilqg_solver* s, double** dptr, int* stride) {
 
 int ilqg_backward(ilqg_solver* s) {
   if (!s || !s->initialized) return fail(ILQG_ERR_ARG, "solver not initialised");
+  s->grp_join = true;
   const ilqg_model* m = s->model;
   HIPCHK(s->timed(4, [&] {
     if (s->riccati == ILQG_RICCATI_MFMA)
@@ -1156,8 +1209,65 @@ int ilqg_backward(ilqg_solver* s) {
   return ILQG_OK;
 }
 
+// iterate() over seed groups (ilqg_solver_set_groups): per group, its rollout +
+// selection on its rollout stream, then its fused sweep on its sweep stream;
+// the group's next rollout waits for that sweep (the gains), and group g's
+// rollout for group g - 1's (which re-creates the stagger after any drain).
+// The solver's stream waits for every group, so work enqueued on it after
+// iterate() sees this iteration's results; the groups wait for the solver's
+// stream only on the first grouped iterate after work was enqueued on it
+// through the solver (grp_join) -- see INTEGRATION.md.
+static int iterate_groups(ilqg_solver* s) {
+  const int G = s->ngroups;
+  if (s->grp_join) {
+    for (int g = 0; g < G; g++) HIPCHK(hipEventRecord(s->grp_done[g], s->stream));
+    s->grp_join = false;
+  }
+  for (int g = 0; g < G; g++) {
+    const int s0 = s->S * g / G, s1 = s->S * (g + 1) / G;
+    SeedRange r{s0, s1 - s0, s->grp_roll[g],
+                reinterpret_cast<unsigned*>(static_cast<char*>(s->grp_sync.p) + g * s->grp_sync_stride), g};
+    HIPCHK(hipStreamWaitEvent(r.st, s->grp_done[g], 0));
+    if (g > 0) HIPCHK(hipStreamWaitEvent(r.st, s->grp_sel[g - 1], 0));
+    HIPCHK(forward_range(s, r));
+    HIPCHK(hipEventRecord(s->grp_sel[g], r.st));
+    const hipStream_t rs = r.st;
+    r.st = s->grp_fd[g];
+    HIPCHK(hipStreamWaitEvent(r.st, s->grp_sel[g], 0));
+    if (s->grp_mw) {
+      // the sweep alone on the sweep stream and, on the rollout stream (the
+      // group's XCD idles until its next rollout), the one-lane-per-entry
+      // recursion streaming the sweep's records as they are announced
+      HIPCHK(fused_zero(s, r));
+      HIPCHK(hipEventRecord(s->grp_zero[g], r.st));
+      HIPCHK(s->timed(3, [&] { return fused_launch(s, r, 0, false); }, r.st));
+      HIPCHK(hipEventRecord(s->grp_fdend[g], r.st));
+      HIPCHK(hipStreamWaitEvent(rs, s->grp_zero[g], 0));
+      const ilqg_model* m = s->model;
+      const HostModel& h = m->host;
+      const size_t s0 = r.s0, P = s->P, nx = s->nx;
+      HIPCHK(s->timed(4, [&] {
+        return launch_backward_mw(m->dm, r.ns, s->P, s->opts.mu, s->deriv.as<double>() + s0 * P * s->Dp, s->Dp,
+                                  toff(s->tview(s->traj), s0 * P, h), s->K.as<double>() + s0 * P * h.nu * nx,
+                                  s->k.as<double>() + s0 * P * h.nu, s->V.as<double>() + s0 * nx * nx,
+                                  s->v.as<double>() + s0 * nx, s->flags(), r.sync + 4 + (size_t)r.ns * P,
+                                  (unsigned)(1 + s->nut + 2 * h.nv), s->fault.as<unsigned>() + 2 * g, rs);
+      }, rs));
+      HIPCHK(hipStreamWaitEvent(rs, s->grp_fdend[g], 0));
+      HIPCHK(hipEventRecord(s->grp_done[g], rs));
+    } else {
+      HIPCHK(s->timed(5, [&] { return fused_launch(s, r, 1); }, r.st));
+      HIPCHK(hipEventRecord(s->grp_done[g], r.st));
+    }
+  }
+  for (int g = 0; g < G; g++) HIPCHK(hipStreamWaitEvent(s->stream, s->grp_done[g], 0));
+  s->vinit_pending = false;
+  return ILQG_OK;
+}
+
 int ilqg_iterate(ilqg_solver* s) {
   if (!s || !s->initialized) return fail(ILQG_ERR_ARG, "solver not initialised");
+  if (s->ngroups > 1 && s->fused) return iterate_groups(s);
   if (!s->fused && s->pipe_chunk > 0) return iterate_pipelined(s);
   int rc = ilqg_forward(s);
   if (rc) return rc;
@@ -1175,11 +1285,14 @@ int ilqg_iterate(ilqg_solver* s) {
 int ilqg_synchronize(ilqg_solver* s) {
   if (!s) return fail(ILQG_ERR_ARG, "null solver");
   HIPCHK(s->sync_all());
+  // every seed group's report word (fault block g at 2 g)
+  unsigned blk[2 * ilqg_solver::kMaxGroups] = {};
+  HIPCHK(hipMemcpy(blk, s->fault.p, sizeof(blk), hipMemcpyDeviceToHost));
   unsigned flt = 0;
-  HIPCHK(hipMemcpy(&flt, s->fault.p, 4, hipMemcpyDeviceToHost));
+  for (int g = 0; g < ilqg_solver::kMaxGroups; g++) flt |= blk[2 * g];
   if (flt) {
     // reported once: cleared by the read (the next launch waits normally)
-    HIPCHK(hipMemset(s->fault.p, 0, 4));
+    for (int g = 0; g < ilqg_solver::kMaxGroups; g++) HIPCHK(hipMemset(s->fault.as<unsigned>() + 2 * g, 0, 4));
     if (flt == 2u)
       return fail(ILQG_ERR_HIP, "fused FD sweep: invalid ticket schedule (item out of range, repeated, or a column "
                                 "before its centre); the sweep ran in the identity order");
@@ -1255,6 +1368,7 @@ int ilqg_solver_set_stream(ilqg_solver* s, void* stream) {
   if (!s) return fail(ILQG_ERR_ARG, "null solver");
   HIPCHK(s->sync_all());
   s->stream = stream ? (hipStream_t)stream : s->own_stream;
+  s->grp_join = true;
   return ILQG_OK;
 }
 
@@ -1322,6 +1436,80 @@ int ilqg_solver_set_value(ilqg_solver* s, const double* V, const double* v) {
   HIPCHK(hipMemcpy(s->V.p, V, s->V.n, hipMemcpyHostToDevice));
   HIPCHK(hipMemcpy(s->v.p, v, s->v.n, hipMemcpyHostToDevice));
   s->vinit_pending = true;
+  return ILQG_OK;
+}
+
+int ilqg_solver_set_groups(ilqg_solver* s, int ngroups) {
+  if (!s || ngroups < 1 || ngroups > ilqg_solver::kMaxGroups || ngroups > s->S)
+    return fail(ILQG_ERR_ARG, "ngroups must be in 1 .. min(4, nseed)");
+  HIPCHK(s->sync_all());
+  s->free_groups();
+  s->grp_join = true;
+  if (ngroups == 1) return ILQG_OK;
+  if (!s->fused)
+    return fail(ILQG_ERR_UNSUPPORTED, "seed groups pipeline the fused sweep (fp64 FD with the exact recursion)");
+  const HostModel& h = s->model->host;
+  const int G = ngroups;
+  hipError_t e;
+  auto bail = [&](hipError_t err, const char* w) {
+    s->free_groups();
+    return hip_fail(err, w);
+  };
+  // the CU masks: KFD deals mask bit c to XCD c % nxcd (MI355X: 8 XCDs of 32
+  // CUs); a rollout workgroup holds a CU (k_rollout2: 480 registers a lane, one
+  // wave per SIMD), so group g's rollout gets the XCDs [g k, g k + k) that hold
+  // its ns * A workgroups, and every group's sweep all CUs but the other
+  // groups' rollout XCDs.  Unmasked streams when the rollouts would take the
+  // whole chip.
+  int ncu = 0;
+  e = hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, s->opts.device);
+  if (e != hipSuccess) return bail(e, "hipDeviceGetAttribute");
+  const int nxcd = (ncu >= 64 && ncu % 8 == 0) ? 8 : 1, per = ncu / nxcd;
+  const int need = ((s->S + G - 1) / G) * s->A;
+  const int k = (need + per - 1) / per;
+  s->grp_xcd = getenv_int("ILQG_GROUP_XCD", 1);
+  s->grp_mw = getenv_int("ILQG_GROUP_BW", 1) != 0 && backward_mw_supported(h.nq, h.nv, h.nu);
+  const bool masked = getenv_int("ILQG_GROUP_MASK", 1) != 0 && G * k < nxcd;
+  s->grp_rcus = masked ? k * per : 0;
+  auto rolls = [&](int g, int c) {  // CU c in group g's rollout set
+    if (s->grp_xcd) return (c % nxcd) / k == g;
+    return c / (k * per) == g;  // the lowest bits: spread over every XCD
+  };
+  for (int g = 0; g < G; g++) {
+    if (masked) {
+      std::vector<uint32_t> rm((ncu + 31) / 32, 0), fm((ncu + 31) / 32, 0);
+      for (int c = 0; c < ncu; c++) {
+        bool other = false;
+        for (int o = 0; o < G; o++)
+          if (o != g && rolls(o, c)) other = true;
+        if (rolls(g, c)) rm[c / 32] |= 1u << (c % 32);
+        if (!other) fm[c / 32] |= 1u << (c % 32);
+      }
+      e = hipExtStreamCreateWithCUMask(&s->grp_roll[g], (uint32_t)rm.size(), rm.data());
+      if (e == hipSuccess) e = hipExtStreamCreateWithCUMask(&s->grp_fd[g], (uint32_t)fm.size(), fm.data());
+    } else {
+      e = hipStreamCreateWithFlags(&s->grp_roll[g], hipStreamNonBlocking);
+      if (e == hipSuccess) e = hipStreamCreateWithFlags(&s->grp_fd[g], hipStreamNonBlocking);
+    }
+    if (e != hipSuccess) return bail(e, "hipStreamCreate");
+    e = hipEventCreateWithFlags(&s->grp_sel[g], hipEventDisableTiming);
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&s->grp_done[g], hipEventDisableTiming);
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&s->grp_zero[g], hipEventDisableTiming);
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&s->grp_fdend[g], hipEventDisableTiming);
+    if (e != hipSuccess) return bail(e, "hipEventCreate");
+  }
+  const size_t ntm = (size_t)s->nut + 2 * (size_t)h.nv;
+  s->grp_sync_stride = (sync_bytes((size_t)((s->S + G - 1) / G) * s->P, ntm) + 255) / 256 * 256;
+  e = s->grp_sync.alloc(G * s->grp_sync_stride);
+  if (e != hipSuccess) return bail(e, "hipMalloc");
+  s->ngroups = G;
+  return ILQG_OK;
+}
+
+int ilqg_solver_get_groups(ilqg_solver* s, int* ngroups, int* rollout_cus) {
+  if (!s || !ngroups) return fail(ILQG_ERR_ARG, "bad argument");
+  *ngroups = s->ngroups;
+  if (rollout_cus) *rollout_cus = s->ngroups > 1 ? s->grp_rcus : 0;
   return ILQG_OK;
 }
 

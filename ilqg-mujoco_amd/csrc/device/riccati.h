@@ -209,6 +209,155 @@ __device__ inline void ldlt_solve_reg(int n, const double* Lm, const int* perm, 
   });
 }
 
+// ldlt_factor_wave and ldlt_solve_reg for a compile-time size N (the MFMA
+// engine's humanoid instance, nu = 21): every loop unrolled, no size guards.
+// The pivot scan is a wave max-reduction instead of the serial shuffle chain:
+// |diagonal| >= 0, so its IEEE bits order like the values; rows whose
+// |diagonal| is NaN take key 0 (the strict > of the scan never picks them), a
+// NaN at row k keeps k (the scan never moves), and the first row attaining the
+// maximum is the scan's choice (a tie at key 0 includes row k itself).
+// max(x, x rotated right by S lanes within its 16-lane row) (DPP row_ror)
+template <int S>
+__device__ __forceinline__ unsigned long long umax_ror(unsigned long long x) {
+  const int lo = __builtin_amdgcn_update_dpp(0, (int)(unsigned)x, 0x120 + S, 0xf, 0xf, false);
+  const int hi = __builtin_amdgcn_update_dpp(0, (int)(unsigned)(x >> 32), 0x120 + S, 0xf, 0xf, false);
+  const unsigned long long y = ((unsigned long long)(unsigned)hi << 32) | (unsigned)lo;
+  return y > x ? y : x;
+}
+__device__ __forceinline__ unsigned long long readlane_u64(unsigned long long x, int l) {
+  const unsigned lo = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)x, l);
+  const unsigned hi = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)(x >> 32), l);
+  return ((unsigned long long)hi << 32) | lo;
+}
+template <int N>
+__device__ inline void ldlt_factor_wave_t(double* mat, int* transp, double* temp, int lane) {
+  static_assert(N >= 1 && N <= 32, "one wavefront, n <= 32");
+  bool stop = false;
+  rreg::sf<0, N>([&](auto kk) __attribute__((always_inline)) {
+    constexpr int k = decltype(kk)::value;
+    if (stop) return;
+    const bool in = lane >= k && lane < N;
+    const int li = lane < N ? lane : N - 1;
+    const double dg = fabs(mat[li + li * N]);
+    unsigned long long key = (in && dg == dg) ? (unsigned long long)__double_as_longlong(dg) : 0ull;
+    // max over each 16-lane row by DPP row rotations, then rows 0 and 1 (n <= 32)
+    key = umax_ror<8>(key);
+    key = umax_ror<4>(key);
+    key = umax_ror<2>(key);
+    key = umax_ror<1>(key);
+    const unsigned long long m0 = readlane_u64(key, 0), m1 = readlane_u64(key, 16);
+    const unsigned long long kmax = m1 > m0 ? m1 : m0;
+    const double dk = fabs(mat[k + k * N]);
+    int big = k;
+    if (dk == dk) {
+      const unsigned long long hit = __ballot(in && dg == dg && (unsigned long long)__double_as_longlong(dg) == kmax);
+      // kmax == 0: every candidate is 0 or NaN, row k (0) the first of them
+      if (kmax != 0ull) big = (int)__builtin_ctzll(hit);
+    }
+    if (lane == 0) transp[k] = big;
+    if (k != big) {
+      const int s = N - big - 1;
+      double t;
+      if (lane < k) {  // row k <-> row big, columns j < k
+        const int j = lane;
+        t = mat[k + j * N]; mat[k + j * N] = mat[big + j * N]; mat[big + j * N] = t;
+      }
+      if (lane < s) {  // rows below big: column k <-> column big
+        const int i = lane;
+        t = mat[(big + 1 + i) + k * N];
+        mat[(big + 1 + i) + k * N] = mat[(big + 1 + i) + big * N];
+        mat[(big + 1 + i) + big * N] = t;
+      }
+      if (lane == 32) {
+        t = mat[k + k * N]; mat[k + k * N] = mat[big + big * N]; mat[big + big * N] = t;
+      }
+      if (lane > 32 + k && lane < 32 + big) {  // between: column k <-> row big
+        const int i = lane - 32;
+        t = mat[i + k * N]; mat[i + k * N] = mat[big + i * N]; mat[big + i * N] = t;
+      }
+    }
+    wave_sync();
+    if constexpr (k > 0) {
+      if (lane < k) temp[lane] = mat[lane + lane * N] * mat[k + lane * N];
+      wave_sync();
+      // lane i >= k: row i's dot with temp (row k: the diagonal update), ascending j
+      double a[k], b[k];
+      rreg::sf<0, k>([&](auto jj) __attribute__((always_inline)) {
+        constexpr int j = decltype(jj)::value;
+        a[j] = mat[li + j * N];
+        b[j] = temp[j];
+      });
+      double si = 0;
+      rreg::sf<0, k>([&](auto jj) __attribute__((always_inline)) {
+        constexpr int j = decltype(jj)::value;
+        si += a[j] * b[j];
+      });
+      if (in) mat[lane + k * N] -= si;
+      wave_sync();
+    }
+    if constexpr (k == 0) {
+      if (!(fabs(mat[0]) > 0)) {
+        for (int j = lane; j < N; j += 64) transp[j] = j;
+        wave_sync();
+        stop = true;
+        return;
+      }
+    }
+    if constexpr (N - k - 1 > 0) {
+      const double d = mat[k + k * N];
+      if (fabs(d) > 0 && lane > k && lane < N) mat[lane + k * N] /= d;
+    }
+    wave_sync();
+  });
+}
+// a zero the compiler cannot see through, produced after v: L reads addressed
+// with it cannot be hoisted above v's computation (left free, the scheduler
+// issues all N^2 reads of an unrolled solve at once and the kernel spills)
+__device__ __forceinline__ int zero_after(double v) {
+  int z;
+  asm volatile("v_mov_b32 %0, 0" : "=v"(z) : "v"(v));
+  return z;
+}
+template <int N>
+__device__ inline void ldlt_solve_reg_t(const double* Lm, const int* perm, double* x, bool active) {
+  const double tol = 2.2250738585072014e-308;
+  double r[N];
+  rreg::sf<0, N>([&](auto ii) __attribute__((always_inline)) {
+    constexpr int i = decltype(ii)::value;
+    r[i] = active ? x[perm[i]] : 0.0;
+  });
+  // forward substitution column by column: r[i] -= L(i, j) r[j] for i > j --
+  // each r[i] still receives its subtractions in ascending j, ldlt_solve's
+  // order.  Column j's L reads wait for r[j - 1] (final one column earlier):
+  // they overlap the previous column's updates, no further ahead.
+  rreg::sf<0, N>([&](auto jj) __attribute__((always_inline)) {
+    constexpr int j = decltype(jj)::value;
+    const double* Lc = Lm + (j > 0 ? zero_after(r[j > 0 ? j - 1 : 0]) : 0);
+    rreg::sf<j + 1, N>([&](auto ii) __attribute__((always_inline)) {
+      constexpr int i = decltype(ii)::value;
+      r[i] -= Lc[i + j * N] * r[j];
+    });
+  });
+  rreg::sf<0, N>([&](auto ii) __attribute__((always_inline)) {
+    constexpr int i = decltype(ii)::value;
+    const double d = Lm[i + i * N];
+    r[i] = fabs(d) > tol ? r[i] / d : 0.0;
+  });
+  // backward rows, i descending: row i's reads wait for r[i + 2]
+  rreg::sf<0, N>([&](auto ii) __attribute__((always_inline)) {
+    constexpr int i = N - 1 - decltype(ii)::value;
+    const double* Lc = Lm + (i + 2 < N ? zero_after(r[i + 2 < N ? i + 2 : 0]) : 0);
+    rreg::sf<i + 1, N>([&](auto jj) __attribute__((always_inline)) {
+      constexpr int j = decltype(jj)::value;
+      r[i] -= Lc[j + i * N] * r[j];
+    });
+  });
+  rreg::sf<0, N>([&](auto ii) __attribute__((always_inline)) {
+    constexpr int i = decltype(ii)::value;
+    if (active) x[perm[i]] = r[i];
+  });
+}
+
 // Three independent fixed-order dot products per lane (ILP 3): each output
 // keeps the oracle's summation order, the three chains overlap in the pipe.
 #define ILP3_BEGIN(n)                                    \

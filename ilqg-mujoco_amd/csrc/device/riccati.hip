@@ -41,17 +41,19 @@ __device__ unsigned long long g_bstamp_cnt[16];
 
 #include "riccati.h"
 #include "riccati_mfma.h"
+#include "riccati_mw.h"
 #include "dsmall.h"
 
 namespace ilqg {
 namespace {
 
+template <int NU_>
 __global__ __launch_bounds__(rmfma::THREADS) void k_backward_mfma(DevModel m, int nq, int nv, int nu, int P, double dt,
                                                                   double mu, const double* deriv, int Ds, TrajDev tr,
                                                                   double* Kg, double* kg, double* Vg, double* vg,
                                                                   RicFlags fl) {
   extern __shared__ double sh[];
-  rmfma::backward_seed_mfma(m, nq, nv, nu, P, dt, mu, deriv, Ds, tr, Kg, kg, Vg, vg, blockIdx.x, sh, fl);
+  rmfma::backward_seed_mfma<NU_>(m, nq, nv, nu, P, dt, mu, deriv, Ds, tr, Kg, kg, Vg, vg, blockIdx.x, sh, fl);
 }
 
 template <int NV_, int NU_>
@@ -62,6 +64,26 @@ __global__ __launch_bounds__(BW_THREADS) void k_backward(DevModel m, int nq, int
   extern __shared__ double sh[];
   backward_seed<NV_, NU_>(m, nq, nv_rt, nu_rt, P, dt, mu, deriv, Ds, tr, Kg, kg, Vg, vg, blockIdx.x, threadIdx.x, sh,
                           nullptr, 0u, nullptr, fl);
+}
+
+template <int NV, int NU>
+__global__ __launch_bounds__((RicMw<NV, NU>::THREADS)) void k_backward_mw(DevModel m, int P, double dt, double mu,
+                                                                       const double* deriv, int Ds, TrajDev tr,
+                                                                       double* Kg, double* kg, double* Vg, double* vg,
+                                                                       const unsigned* done, unsigned target,
+                                                                       unsigned* fault, RicFlags fl) {
+  extern __shared__ double sh[];
+  backward_seed_mw<NV, NU>(m, P, dt, mu, deriv, Ds, tr, Kg, kg, Vg, vg, blockIdx.x, threadIdx.x, sh, done, target,
+                           fault, fl);
+}
+
+template <int NV, int NU>
+void launch_mw_t(const DevModel& m, int S, int P, double mu, const double* deriv, int Ds, TrajDev tr, double* K,
+                 double* k, double* V, double* v, RicFlags fl, const unsigned* done, unsigned target, unsigned* fault,
+                 hipStream_t st) {
+  using R = RicMw<NV, NU>;
+  hipLaunchKernelGGL((k_backward_mw<NV, NU>), dim3(S), dim3(R::THREADS), R::bytes, st, m, P, m.opt_timestep, mu,
+                     deriv, Ds, tr, K, k, V, v, done, target, fault, fl);
 }
 
 template <int NV, int NU>
@@ -96,16 +118,47 @@ hipError_t launch_backward_mfma(const DevModel& m, int S, int P, double mu, cons
                                 double* K, double* k, double* V, double* v, RicFlags fl, hipStream_t st) {
   if (!backward_mfma_supported(m.nv, m.nu)) return hipErrorInvalidValue;
   const size_t lds = rmfma::lds_doubles(m.nv, m.nu) * sizeof(double);  // dynamic part
-  hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(k_backward_mfma),
-                                     hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  // nu = 21 (the bundled humanoid): the compile-time instance (ILQG_MFMA_T=0: the generic one, A/B)
+  static const int ct = [] {
+    const char* e = getenv("ILQG_MFMA_T");
+    return (e && e[0] == '0') ? 0 : 1;
+  }();
+  const void* kf = (ct && m.nu == 21) ? reinterpret_cast<const void*>(k_backward_mfma<21>)
+                                      : reinterpret_cast<const void*>(k_backward_mfma<0>);
+  hipError_t e = hipFuncSetAttribute(kf, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   if (e != hipSuccess) return e;
-  hipLaunchKernelGGL(k_backward_mfma, dim3(S), dim3(rmfma::THREADS), lds, st, m, m.nq, m.nv, m.nu, P,
-                     m.opt_timestep, mu, deriv, Ds, tr, K, k, V, v, fl);
+  if (ct && m.nu == 21)
+    hipLaunchKernelGGL(k_backward_mfma<21>, dim3(S), dim3(rmfma::THREADS), lds, st, m, m.nq, m.nv, m.nu, P,
+                       m.opt_timestep, mu, deriv, Ds, tr, K, k, V, v, fl);
+  else
+    hipLaunchKernelGGL(k_backward_mfma<0>, dim3(S), dim3(rmfma::THREADS), lds, st, m, m.nq, m.nv, m.nu, P,
+                       m.opt_timestep, mu, deriv, Ds, tr, K, k, V, v, fl);
+  return hipGetLastError();
+}
+
+bool backward_mw_supported(int nq, int nv, int nu) {
+  return nq == nv && ((nv == 6 && nu == 3) || (nv == 2 && nu == 1));
+}
+
+hipError_t launch_backward_mw(const DevModel& m, int S, int P, double mu, const double* deriv, int Ds, TrajDev tr,
+                              double* K, double* k, double* V, double* v, RicFlags fl, const unsigned* done,
+                              unsigned target, unsigned* fault, hipStream_t st) {
+  if (!backward_mw_supported(m.nq, m.nv, m.nu)) return hipErrorInvalidValue;
+  if (m.nv == 6) launch_mw_t<6, 3>(m, S, P, mu, deriv, Ds, tr, K, k, V, v, fl, done, target, fault, st);
+  else launch_mw_t<2, 1>(m, S, P, mu, deriv, Ds, tr, K, k, V, v, fl, done, target, fault, st);
   return hipGetLastError();
 }
 
 hipError_t launch_backward(const DevModel& m, int S, int P, double mu, const double* deriv, int Ds, TrajDev tr,
                            double* K, double* k, double* V, double* v, RicFlags fl, hipStream_t st) {
+  // the register-formulation sizes: one lane per matrix entry (riccati_mw.h);
+  // ILQG_BW_MW=0 keeps the one-wave kernel (A/B)
+  static const int mw = [] {
+    const char* e = getenv("ILQG_BW_MW");
+    return (e && e[0] == '0') ? 0 : 1;
+  }();
+  if (mw && backward_mw_supported(m.nq, m.nv, m.nu))
+    return launch_backward_mw(m, S, P, mu, deriv, Ds, tr, K, k, V, v, fl, nullptr, 0u, nullptr, st);
   if (m.nu > 32) return hipErrorInvalidValue;  // LDLT scratch bound
   const size_t lds = backward_lds_bytes(m.nv, m.nu);
   if (lds > 160 * 1024) return hipErrorInvalidValue;

@@ -39,7 +39,20 @@ template <class GA, class GB>
 __device__ __forceinline__ d4 tile(int i0, int j0, int K, const GA& ga, const GB& gb, int lane) {
   const int r = lane & 15, kq = lane >> 4;
   d4 acc = {0.0, 0.0, 0.0, 0.0};
-  for (int k0 = 0; k0 < K; k0 += 4) {
+  int k0 = 0;
+  // four K steps a block: the block's eight operand reads issue together, then
+  // its four MFMAs (the same accumulation sequence as one step at a time)
+  for (; k0 + 16 <= K; k0 += 16) {
+    double a[4], b[4];
+#pragma unroll
+    for (int u = 0; u < 4; u++) {
+      a[u] = ga(i0 + r, k0 + 4 * u + kq);
+      b[u] = gb(k0 + 4 * u + kq, j0 + r);
+    }
+#pragma unroll
+    for (int u = 0; u < 4; u++) acc = __builtin_amdgcn_mfma_f64_16x16x4f64(a[u], b[u], acc, 0, 0, 0);
+  }
+  for (; k0 < K; k0 += 4) {
     const double a = ga(i0 + r, k0 + kq);
     const double b = gb(k0 + kq, j0 + r);
     acc = __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, acc, 0, 0, 0);
@@ -74,10 +87,14 @@ __host__ __device__ inline size_t lds_doubles(int nv, int nu) {
 
 // Eigen-style LDLT with symmetric pivoting (oracle ora_ldlt_factor) and its
 // solve: riccati.h ldlt_factor_wave (one wavefront) / ldlt_solve (per column)
-template <class MD>
-__device__ inline void backward_seed_mfma(const MD& m, int nq, int nv, int nu, int P, double dt, double mu,
+// NU_ > 0: nu fixed at compile time (the humanoid's 21): the LDLT and its
+// solves fully unrolled (riccati.h ldlt_factor_wave_t / ldlt_solve_reg_t, the
+// same operations); 0: any nu <= NU_MAX
+template <int NU_, class MD>
+__device__ inline void backward_seed_mfma(const MD& m, int nq, int nv, int nu_rt, int P, double dt, double mu,
                                           const double* deriv, int Ds, TrajDev tr, double* Kg, double* kg,
                                           double* Vg, double* vg, int s, double* sh, RicFlags fl) {
+  const int nu = NU_ > 0 ? NU_ : nu_rt;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int nx = 2 * nv, D = nv * (2 * nv + nu) + 2 * nv + nu;
   const int LX = nx | 1, LU = nu | 1;
@@ -126,16 +143,19 @@ __device__ inline void backward_seed_mfma(const MD& m, int nq, int nv, int nu, i
   }
   for (int n = 1; n < P; n++) {
     const size_t pc = (size_t)s * P + n, pp = pc - 1;
-    // next step's FD record, consumed at the end of this step
+    // next step's FD record, consumed at the end of this step: loaded after
+    // the LDLT solves (stage 5), which need the registers
     double pf[MPF];
-    if (n + 1 < P) {
-      const double* dn1 = deriv + (pc + 1) * Ds;
+    auto prefetch = [&]() __attribute__((always_inline)) {
+      if (n + 1 < P) {
+        const double* dn1 = deriv + (pc + 1) * Ds;
 #pragma unroll
-      for (int t = 0; t < MPF; t++) {
-        const int i = tid + t * THREADS;
-        pf[t] = i < D ? dn1[rec_src(i, nv, nu, fl.layout)] : 0.0;
+        for (int t = 0; t < MPF; t++) {
+          const int i = tid + t * THREADS;
+          pf[t] = i < D ? dn1[rec_src(i, nv, nu, fl.layout)] : 0.0;
+        }
       }
-    }
+    };
     const double* dn = dl;
     // stage 1: symmetrise V, assemble A/B (differentiator.h:66-71,89-92), q, r, c
     for (int e = tid; e < nx * nx; e += THREADS) {
@@ -191,7 +211,10 @@ __device__ inline void backward_seed_mfma(const MD& m, int nq, int nv, int nu, i
     __syncthreads();
     BSTAMP(2);
     // stage 4: LDLT of Mm (wave 0); col = B'w + r beside it (wave 1)
-    if (wave == 0) ldlt_factor_wave(nu, Mm, trn, tmp, lane);
+    if (wave == 0) {
+      if constexpr (NU_ > 0) ldlt_factor_wave_t<NU_>(Mm, trn, tmp, lane);
+      else ldlt_factor_wave(nu, Mm, trn, tmp, lane);
+    }
     for (int a = tid - 64; a >= 0 && a < nu; a += THREADS) {
       double sm = 0;
       for (int kk = 0; kk < nx; kk++) sm += B[kk + a * LX] * w[kk];
@@ -213,10 +236,12 @@ __device__ inline void backward_seed_mfma(const MD& m, int nq, int nv, int nu, i
     }
     {
       const int j = lane * WAVES + wave;  // one column per thread: nx + 1 <= THREADS (launch_backward_mfma)
-      ldlt_solve_reg(nu, Mm, perm, j < nx ? Y1 + j * LU : kl, j < nx + 1);
+      if constexpr (NU_ > 0) ldlt_solve_reg_t<NU_>(Mm, perm, j < nx ? Y1 + j * LU : kl, j < nx + 1);
+      else ldlt_solve_reg(nu, Mm, perm, j < nx ? Y1 + j * LU : kl, j < nx + 1);
     }
     __syncthreads();
     BSTAMP(4);
+    prefetch();
     // stage 6: ABK = A + B K ; T6 = K'R ; y = B k + c ; kR = k'R
     auto gK = [&](int a, int j) { return (a < nu && j < nx) ? Y1[a + j * LU] : 0.0; };
     product(

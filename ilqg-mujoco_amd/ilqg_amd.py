@@ -17,6 +17,7 @@ There is no CPU fallback: a missing library or missing GPU raises.
 from __future__ import annotations
 
 import ctypes
+import sys
 import os
 from dataclasses import dataclass
 from typing import Optional, Sequence
@@ -65,7 +66,7 @@ EXPORTS = [
     "ilqg_solver_debug_set_fault", "ilqg_solver_device_traj", "ilqg_solver_set_layout", "ilqg_solver_set_value", "ilqg_solver_debug_plan",
     "ilqg_solver_set_riccati", "ilqg_selftest_div", "ilqg_solver_set_fd_precision",
     "ilqg_solver_set_mu", "ilqg_solver_get_deriv_point", "ilqg_solver_debug_plant_schedule",
-    "ilqg_fd_sweep_range", "ilqg_solver_device_deriv",
+    "ilqg_fd_sweep_range", "ilqg_solver_device_deriv", "ilqg_solver_set_groups", "ilqg_solver_get_groups",
 ]
 KERNELS = ("rollout", "select", "fd_centre", "fd_cols", "backward", "fd_backward")
 
@@ -95,6 +96,16 @@ def lib() -> ctypes.CDLL:
     if _lib is None:
         if not os.path.exists(LIB_PATH):
             raise IlqgError(f"{LIB_PATH} missing: run `make -C ilqg-mujoco_amd` (hipcc, gfx950)")
+        # torch bundles a HIP runtime of its own: when both share the process,
+        # torch's must initialise first (the other order leaves torch with "No
+        # HIP GPUs are available" on the GPU box), so a torch already imported
+        # is initialised here
+        t = sys.modules.get("torch")
+        if t is not None:
+            try:
+                t.cuda.is_available()
+            except Exception:
+                pass
         L = ctypes.CDLL(LIB_PATH)
         L.ilqg_last_error.restype = ctypes.c_char_p
         L.ilqg_solver_stream.restype = ctypes.c_void_p
@@ -449,6 +460,26 @@ class ILQR:
         """Levenberg-Marquardt constant (ILQR::mu, inc/ilqr.h:65,166) for the
         backward passes enqueued from now on: ilqg_solver_set_mu"""
         _check(lib().ilqg_solver_set_mu(self._h, ctypes.c_double(mu)), "set_mu")
+
+    def set_groups(self, ngroups: int):
+        """seed groups (ilqg_solver_set_groups): iterate() software-pipelines
+        the seeds as ngroups contiguous ranges -- one group's fused sweep beside
+        the next group's rollout, each on CU-masked streams; the same bits as
+        the ungrouped iterate.  1 restores it."""
+        _check(lib().ilqg_solver_set_groups(self._h, int(ngroups)), "set_groups")
+
+    @property
+    def groups(self) -> int:
+        g = ctypes.c_int(0)
+        _check(lib().ilqg_solver_get_groups(self._h, ctypes.byref(g), None), "get_groups")
+        return g.value
+
+    @property
+    def group_rollout_cus(self) -> int:
+        """CUs in each group's rollout mask (0: unmasked streams or no groups)"""
+        g, c = ctypes.c_int(0), ctypes.c_int(0)
+        _check(lib().ilqg_solver_get_groups(self._h, ctypes.byref(g), ctypes.byref(c)), "get_groups")
+        return c.value
 
     def set_riccati(self, mode: str):
         """'exact' (bit-identical to the oracle, default) or 'mfma' (matrix-core

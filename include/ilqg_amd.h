@@ -217,6 +217,24 @@ int ilqg_solver_set_riccati(ilqg_solver* s, int mode);
 #define ILQG_FD_F32 1
 #define ILQG_FD32_EPS 1e-3
 int ilqg_solver_set_fd_precision(ilqg_solver* s, int prec);
+/* Seed groups: ilqg_iterate runs the seeds as ngroups (1..4, <= nseed)
+   contiguous ranges, software-pipelined -- each group's rollout on a stream
+   CU-masked to XCDs of its own, its fused FD sweep + recursion on a stream
+   masked to the rest, and group g's rollout of an iteration behind group
+   g - 1's, so one group's sweep runs beside the next group's (latency-bound)
+   rollout.  Every seed's launches and results are the ungrouped iterate's (bit
+   for bit); only the overlap between independent seeds changes.  Work enqueued
+   on the solver's stream after ilqg_iterate waits for every group; the groups
+   wait for work on that stream only when it came through this API (ilqg_forward,
+   ilqg_fd_sweep, ilqg_backward, set_stream, ...) -- synchronise work of your
+   own before the next ilqg_iterate.  The seeds of MahanFathi/iLQG-MuJoCo's
+   driver are independent (one ILQR per MPC problem, inc/ilqr.h:52-71), so
+   the reference has no counterpart call.  ILQG_ERR_UNSUPPORTED unless the fused
+   sweep is in use (fp64 FD, exact recursion, cooperative model); 1 restores
+   the ungrouped iterate.  get_groups: the count and the CUs of each group's
+   rollout mask (0: unmasked). */
+int ilqg_solver_set_groups(ilqg_solver* s, int ngroups);
+int ilqg_solver_get_groups(ilqg_solver* s, int* ngroups, int* rollout_cus);
 /* device pointer to the per-seed selected-candidate cost (nseed doubles), for
    an in-stream collective (RCCL all-gather) without a host round trip */
 int ilqg_solver_device_costs(ilqg_solver* s, double** dptr);

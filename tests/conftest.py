@@ -5,6 +5,15 @@ import sys
 import numpy as np
 import pytest
 
+# torch bundles a HIP runtime of its own and must initialise before the
+# library's in a process that uses both (ilqg_amd.lib): tests that hand solver
+# memory to torch (seed_shard.device_view) run after tests that loaded the library
+try:
+    import torch
+    torch.cuda.is_available()
+except Exception:  # torch absent: the tests that need it skip or fail on their own
+    pass
+
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 PKG = os.path.join(ROOT, "ilqg-mujoco_amd")
 ORACLE = os.path.join(ROOT, "oracle")

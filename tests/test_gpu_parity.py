@@ -509,7 +509,9 @@ def test_fd_sweep_range_blocks(ia, ora, name, prec):
     single-rank RecordExchange over the solver's resident records) gives the
     gains of the unsharded iteration"""
     import workloads
+    import torch
     from seed_shard import RecordExchange, point_range
+    assert torch.cuda.is_available()  # torch's HIP runtime first (ilqg_amd.lib)
     m = ia.Model.load(workloads.model_file(name))
     if name == "hopper":
         dmain, H, cost = workloads.hopper_dmain(m, 2, sigma=0.01), 30, ia.HOPPER_COST
@@ -577,6 +579,40 @@ def test_pipelined_iterate(ia, ora, name, prec, chunk, monkeypatch):
             il = _oracle_ilqr(ora, om, _state_dict(dmain, s), H, "ora_cost_desc_fn", 2)
             exact(out[chunk][4][s], il.arrays()["K"], f"seed {s} K vs oracle")
             exact(out[chunk][0][s * P:(s + 1) * P], il.traj()["qpos"], f"seed {s} qpos vs oracle")
+
+
+@pytest.mark.parametrize("G", [2, 3])
+def test_seed_groups_bitexact(ia, ora, G):
+    """ilqg_solver_set_groups: iterate() software-pipelines the seeds as G
+    ranges (per group: rollout + selection on an XCD-masked stream, the fused
+    sweep + recursion on a stream masked to the rest, staggered behind the
+    previous group).  Every seed's trajectory, records, gains, value and costs
+    equal the ungrouped iterate's bit for bit (G = 3 over 4 seeds: uneven
+    ranges 1, 1, 2), through a switch back to one group and an API launch on
+    the solver's stream (ilqg_fd_sweep) between grouped iterates."""
+    import workloads
+    m, _ = setup(ia, ora, "hopper", ia.HOPPER_COST)
+    S, H = 4, 60
+    dmain = workloads.hopper_dmain(m, S, sigma=0.01)
+    out = {}
+    for grp in (1, G):
+        g = ia.ILQR(m, dmain, H, ia.HOPPER_COST, alphas=workloads.LINESEARCH_ALPHAS[:4], select="min_cost")
+        g.set_groups(grp)
+        assert g.groups == grp
+        if grp > 1:
+            assert g.group_rollout_cus in (0, 32)
+        for _ in range(3):
+            g.iterate()
+        g.fd_sweep()  # a launch on the solver's stream: the next grouped iterate joins it
+        g.iterate()
+        g.synchronize()
+        g.set_groups(1)
+        g.iterate()
+        g.synchronize()
+        t = g.traj()
+        out[grp] = (t.qpos, t.qvel, t.ctrl, g.deriv(), *g.gains(), *g.value(), *g.costs())
+    for a, b, what in zip(out[1], out[G], ("qpos", "qvel", "ctrl", "deriv", "K", "k", "V", "v", "costs", "sel")):
+        exact(b, a, what)
 
 
 def test_bench_workload_bitexact(ia, ora):

@@ -81,8 +81,8 @@ for what, fn, rd, rls in (("rollout (1 seed)", g.forward_pass, L.ilqg_debug_stam
             if cnt[i]:
                 print(f"  {W2[i]:24s} calls {cnt[i]:6d}  cycles/call {acc[i]/cnt[i]:9.0f}  share {acc[i]/tot2:6.1%}")
 
-BN = ["stage1 sym/A/B/q/c/r", "stage2 T1=B'V", "stage3 Mm,T3,w,ldlt,col", "stage4 K,k solves",
-      "stage5 ABK,T6,y,kR", "stage6 T4", "stage7 Vn", "stage8 z,vn,K/k out", "V copy + prefetch store"]
+# ilqg_backward on the hopper: the one-lane-per-entry recursion (riccati_mw.h)
+BN = ["A Vs col, T1, v(prev), w", "B T3, Mm, col", "C LDLT, k, K col, ABK, y", "D T4, T6", "E Vn, z, record"]
 if MFMA:
     g.set_riccati("mfma")
     BN = ["1 sym/A/B/q/c/r", "2 T1=B'Vs (mfma)", "3 Mm,T3 (mfma), w", "4 LDLT(Quu), col", "5 perm, K,k solves",
