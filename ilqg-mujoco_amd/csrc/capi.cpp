@@ -296,7 +296,7 @@ struct ilqg_solver {
   bool grp_mw = false;
   DevBuf grp_sync;  // one hand-off block per group
   size_t grp_sync_stride = 0;
-  int grp_xcd = 1;  // ILQG_GROUP_XCD: 1 a whole XCD per group rollout, 0 spread over every XCD (A/B)
+  int grp_xcd = 0;  // ILQG_GROUP_XCD: 1 a whole XCD per group rollout, 0 spread over every XCD (default)
   int grp_rcus = 0;  // CUs per group rollout mask (0: unmasked streams)
   // (A split variant -- the Riccati recursion as a launch of its own on a second
   // stream, streaming a concurrent sweep launch's records -- deadlocked when the
@@ -1467,7 +1467,9 @@ int ilqg_solver_set_groups(ilqg_solver* s, int ngroups) {
   const int nxcd = (ncu >= 64 && ncu % 8 == 0) ? 8 : 1, per = ncu / nxcd;
   const int need = ((s->S + G - 1) / G) * s->A;
   const int k = (need + per - 1) / per;
-  s->grp_xcd = getenv_int("ILQG_GROUP_XCD", 1);
+  // default: the lowest mask bits (the group's rollout spread over every XCD):
+  // measured ahead of a whole XCD per group (profiles/r05_seed_groups.txt)
+  s->grp_xcd = getenv_int("ILQG_GROUP_XCD", 0);
   s->grp_mw = getenv_int("ILQG_GROUP_BW", 1) != 0 && backward_mw_supported(h.nq, h.nv, h.nu);
   const bool masked = getenv_int("ILQG_GROUP_MASK", 1) != 0 && G * k < nxcd;
   s->grp_rcus = masked ? k * per : 0;

@@ -172,6 +172,18 @@ __device__ __forceinline__ real tdotw(const real* a, const real* b, int n) {
 // model traits with compile-time sizes and tables (static_models.h)
 template <class M>
 concept StaticModel = requires { std::integral_constant<int, M::nbody>{}; };
+// a run-time model whose dof count alone is a compile-time constant (the
+// generic rollout kernel's instance for 27-dof models: the humanoid); the
+// Newton Hessian's Cholesky and its substitution drop their size guards
+template <int NV_>
+struct DevModelNV : DevModel {
+  static constexpr int kNV = NV_;
+};
+template <class M>
+constexpr int nv_const() {
+  if constexpr (requires { std::integral_constant<int, M::kNV>{}; }) return M::kNV;
+  else return 0;
+}
 
 // rot_vec_quat / normalize4 with their special cases as selects instead of
 // branches: the same doubles in every case (the general formula is computed
@@ -2248,7 +2260,8 @@ __device__ inline real constraint_update(const auto& m, const auto& L, const aut
 
 __device__ inline void hessian_factor(const auto& m, const auto& L, const auto& C, const Team& T,
                                       real* H) {
-  const int nv = m.nv, ne = T.iw[L.nefc];
+  constexpr int NVC = nv_const<std::remove_cvref_t<decltype(m)>>();
+  const int nv = NVC > 0 ? NVC : m.nv, ne = T.iw[L.nefc];
   real* J = T.w + L.efc_J;
   real* D = T.w + L.efc_D;
   real* qM = T.w + L.qM;
@@ -2311,7 +2324,7 @@ __device__ inline void hessian_factor(const auto& m, const auto& L, const auto& 
   }
 #if ILQG_CHOL32
   if (nv <= 32 && T.nt == TEAM_SIZE) {
-    cholesky_rows32(nv, T.tid, H);
+    cholesky_rows32<nv_const<std::remove_cvref_t<decltype(m)>>()>(nv, T.tid, H);
     return;
   }
 #endif
@@ -2612,7 +2625,8 @@ __device__ inline real ls_iterate(int ne, real g1, real g2, real jr, real jv, re
 
 __device__ inline void solver_newton(const auto& m, const auto& L, const auto& C, const Team& T,
                                      int maxiter, real tol) {
-  const int nv = m.nv, ne = T.iw[L.nefc];
+  constexpr int NVC = nv_const<std::remove_cvref_t<decltype(m)>>();
+  const int nv = NVC > 0 ? NVC : m.nv, ne = T.iw[L.nefc];
   const real scale = 1 / (m.stat_meaninertia * (nv > 1 ? nv : 1));
   real* s = T.w + L.s_newton;
   real *Ma = s, *grad = s + nv, *search = s + 2 * nv, *Mv = s + 3 * nv, *H = s + 4 * nv;
@@ -2652,7 +2666,7 @@ __device__ inline void solver_newton(const auto& m, const auto& L, const auto& C
     } else if (ILQG_CHOLS == 1 && nv <= 32 && T.nt == TEAM_SIZE) {
       chol_solve_rows32(nv, T.tid, H, grad, search);
     } else if (ILQG_CHOLS == 2 && nv <= 32 && T.nt == TEAM_SIZE) {
-      chol_solve_u2(nv, T.tid, H, grad, search);
+      chol_solve_u2<nv_const<std::remove_cvref_t<decltype(m)>>()>(nv, T.tid, H, grad, search);
     } else if (nv <= TEAM_SIZE) {
       chol_solve_wave(nv, T.tid, H, grad, search);
     } else {
@@ -4072,6 +4086,24 @@ constexpr bool coll_split_ok() {
 //     M + h D in one register-row pass;
 //   phase 5: the primary's acceleration stage and constraint solve find the
 //     Newton warm start ready.
+// the rollout teams' phase barriers order LDS only: inside a step the waves
+// hand each other nothing through global memory (the trajectory record's
+// stores and the next record's loads are the only global traffic), so those
+// stay in flight across the barriers instead of being drained at each one
+// (__syncthreads waits for vmcnt(0)); ILQG_PHASE_LDS=0 restores it (A/B)
+#ifndef ILQG_PHASE_LDS
+#define ILQG_PHASE_LDS 1
+#endif
+__device__ __forceinline__ void phase_sync() {
+#if ILQG_PHASE_LDS
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+  __builtin_amdgcn_s_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+#else
+  __syncthreads();
+#endif
+}
+
 __device__ inline void step_dual_split(const auto& m, const auto& L, const auto& C, const auto& X, const Team& T,
                                        int wave, int sid, auto&& pre, auto&& late) {
   const bool A = wave == 0, B = wave == 1;
@@ -4087,9 +4119,9 @@ __device__ inline void step_dual_split(const auto& m, const auto& L, const auto&
       pre();
       late();
     }
-    __syncthreads();
+    phase_sync();
     if (A) reset_data(m, L, T);
-    __syncthreads();  // the helpers' phase-1 work reads the reset state
+    phase_sync();  // the helpers' phase-1 work reads the reset state
   }
   int* nlim_sh = T.ci + C.ibc + 5;  // the limit rows' count, from wave 2 to wave 1
   constexpr bool ksplit = kin_split_ok<std::remove_cvref_t<decltype(m)>>();
@@ -4112,7 +4144,7 @@ __device__ inline void step_dual_split(const auto& m, const auto& L, const auto&
     actuator_force(m, L, T);
     STAMPB(42);
   }
-  __syncthreads();
+  phase_sync();
   const int nlim = *nlim_sh;
   STAMP(24);
   STAMPB(32);
@@ -4146,7 +4178,7 @@ __device__ inline void step_dual_split(const auto& m, const auto& L, const auto&
       STAMPB(33);
     }
   }
-  __syncthreads();
+  phase_sync();
   STAMP(25);
   STAMPB(34);
   STAMPC(51);
@@ -4194,7 +4226,7 @@ __device__ inline void step_dual_split(const auto& m, const auto& L, const auto&
       STAMPC(57);
     }
   }
-  __syncthreads();
+  phase_sync();
   STAMP(26);
   STAMPB(36);
   STAMPC(52);
@@ -4255,7 +4287,7 @@ __device__ inline void step_dual_split(const auto& m, const auto& L, const auto&
     else if constexpr (!split3) factor_m_and_euler(m, L, C, X, T, eul);
     STAMPC(53);
   }
-  __syncthreads();
+  phase_sync();
   STAMP(27);
   STAMPB(39);
   STAMPC(54);
@@ -4268,12 +4300,12 @@ __device__ inline void step_dual_split(const auto& m, const auto& L, const auto&
     if (spec) {
       fwd_constraint_fast(m, L, C, X, T, m.opt_iterations, m.opt_tolerance, true);
     } else {
-      __syncthreads();
+      phase_sync();
       fwd_constraint(m, L, C, X, T, m.opt_iterations, m.opt_tolerance);
     }
     STAMP(8);
   } else {
-    __syncthreads();  // the primary's barrier inside its Newton start
+    phase_sync();  // the primary's barrier inside its Newton start
     // `late` (the caller's work after `pre` that no phase reads: parking the
     // prefetched record) runs here, where wave 1 has slack, so its loads have
     // landed long before
@@ -4282,7 +4314,7 @@ __device__ inline void step_dual_split(const auto& m, const auto& L, const auto&
     if (!B && euler_late) euler_factor_rows(m, L, X, T);
     STAMPB(38);
   }
-  __syncthreads();
+  phase_sync();
   STAMP(29);
   STAMPB(43);
   STAMPC(55);
@@ -4304,7 +4336,7 @@ __device__ inline void step_dual_split(const auto& m, const auto& L, const auto&
     }
     STAMP(9);
   }
-  __syncthreads();
+  phase_sync();
   STAMP(28);
   STAMPB(40);
   STAMPC(56);
@@ -4317,7 +4349,7 @@ __device__ inline void step_dual_split(const auto& m, const auto& L, const auto&
 // quantity is still computed by the same code, so results are unchanged;
 // both waves pass the same __syncthreads sequence.
 __device__ inline void step_dual(const auto& m, const auto& L, const auto& C, const auto& X, const Team& T,
-                                 int wave, auto&& pre) {
+                                 int wave, auto&& pre, auto&& late) {
   const bool A = wave == 0;
   const bool eul = m.opt_integrator != 1;
   STAMP(-1);
@@ -4329,7 +4361,7 @@ __device__ inline void step_dual(const auto& m, const auto& L, const auto& C, co
   const bool bad = any_bad(T, C, T.w + L.qpos, m.nq) || any_bad(T, C, T.w + L.qvel, m.nv);
   if (bad) {
     if (!A) pre();
-    __syncthreads();
+    phase_sync();
     if (A) reset_data(m, L, T);
   }
   if (A) {
@@ -4339,7 +4371,7 @@ __device__ inline void step_dual(const auto& m, const auto& L, const auto& C, co
     pre();
     STAMPB(41);
   }
-  __syncthreads();
+  phase_sync();
   STAMP(24);
   STAMPB(32);
   if (A) {
@@ -4349,7 +4381,7 @@ __device__ inline void step_dual(const auto& m, const auto& L, const auto& C, co
     collision(m, L, C, X, T);
     STAMPB(33);
   }
-  __syncthreads();
+  phase_sync();
   STAMP(25);
   STAMPB(34);
   if (A) {
@@ -4360,7 +4392,7 @@ __device__ inline void step_dual(const auto& m, const auto& L, const auto& C, co
     make_constraint(m, L, C, X, T);
     STAMPB(35);
   }
-  __syncthreads();
+  phase_sync();
   STAMP(26);
   STAMPB(36);
   // the L'DL factor of M runs on the helper beside the com velocities and RNE
@@ -4374,7 +4406,7 @@ __device__ inline void step_dual(const auto& m, const auto& L, const auto& C, co
     factor_ld(m, X, T, T.w + L.qM, T.w + L.qLD, T.w + L.qLDinv, T.c + C.ftmp);
     STAMPB(42);
   }
-  __syncthreads();
+  phase_sync();
   STAMP(27);
   STAMPB(39);
   // the Euler factor of M + h D on the helper beside the constraint solve
@@ -4388,7 +4420,7 @@ __device__ inline void step_dual(const auto& m, const auto& L, const auto& C, co
     if (spec) {
       fwd_constraint_fast(m, L, C, X, T, m.opt_iterations, m.opt_tolerance, true);
     } else {
-      __syncthreads();
+      phase_sync();
       fwd_constraint(m, L, C, X, T, m.opt_iterations, m.opt_tolerance);
     }
     STAMP(8);
@@ -4405,11 +4437,14 @@ __device__ inline void step_dual(const auto& m, const auto& L, const auto& C, co
       if (!done_u) newton_warm_prep(m, L, C, T);
     }
     STAMPB(30);
-    __syncthreads();
+    phase_sync();
     if (eul) euler_prefactor(m, L, C, X, T);
+    // `late` (the caller's work no phase reads: the next point's record into
+    // its second buffer) where the helper waits for the constraint solve
+    late();
     STAMPB(38);
   }
-  __syncthreads();
+  phase_sync();
   STAMP(29);
   STAMPB(43);
   if (A) {
@@ -4425,7 +4460,7 @@ __device__ inline void step_dual(const auto& m, const auto& L, const auto& C, co
     else euler_finish(m, L, C, X, T, !reset);
     STAMP(9);
   }
-  __syncthreads();
+  phase_sync();
   STAMP(28);
   STAMPB(40);
 }

@@ -406,9 +406,11 @@ __device__ inline void cholesky_rows(int nv, int tid, R* H) {
 // diagonal's dot product is lane j's own row dot product -- the oracle's
 // tdot(H_j, H_j, j) and tdot(H_i, H_j, j), ascending from +0.  No LDS round
 // trip or barrier per column (the LDS form: one of each).
-template <class R>
-__device__ inline void cholesky_rows32(int nv, int tid, R* H) {
-  constexpr int NM = 32;
+template <int NC = 0, class R>
+__device__ inline void cholesky_rows32(int nv_rt, int tid, R* H) {
+  // NC > 0: the dof count known at compile time (DevModelNV): no size guards
+  constexpr int NM = NC > 0 ? NC : 32;
+  const int nv = NC > 0 ? NC : nv_rt;
   const bool own = tid < nv;
   R r[NM];
   sfor<0, NM>(SLAM(jj) {
@@ -553,9 +555,10 @@ __device__ inline void chol_solve_wave(int nv, int tid, const R* H, const R* gra
 // each backward step is broadcast from its lane with its reciprocal ready.
 // A handful of VGPRs: no per-row register arrays (register-light for the
 // large generic kernels).
-template <class R>
-__device__ inline void chol_solve_u2(int nv, int tid, const R* H, const R* grad, R* search) {
-  constexpr int NM = 32;
+template <int NC = 0, class R>
+__device__ inline void chol_solve_u2(int nv_rt, int tid, const R* H, const R* grad, R* search) {
+  constexpr int NM = NC > 0 ? NC : 32;
+  const int nv = NC > 0 ? NC : nv_rt;
   const bool own = tid < nv;
   const R dg = own ? H[tid * nv + tid] : (R)1.0;
   const R rg = rcp_ref(dg);

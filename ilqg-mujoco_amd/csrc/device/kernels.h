@@ -25,6 +25,10 @@ struct TrajDev {
 struct RollChunk {
   TrajDev carry{};
   int n_hi = -1, n_lo = 0;
+  // set by launch_rollout_coop (two-wave generic kernel): the nominal record
+  // double-buffered in LDS past the team's workspace, the next point's copied
+  // by the helper wave while the primary runs the constraint solve
+  int dbuf = 0;
 };
 
 // device cost descriptor (all 9 arrays present, zero where unused)

@@ -24,7 +24,7 @@ namespace ilqg {
 namespace {
 
 __device__ inline void rollout_body(const auto& m, const auto& L, const auto& C, const auto& X, const Team& T,
-                                int S, int A, int P, TrajDev nom, TrajDev out, int out_is_cand, const double* K, const double* k, const double* alphas, TrajDev dinit, const double* qfrc_applied, const double* xfrc_applied, int passive, CostDev cost, double* cost_cand, RollChunk ch, int wave, auto split) {
+                                int S, int A, int P, TrajDev nom, TrajDev out, int out_is_cand, const double* K, const double* k, const double* alphas, TrajDev dinit, const double* qfrc_applied, const double* xfrc_applied, int passive, CostDev cost, double* cost_cand, RollChunk ch, int wave, auto split, auto lowreg) {
   // wave < 0: one-wave team; 0/1: primary/helper wave of a two-wave team (step_dual)
   const bool prim = wave <= 0;
   STAMP_INIT();
@@ -49,11 +49,15 @@ __device__ inline void rollout_body(const auto& m, const auto& L, const auto& C,
   // prefetched one point ahead into registers and parked in LDS (C.rec)
   double* rec = T.c + C.rec;
   const int R = nq + nv + nu + nu * nx + nu;
-  const double* rq = rec;
-  const double* rv = rec + nq;
-  const double* ru = rec + nq + nv;
-  const double* rK = ru + nu;
-  const double* rk = rK + nu * nx;
+  // ch.dbuf (generic two-wave kernel): point n's record in buffer (nhi - n) & 1,
+  // the second one past the team's LDS (launch_rollout_coop sized the launch)
+  double* rec2 = rec;
+  if (ch.dbuf) {
+    extern __shared__ double lds[];
+    const size_t off = ((size_t)(L.nd + C.nd + C.imgd) * 8 + (size_t)(L.ni + C.ni) * 4 + 15) / 16 * 16;
+    rec2 = reinterpret_cast<double*>(reinterpret_cast<char*>(lds) + off);
+  }
+  auto recp = [&](int n) -> double* { return ((nhi - n) & 1) ? rec2 : rec; };
   auto fetch = [&](size_t pn, int t) -> double {
     if (t < nq) return nom.qpos[pn * nq + t];
     t -= nq;
@@ -68,7 +72,9 @@ __device__ inline void rollout_body(const auto& m, const auto& L, const auto& C,
   // records up to 20 * 64 doubles (the humanoid's is 1231: K alone is
   // nu x 2nv = 1134) in flight a step ahead as well
   using MT = std::remove_cvref_t<decltype(m)>;
-  constexpr int PFR = StaticModel<MT> ? 4 : 20;
+  // (lowreg: the two-wave generic kernel, whose record is double-buffered in LDS
+  // instead -- 20 prefetch registers spilled to scratch there, a 512-register kernel)
+  constexpr int PFR = StaticModel<MT> ? 4 : (decltype(lowreg)::value ? 1 : 20);
   double pf[PFR];
   // larger records are not prefetched: park() copies them from global memory directly
   const bool pfok = R <= PFR * TEAM_SIZE;
@@ -86,7 +92,12 @@ __device__ inline void rollout_body(const auto& m, const auto& L, const auto& C,
   // control law u = u* + alpha k + K (x - x*) for point n, its record and cost
   // (ilqr.h:116-133); the next point's nominal record is prefetched first
   auto pre_step = [&](int n) {
-    const bool pre = !passive && n > 0 && pfok;
+    const double* rq = recp(n);
+    const double* rv = rq + nq;
+    const double* ru = rq + nq + nv;
+    const double* rK = ru + nu;
+    const double* rk = rK + nu * nx;
+    const bool pre = !passive && n > 0 && pfok && !ch.dbuf;
     if (pre) {
       const size_t pn1 = (size_t)s * P + (n - 1);
 #pragma unroll
@@ -134,7 +145,7 @@ __device__ inline void rollout_body(const auto& m, const auto& L, const auto& C,
   };
   // the prefetched record replaces the current one once the step no longer reads it
   auto park = [&](int n) {
-    if (!passive && n > 0) {
+    if (!passive && n > 0 && !ch.dbuf) {
       if (pfok) {
 #pragma unroll
         for (int q = 0; q < PFR; q++) {
@@ -163,10 +174,30 @@ __device__ inline void rollout_body(const auto& m, const auto& L, const auto& C,
       if constexpr (decltype(split)::value) {
         step_dual_split(m, L, C, X, T, wave, P - n, [&]() { pre_step(n); }, [&]() { park(n); });
       } else {
-        step_dual(m, L, C, X, T, wave, [&]() {
-          pre_step(n);
-          park(n);
-        });
+        step_dual(
+            m, L, C, X, T, wave,
+            [&]() {
+              pre_step(n);
+              park(n);
+            },
+            [&]() {
+              // the next point's record into the other buffer (ch.dbuf)
+              if (ch.dbuf && !passive && n > 0) {
+                double* dst = recp(n - 1);
+                const size_t pn1 = (size_t)s * P + (n - 1);
+                for (int t0 = T.tid; t0 < R; t0 += 4 * TEAM_SIZE) {
+                  double v[4];
+#pragma unroll
+                  for (int q = 0; q < 4; q++) {
+                    const int t = t0 + q * TEAM_SIZE;
+                    v[q] = t < R ? fetch(pn1, t) : 0.0;
+                  }
+#pragma unroll
+                  for (int q = 0; q < 4; q++)
+                    if (t0 + q * TEAM_SIZE < R) dst[t0 + q * TEAM_SIZE] = v[q];
+                }
+              }
+            });
       }
     }
   }
@@ -198,7 +229,7 @@ __global__ __launch_bounds__(TEAM) void k_rollout_coop(DevModel mg, WsLayout L, 
   DevModel m;
   CoopAux X;
   stage_model(mg, Xg, L, C, T, m, X);
-  rollout_body(m, L, C, X, T, S, A, P, nom, out, out_is_cand, K, k, alphas, dinit, qfrc_applied, xfrc_applied, passive, cost, cost_cand, ch, -1, std::false_type{});
+  rollout_body(m, L, C, X, T, S, A, P, nom, out, out_is_cand, K, k, alphas, dinit, qfrc_applied, xfrc_applied, passive, cost, cost_cand, ch, -1, std::false_type{}, std::false_type{});
 }
 
 // model-specific instance (static_models.h): compile-time sizes, tables and LDS layout
@@ -210,17 +241,20 @@ __global__ __launch_bounds__(TEAM) void k_rollout_s(DevModel mg, int S, int A, i
   Team T = make_team(L, C);
   SM m;
   stage_model_sep(mg, T, m);
-  rollout_body(m, L, C, X, T, S, A, P, nom, out, out_is_cand, K, k, alphas, dinit, qfrc_applied, xfrc_applied, passive, cost, cost_cand, ch, -1, std::false_type{});
+  rollout_body(m, L, C, X, T, S, A, P, nom, out, out_is_cand, K, k, alphas, dinit, qfrc_applied, xfrc_applied, passive, cost, cost_cand, ch, -1, std::false_type{}, std::false_type{});
 }
 
-// two-wave teams (step_dual): 128 threads per (seed, candidate)
+// two-wave teams (step_dual): 128 threads per (seed, candidate).  MT: DevModel,
+// or DevModelNV<27> for 27-dof models (the humanoid: compile-time sizes in the
+// Newton Cholesky and its substitution)
+template <class MT>
 __global__ __launch_bounds__(2 * TEAM) void k_rollout2_coop(DevModel mg, WsLayout L, CoopLayout C, CoopAux Xg, int S, int A, int P, TrajDev nom, TrajDev out, int out_is_cand, const double* K, const double* k, const double* alphas, TrajDev dinit, const double* qfrc_applied, const double* xfrc_applied, int passive, CostDev cost, double* cost_cand, RollChunk ch) {
   Team T = make_team(L, C);
-  DevModel m;
+  MT m;
   CoopAux X;
   stage_model(mg, Xg, L, C, T, m, X);
   rollout_body(m, L, C, X, T, S, A, P, nom, out, out_is_cand, K, k, alphas, dinit, qfrc_applied, xfrc_applied,
-               passive, cost, cost_cand, ch, (int)(threadIdx.x / TEAM), std::false_type{});
+               passive, cost, cost_cand, ch, (int)(threadIdx.x / TEAM), std::false_type{}, std::true_type{});
 }
 // three-wave teams for the compile-time register-row models (step_dual_split),
 // two-wave otherwise
@@ -235,7 +269,8 @@ __global__ __launch_bounds__(3 * TEAM) void k_rollout2_s(DevModel mg, int S, int
   SM m;
   stage_model_sep(mg, T, m);
   rollout_body(m, L, C, X, T, S, A, P, nom, out, out_is_cand, K, k, alphas, dinit, qfrc_applied, xfrc_applied,
-               passive, cost, cost_cand, ch, (int)(threadIdx.x / TEAM), std::bool_constant<SM::nv <= RMAX>{});
+               passive, cost, cost_cand, ch, (int)(threadIdx.x / TEAM), std::bool_constant<SM::nv <= RMAX>{},
+               std::false_type{});
 }
 
 // ---- batch physics (ilqg_step_batch / ilqg_forward_batch): one wavefront per state
@@ -397,9 +432,36 @@ hipError_t launch_rollout_coop(const DevModel& m, const WsLayout& L, const CoopL
         break;
     }
 #undef ILQG_CASE
-    e = allow_lds(k_rollout2_coop, lds);
+    // the record's second buffer past the workspace when it fits (RollChunk.dbuf;
+    // ILQG_ROLL_DBUF=0 keeps the register prefetch, A/B)
+    size_t lds_d = lds;
+    {
+      static const int dbuf_env = [] {
+        const char* v = getenv("ILQG_ROLL_DBUF");
+        return (v && v[0] == '0') ? 0 : 1;
+      }();
+      const size_t R = (size_t)m.nq + m.nv + m.nu + (size_t)m.nu * 2 * m.nv + m.nu;
+      const size_t need = (coop_lds_bytes(L, C) + 15) / 16 * 16 + R * sizeof(double);
+      if (dbuf_env && need <= 160 * 1024) {
+        ch.dbuf = 1;
+        lds_d = need > lds ? need : lds;
+      }
+    }
+    static const int nvc_env = [] {
+      const char* v = getenv("ILQG_NV_CONST");
+      return (v && v[0] == '0') ? 0 : 1;
+    }();
+    const bool nv27 = nvc_env && m.nv == 27;
+    const void* kf = nv27 ? reinterpret_cast<const void*>(k_rollout2_coop<DevModelNV<27>>)
+                          : reinterpret_cast<const void*>(k_rollout2_coop<DevModel>);
+    e = hipFuncSetAttribute(kf, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_d);
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(k_rollout2_coop, dim3(S * A), dim3(2 * TEAM), lds, st, m, L, C, X, S, A, P, nominal, out,
+    if (nv27)
+      hipLaunchKernelGGL(k_rollout2_coop<DevModelNV<27>>, dim3(S * A), dim3(2 * TEAM), lds_d, st, m, L, C, X, S, A,
+                         P, nominal, out, out_is_cand, K, k, alphas, dinit, qfrc_applied, xfrc_applied, passive, cost,
+                         cost_cand, ch);
+    else
+    hipLaunchKernelGGL(k_rollout2_coop<DevModel>, dim3(S * A), dim3(2 * TEAM), lds_d, st, m, L, C, X, S, A, P, nominal, out,
                        out_is_cand, K, k, alphas, dinit, qfrc_applied, xfrc_applied, passive, cost, cost_cand, ch);
     return hipGetLastError();
   }

@@ -151,11 +151,13 @@ hipError_t launch_backward_mw(const DevModel& m, int S, int P, double mu, const 
 
 hipError_t launch_backward(const DevModel& m, int S, int P, double mu, const double* deriv, int Ds, TrajDev tr,
                            double* K, double* k, double* V, double* v, RicFlags fl, hipStream_t st) {
-  // the register-formulation sizes: one lane per matrix entry (riccati_mw.h);
-  // ILQG_BW_MW=0 keeps the one-wave kernel (A/B)
+  // ILQG_BW_MW=1: the register-formulation sizes on the one-lane-per-entry
+  // kernel (riccati_mw.h; the seed groups' streaming recursion).  Off by
+  // default: standalone it measured 3.8 us a hopper step against the one-wave
+  // kernel's 3.55 (profiles/r05_seed_groups.txt)
   static const int mw = [] {
     const char* e = getenv("ILQG_BW_MW");
-    return (e && e[0] == '0') ? 0 : 1;
+    return (e && e[0] == '1') ? 1 : 0;
   }();
   if (mw && backward_mw_supported(m.nq, m.nv, m.nu))
     return launch_backward_mw(m, S, P, mu, deriv, Ds, tr, K, k, V, v, fl, nullptr, 0u, nullptr, st);
