@@ -73,10 +73,15 @@ __device__ inline void load_state32(const DevModel& m, const WsLayout& L, const 
   TSYNC();
 }
 
-__global__ __launch_bounds__(TEAM32) void k_fd_centre32(DevModel m, WsLayout L, coop::CoopLayout C, coop::CoopAux X,
+// MT: DevModel, or DevModelNV<27> for 27-dof models (the humanoid: compile-time
+// sizes in the Newton Cholesky and its substitution, as the rollout's instance)
+template <class MT>
+__global__ __launch_bounds__(TEAM32) void k_fd_centre32(DevModel mg, WsLayout L, coop::CoopLayout C, coop::CoopAux X,
                                                         TrajDev tr, int P, const double* qfrc_applied,
                                                         const double* xfrc_applied, CostDev cost, double* warm_c,
                                                         double* cost_c) {
+  MT m;
+  static_cast<DevModel&>(m) = mg;
   Team T = make_team32(L, C);
   const int pt = blockIdx.x;
   load_state32(m, L, T, tr, pt, pt / P, qfrc_applied, xfrc_applied);
@@ -87,10 +92,13 @@ __global__ __launch_bounds__(TEAM32) void k_fd_centre32(DevModel m, WsLayout L, 
   if (T.tid == 0) cost_c[pt] = step_cost32(m, cost, T.w + L.qpos, T.w + L.qvel, T.w + L.ctrl);
 }
 
-__global__ __launch_bounds__(TEAM32) void k_fd_cols32(DevModel m, WsLayout L, coop::CoopLayout C, coop::CoopAux X,
+template <class MT>
+__global__ __launch_bounds__(TEAM32) void k_fd_cols32(DevModel mg, WsLayout L, coop::CoopLayout C, coop::CoopAux X,
                                                       TrajDev tr, int P, const double* qfrc_applied,
                                                       const double* xfrc_applied, CostDev cost, const double* warm_c,
                                                       const double* cost_c, double* deriv, int Ds, float eps) {
+  MT m;
+  static_cast<DevModel&>(m) = mg;
   Team T = make_team32(L, C);
   const int nv = m.nv, nu = m.nu;
   const int nctrl = nu < nv ? nu : nv;  // mjderivative.cpp:78-82 (assumes nv >= nu)
@@ -177,25 +185,40 @@ static hipError_t allow_lds32(const void* kern, size_t lds) {
   return hipFuncSetAttribute(kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
 }
 
-hipError_t launch_fd_sweep_f32(const DevModel& m, const WsLayout& L, const coop::CoopLayout& C,
-                               const coop::CoopAux& X, TrajDev tr, int npts, int P, const double* qfrc_applied,
-                               const double* xfrc_applied, CostDev cost, double* warm_c, double* cost_c,
-                               double* deriv, int Ds, double eps, hipStream_t st) {
-  if (npts <= 0) return hipSuccess;
+template <class MT>
+static hipError_t launch_fd32_t(const DevModel& m, const WsLayout& L, const coop::CoopLayout& C, const coop::CoopAux& X,
+                                TrajDev tr, int npts, int P, const double* qfrc_applied, const double* xfrc_applied,
+                                CostDev cost, double* warm_c, double* cost_c, double* deriv, int Ds, double eps,
+                                hipStream_t st) {
   const size_t lds = coop_lds_bytes_f32(L, C);
-  hipError_t e = allow_lds32(reinterpret_cast<const void*>(k_fd_centre32), lds);
+  hipError_t e = allow_lds32(reinterpret_cast<const void*>(k_fd_centre32<MT>), lds);
   if (e != hipSuccess) return e;
-  e = allow_lds32(reinterpret_cast<const void*>(k_fd_cols32), lds);
+  e = allow_lds32(reinterpret_cast<const void*>(k_fd_cols32<MT>), lds);
   if (e != hipSuccess) return e;
-  hipLaunchKernelGGL(k_fd_centre32, dim3(npts), dim3(TEAM32), lds, st, m, L, C, X, tr, P, qfrc_applied,
+  hipLaunchKernelGGL(k_fd_centre32<MT>, dim3(npts), dim3(TEAM32), lds, st, m, L, C, X, tr, P, qfrc_applied,
                      xfrc_applied, cost, warm_c, cost_c);
   e = hipGetLastError();
   if (e != hipSuccess) return e;
   const int nctrl = m.nu < m.nv ? m.nu : m.nv;
   const long blocks = (long)npts * (nctrl + 2 * m.nv);
-  hipLaunchKernelGGL(k_fd_cols32, dim3((unsigned)blocks), dim3(TEAM32), lds, st, m, L, C, X, tr, P, qfrc_applied,
+  hipLaunchKernelGGL(k_fd_cols32<MT>, dim3((unsigned)blocks), dim3(TEAM32), lds, st, m, L, C, X, tr, P, qfrc_applied,
                      xfrc_applied, cost, warm_c, cost_c, deriv, Ds, (float)eps);
   return hipGetLastError();
+}
+
+hipError_t launch_fd_sweep_f32(const DevModel& m, const WsLayout& L, const coop::CoopLayout& C,
+                               const coop::CoopAux& X, TrajDev tr, int npts, int P, const double* qfrc_applied,
+                               const double* xfrc_applied, CostDev cost, double* warm_c, double* cost_c,
+                               double* deriv, int Ds, double eps, hipStream_t st) {
+  if (npts <= 0) return hipSuccess;
+  static const int nvc_env = [] {
+    const char* v = getenv("ILQG_NV_CONST");
+    return (v && v[0] == '0') ? 0 : 1;
+  }();
+  if (nvc_env && m.nv == 27) return launch_fd32_t<DevModelNV<27>>(m, L, C, X, tr, npts, P, qfrc_applied, xfrc_applied,
+                                                                 cost, warm_c, cost_c, deriv, Ds, eps, st);
+  return launch_fd32_t<DevModel>(m, L, C, X, tr, npts, P, qfrc_applied, xfrc_applied, cost, warm_c, cost_c, deriv, Ds,
+                                 eps, st);
 }
 
 }  // namespace ilqg
