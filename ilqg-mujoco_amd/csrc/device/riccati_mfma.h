@@ -77,6 +77,26 @@ __device__ __forceinline__ void product(int rows, int cols, int K, const GA& ga,
   }
 }
 
+// sum_{k<n} fa(k) fb(k), ascending from +0 (the oracle's loops), with eight
+// terms' operands read ahead of their additions
+template <class FA, class FB>
+__device__ __forceinline__ double dot8(int n, const FA& fa, const FB& fb) {
+  double s = 0;
+  int k = 0;
+  for (; k + 8 <= n; k += 8) {
+    double a[8], b[8];
+#pragma unroll
+    for (int q = 0; q < 8; q++) {
+      a[q] = fa(k + q);
+      b[q] = fb(k + q);
+    }
+#pragma unroll
+    for (int q = 0; q < 8; q++) s += a[q] * b[q];
+  }
+  for (; k < n; k++) s += fa(k) * fb(k);
+  return s;
+}
+
 // LDS (doubles) for (nv, nu): see the layout in backward_seed_mfma
 __host__ __device__ inline size_t lds_doubles(int nv, int nu) {
   const size_t nx = 2 * (size_t)nv, LX = nx | 1, LU = (size_t)nu | 1;
@@ -204,8 +224,7 @@ __device__ inline void backward_seed_mfma(const MD& m, int nq, int nv, int nu_rt
         nu, nx, nx, gT1, [&](int k, int j) { return (k < nx && j < nx) ? A[k + j * LX] : 0.0; },
         [&](int a, int j, double x) { Y1[a + j * LU] = x; }, wave, lane);
     for (int i = tid; i < nx; i += THREADS) {
-      double sm = 0;
-      for (int j = 0; j < nx; j++) sm += Vs[i + j * LX] * c[j];
+      const double sm = dot8(nx, [&](int j) { return Vs[i + j * LX]; }, [&](int j) { return c[j]; });
       w[i] = v[i] + 2 * sm;
     }
     __syncthreads();
@@ -216,8 +235,7 @@ __device__ inline void backward_seed_mfma(const MD& m, int nq, int nv, int nu_rt
       else ldlt_factor_wave(nu, Mm, trn, tmp, lane);
     }
     for (int a = tid - 64; a >= 0 && a < nu; a += THREADS) {
-      double sm = 0;
-      for (int kk = 0; kk < nx; kk++) sm += B[kk + a * LX] * w[kk];
+      const double sm = dot8(nx, [&](int kk) { return B[kk + a * LX]; }, [&](int kk) { return w[kk]; });
       col[a] = sm + r[a];
     }
     __syncthreads();
@@ -252,15 +270,11 @@ __device__ inline void backward_seed_mfma(const MD& m, int nq, int nv, int nu_rt
         [&](int a, int b) { return (a < nu && b < nu) ? r[a] * r[b] : 0.0; },
         [&](int i, int b, double x) { X1[i + b * LX] = x; }, wave, lane);
     for (int i = tid; i < nx; i += THREADS) {
-      double sm = 0;
-      for (int a = 0; a < nu; a++) sm += B[i + a * LX] * kl[a];
+      const double sm = dot8(nu, [&](int a) { return B[i + a * LX]; }, [&](int a) { return kl[a]; });
       y[i] = sm + c[i];
     }
-    for (int b = tid; b < nu; b += THREADS) {
-      double sm = 0;
-      for (int a = 0; a < nu; a++) sm += kl[a] * (r[a] * r[b]);
-      kR[b] = sm;
-    }
+    for (int b = tid; b < nu; b += THREADS)
+      kR[b] = dot8(nu, [&](int a) { return kl[a]; }, [&](int a) { return r[a] * r[b]; });
     __syncthreads();
     BSTAMP(5);
     // stage 7: T4 = ABK' Vs (into A's buffer: A is dead)
@@ -291,19 +305,13 @@ __device__ inline void backward_seed_mfma(const MD& m, int nq, int nv, int nu_rt
     __syncthreads();
     BSTAMP(7);
     // stage 9: z = (2y)' V_new ; v_new (reads the NEW V, quirk Q14)
-    for (int j = tid; j < nx; j += THREADS) {
-      double sm = 0;
-      for (int i = 0; i < nx; i++) sm += (2 * y[i]) * Vn[i + j * LX];
-      z[j] = sm;
-    }
+    for (int j = tid; j < nx; j += THREADS)
+      z[j] = dot8(nx, [&](int i) { return 2 * y[i]; }, [&](int i) { return Vn[i + j * LX]; });
     __syncthreads();
     for (int j = tid; j < nx; j += THREADS) {
-      double ta = 0, tb = 0, td = 0;
-      for (int i = 0; i < nx; i++) {
-        ta += z[i] * ABK[i + j * LX];
-        tb += v[i] * ABK[i + j * LX];
-      }
-      for (int b = 0; b < nu; b++) td += (2 * kR[b]) * Y1[b + j * LU];
+      const double ta = dot8(nx, [&](int i) { return z[i]; }, [&](int i) { return ABK[i + j * LX]; });
+      const double tb = dot8(nx, [&](int i) { return v[i]; }, [&](int i) { return ABK[i + j * LX]; });
+      const double td = dot8(nu, [&](int b) { return 2 * kR[b]; }, [&](int b) { return Y1[b + j * LU]; });
       vn[j] = ((ta + tb) + q[j]) + td;
     }
     // gains out (Eigen col-major K[a + j nu])
