@@ -272,8 +272,9 @@ struct ilqg_solver {
   // fd_stream behind it (ILQG_PIPE_CHUNK, read at creation; 0 = off)
   int pipe_chunk = 0;
   bool pipe_flat = false;  // ILQG_PIPE_FLAT: equal chunks to the end (A/B)
-  static constexpr int kFdStreams = 3;  // chunk c's sweep on fd_stream[c % 3]: the launches' tails overlap
+  static constexpr int kFdStreams = 4;  // chunk c's sweep on fd_stream[c % nfd]: the launches' tails overlap
   hipStream_t fd_stream[kFdStreams] = {};
+  int nfd = 3;  // ILQG_PIPE_STREAMS (1 .. 4), read at creation
   std::vector<hipEvent_t> pipe_ev;
   DevBuf carry[5];  // the chunked rollout's state between launches, [S][...]
   // seed groups (ilqg_solver_set_groups): the seeds as G contiguous ranges,
@@ -729,8 +730,11 @@ int ilqg_solver_create(const ilqg_model* mc, const ilqg_solver_opts* o, const il
     }
   }
   ALLOC(s->fault, 2 * ilqg_solver::kMaxGroups * sizeof(unsigned));  // one fault block (handoff.h) per seed group
-  s->pipe_chunk = getenv_int("ILQG_PIPE_CHUNK", 16);
-  s->pipe_flat = getenv_int("ILQG_PIPE_FLAT", 0) != 0;
+  // chunks of 8 points to the end (flat): cfg 5 18.4 iterations/s against
+  // 17.7-17.8 with 16 and halving tail chunks (profiles/r05_cfg5_pipeline.txt)
+  s->pipe_chunk = getenv_int("ILQG_PIPE_CHUNK", 8);
+  s->pipe_flat = getenv_int("ILQG_PIPE_FLAT", 1) != 0;
+  s->nfd = std::min(std::max(getenv_int("ILQG_PIPE_STREAMS", 3), 1), (int)ilqg_solver::kFdStreams);
   if (s->A == 1 && s->pipe_chunk > 0 && s->pipe_chunk < (int)P) {
     // the sweep streams leave CUs to the rollout: a rollout chunk's workgroup
     // (the humanoid's: 147 KB of LDS, a CU to itself) waited up to 13 ms for
@@ -739,21 +743,26 @@ int ilqg_solver_create(const ilqg_model* mc, const ilqg_solver_opts* o, const il
     int ncu = 0;
     e = hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, o->device);
     if (e != hipSuccess) return fail_free(e, "hipDeviceGetAttribute");
-    // (ILQG_PIPE_KEEP: how many; ILQG_PIPE_LOW=1: the lowest-numbered ones)
-    // Default: the lowest ncu / 8 CUs -- one XCD's worth, so the rollout keeps an
-    // L2 of its own (the humanoid reads its model image from global memory
-    // every step): cfg 5 rollout chunks 212 -> 177 us per step beside the
-    // sweep (profiles/r05_cfg5_pipeline.txt; one CU per seed spread over the
-    // chip did not help)
+    // (ILQG_PIPE_KEEP: how many; ILQG_PIPE_LOW: 1 the lowest-numbered mask
+    // bits, which KFD deals round-robin over the XCDs (bit c -> XCD c % 8), so
+    // ncu / 8 of them are four CUs on every XCD; 2 the CUs of one XCD (bits
+    // c % 8 == 0), an L2 of the rollout's own; 0 spread evenly by bit).
+    // Default: the lowest ncu / 8: cfg 5 rollout chunks 212 -> 177 us per step
+    // beside the sweep (profiles/r05_cfg5_pipeline.txt)
     const int keep = std::min(getenv_int("ILQG_PIPE_KEEP", std::max((int)S, ncu / 8)), ncu / 4);
-    const bool low = getenv_int("ILQG_PIPE_LOW", 1) != 0;
+    const int low = getenv_int("ILQG_PIPE_LOW", 1);
+    const int nxcd = (ncu >= 64 && ncu % 8 == 0) ? 8 : 1;
     std::vector<uint32_t> fmask((ncu + 31) / 32, 0);
     for (int c = 0, j = 0; c < ncu; c++) {
-      const bool r = low ? c < keep : (j < keep && (long)c * keep / ncu >= j);  // spread: over every XCD
+      bool r;
+      if (low == 1) r = c < keep;
+      else if (low == 2) r = j < keep && c % nxcd == 0;
+      else r = j < keep && (long)c * keep / ncu >= j;  // spread evenly by bit
       if (r) j++;
       else fmask[c / 32] |= 1u << (c % 32);
     }
-    for (auto& fs : s->fd_stream) {
+    for (int f = 0; f < s->nfd; f++) {
+      hipStream_t& fs = s->fd_stream[f];
       e = keep > 0 ? hipExtStreamCreateWithCUMask(&fs, (uint32_t)fmask.size(), fmask.data())
                    : hipStreamCreateWithFlags(&fs, hipStreamNonBlocking);
       if (e != hipSuccess) return fail_free(e, "hipStreamCreate");
@@ -992,7 +1001,7 @@ static int iterate_pipelined(ilqg_solver* s) {
     ch.n_lo = lo;
     HIPCHK(rollout_launch(s, r, ch));
     HIPCHK(hipEventRecord(s->pipe_ev[ev], s->stream));
-    hipStream_t fs = s->fd_stream[ev % ilqg_solver::kFdStreams];
+    hipStream_t fs = s->fd_stream[ev % s->nfd];
     HIPCHK(hipStreamWaitEvent(fs, s->pipe_ev[ev], 0));
     ev++;
     HIPCHK(s->timed(3, [&] { return fd_range_launch(s, lo, hi - lo + 1, fs); }, fs));
@@ -1004,6 +1013,7 @@ static int iterate_pipelined(ilqg_solver* s) {
                          s->sel.as<int>(), s->cost_sel.as<double>(), nom, nom, di, s->stream);
   }));
   for (auto fs : s->fd_stream) {
+    if (!fs) continue;
     HIPCHK(hipEventRecord(s->pipe_ev[ev], fs));
     HIPCHK(hipStreamWaitEvent(s->stream, s->pipe_ev[ev], 0));
     ev++;
