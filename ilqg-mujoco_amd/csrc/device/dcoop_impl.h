@@ -116,6 +116,11 @@ __shared__ unsigned long long s_stamp_acc[STAMP_N], s_stamp_cnt[STAMP_N], s_stam
 #endif
 // below this many dofs the small factorizations run on lane 0 (fewer LDS round trips)
 constexpr int SERIAL_NV = 12;
+// the Newton Hessian's build for compile-time dof counts: a lane per row block
+// (HessLanes) instead of a lane per entry (0: the per-entry form, A/B)
+#ifndef ILQG_HESS_ROWS
+#define ILQG_HESS_ROWS 1
+#endif
 // the Newton Hessian's Cholesky in row registers up to 32 dofs (cholesky_rows32)
 #ifndef ILQG_CHOL32
 #define ILQG_CHOL32 1
@@ -2258,6 +2263,23 @@ __device__ inline real constraint_update(const auto& m, const auto& L, const aut
   return T.c[C.bc];
 }
 
+// compile-time lane map of the Hessian build for NVC dofs: lane t owns up to
+// HB consecutive entries of one lower-triangle row (row r, columns c0 ..
+// c0 + cnt - 1); every row takes ceil((r + 1) / HB) lanes
+constexpr int HB = 8;
+template <int NVC>
+struct HessLanes {
+  int n = 0;
+  constexpr HessLanes() {
+    for (int rr = 0; rr < NVC; rr++) n += rr / HB + 1;
+  }
+};
+template <int NVC>
+constexpr bool hess_lanes_ok() {
+  if constexpr (NVC > 0) return HessLanes<NVC>{}.n <= 64;
+  else return false;
+}
+
 __device__ inline void hessian_factor(const auto& m, const auto& L, const auto& C, const Team& T,
                                       real* H) {
   constexpr int NVC = nv_const<std::remove_cvref_t<decltype(m)>>();
@@ -2279,6 +2301,55 @@ __device__ inline void hessian_factor(const auto& m, const auto& L, const auto& 
   for (int q = 0; q < HMASK; q++) {
     const int i = 64 * q + T.tid;
     am[q] = bal && 64 * q < ne ? __ballot(i < ne && state[i] != 0) : 0ull;
+  }
+  // (fp64 only: the fp32 FD sweep's instance measured slower, 4.31 -> 4.41 ms a
+  // chunk, while the fp64 rollout's chunk went 1.509 -> 1.395 ms)
+  if constexpr (hess_lanes_ok<NVC>() && ILQG_HESS_ROWS && sizeof(real) == 8) {
+    if (bal) {
+      // lane t: entries (r, c0 .. c0 + cnt - 1) of one row; per active row i
+      // (ascending, the oracle's order) J(i, r) D(i) is formed once and each
+      // entry adds (J(i, r) D(i)) J(i, c) -- the per-entry form's operations
+      constexpr int NL = HessLanes<NVC>{}.n;
+      const int t = T.tid;
+      const bool own = t < NL;
+      // lane t's block: rows take rr / HB + 1 lanes each, in row order
+      int r = 0, c0 = 0, cnt = 0;
+      {
+        int acc = 0;
+        sfor<0, NVC>(SLAM(rq) {
+          constexpr int rr = SK(rq), nb = rr / HB + 1;
+          if (t >= acc && t < acc + nb) {
+            r = rr;
+            c0 = (t - acc) * HB;
+            cnt = rr + 1 - c0 < HB ? rr + 1 - c0 : HB;
+          }
+          acc += nb;
+        });
+      }
+      real h[HB];
+#pragma unroll
+      for (int q = 0; q < HB; q++) h[q] = 0;
+#pragma unroll
+      for (int w = 0; w < HMASK; w++) {
+        for (unsigned long long mm = am[w]; mm; mm &= mm - 1) {
+          const int i = 64 * w + __builtin_ctzll(mm);
+          const real* Ji = J + i * nv;
+          const real ad = Ji[r] * D[i];
+          real b[HB];
+#pragma unroll
+          for (int q = 0; q < HB; q++) b[q] = Ji[c0 + (q < cnt ? q : 0)];
+#pragma unroll
+          for (int q = 0; q < HB; q++)
+            if (q < cnt) h[q] += ad * b[q];
+        }
+      }
+      if (own) {
+#pragma unroll
+        for (int q = 0; q < HB; q++)
+          if (q < cnt) H[r * nv + c0 + q] = qM[r * nv + c0 + q] + h[q];
+      }
+      goto built;
+    }
   }
   FOR_T(e, ntri) {
     int r = (int)((sqrtf(8.0f * (float)e + 1.0f) - 1.0f) * 0.5f);
@@ -2316,6 +2387,7 @@ __device__ inline void hessian_factor(const auto& m, const auto& L, const auto& 
     }
     H[r * nv + c] = qM[r * nv + c] + h;
   }
+built:
   TSYNC();
   STAMP(31);
   if (nv <= RMAX) {
