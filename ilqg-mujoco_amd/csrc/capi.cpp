@@ -730,9 +730,10 @@ int ilqg_solver_create(const ilqg_model* mc, const ilqg_solver_opts* o, const il
     }
   }
   ALLOC(s->fault, 2 * ilqg_solver::kMaxGroups * sizeof(unsigned));  // one fault block (handoff.h) per seed group
-  // chunks of 8 points to the end (flat): cfg 5 18.4 iterations/s against
-  // 17.7-17.8 with 16 and halving tail chunks (profiles/r05_cfg5_pipeline.txt)
-  s->pipe_chunk = getenv_int("ILQG_PIPE_CHUNK", 8);
+  // chunks of 10 points to the end (flat): cfg 5 19.4 iterations/s against
+  // 18.3-18.4 with 8 and 17.7-17.8 with 16 and halving tail chunks
+  // (profiles/r05_cfg5_pipeline.txt)
+  s->pipe_chunk = getenv_int("ILQG_PIPE_CHUNK", 10);
   s->pipe_flat = getenv_int("ILQG_PIPE_FLAT", 1) != 0;
   s->nfd = std::min(std::max(getenv_int("ILQG_PIPE_STREAMS", 3), 1), (int)ilqg_solver::kFdStreams);
   if (s->A == 1 && s->pipe_chunk > 0 && s->pipe_chunk < (int)P) {
