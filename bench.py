@@ -272,11 +272,13 @@ def run_humanoid_cfg5(args, world, rank, local_rank):
     root at z = 1.4, humanoid.xml:49-50), fp32 FD (eps 1e-3) with the fp64
     Riccati recursion on the matrix cores (ilqg_solver_set_riccati MFMA).  On
     N > 1 GPUs the one seed's FD sweep is point-sharded (--cfg5-shard points,
-    the default): every rank rolls out the same trajectory, differentiates its
-    block of the H + 1 points (ilqg_fd_sweep_range), one RCCL all-gather of the
-    fp64 records (RecordExchange, 3.4 MB) gives every rank all of them, and
-    every rank runs the recursion; value = iterations/s of that one seed
-    (strong scaling).  --cfg5-shard replicas runs N independent replicas
+    the default): every rank rolls out the same trajectory in the pipelined
+    iterate's chunks and differentiates the points it owns behind them
+    (ilqg_forward_sharded: chunks round-robin, the last chunks split over all
+    ranks), one RCCL all-gather of the fp64 records (RecordExchange, 3.4 MB)
+    gives every rank all of them, and every rank runs the recursion; the
+    warm-up checks that every rank's trajectory is bit-identical.  value =
+    iterations/s of that one seed (strong scaling).  --cfg5-shard replicas runs N independent replicas
     instead.  A separate line, not the headline."""
     H = 200
     P = H + 1
@@ -288,15 +290,19 @@ def run_humanoid_cfg5(args, world, rank, local_rank):
     g.set_fd_precision("f32")
     shard = world > 1 and args.cfg5_shard == "points"
     if shard:
-        from seed_shard import RecordExchange
+        from seed_shard import RecordExchange, check_same_trajectory, device_view
         stream = torch.cuda.Stream()
         g.set_stream(stream.cuda_stream)
         rx = RecordExchange.for_solver(g, rank, world)
+        # the resident nominal trajectory (every rank's own rollout), for the
+        # cross-rank check that the records spliced together describe one trajectory
+        traj = [device_view(g.device_traj_ptr(f), P * n) for f, n in (("qpos", m.nq), ("qvel", m.nv), ("ctrl", m.nu))]
 
         def one_iter():
             with torch.cuda.stream(stream):
-                g.forward_pass()
-                g.fd_sweep_range(rx.p0, rx.np)
+                # the pipelined rollout with this rank's points differentiated
+                # behind its chunks, the gather, then the recursion on every rank
+                g.forward_sharded(rank, world)
                 rx.exchange()
                 g.riccati_pass()
     else:
@@ -304,6 +310,9 @@ def run_humanoid_cfg5(args, world, rank, local_rank):
             g.iterate()
     for _ in range(args.warmup):
         one_iter()
+        if shard:
+            with torch.cuda.stream(stream):
+                check_same_trajectory(traj, world)
     g.synchronize()
     if world > 1:
         dist.barrier()
@@ -328,7 +337,8 @@ def run_humanoid_cfg5(args, world, rank, local_rank):
     # points one FD launch differentiates: this rank's block, over the chunks
     # of the pipelined iteration (ILQG_PIPE_CHUNK: one sweep launch per chunk)
     fd_launches = max((kt.get("fd_cols", {}).get("launches", 0) or kt.get("fd_centre", {}).get("launches", 0)), 1)
-    fd_pts = (rx.np if shard else P) / max(fd_launches / args.steps, 1.0)
+    fd_pts = (rx.nown if shard else P) / max(fd_launches / args.steps, 1.0)
+    roll_pts = P / max(kt.get("rollout", {}).get("launches", 0) / args.steps, 1.0)
     fd_tf = fd_pts * hf["fd_point"]["flops"] / (fd_ms * 1e-3) / 1e12 if fd_ms else 0.0
     bw_tf = H * hf["riccati_step"]["flops"] / (bw_ms * 1e-3) / 1e12 if bw_ms else 0.0
     value = (1 if shard else world) * args.steps / elapsed
@@ -347,7 +357,10 @@ def run_humanoid_cfg5(args, world, rank, local_rank):
                                   f"replicas x{world}"},
         "kernels": kt,
         "roofline": {
-            "rollout": {"bound": "latency", "us_per_step": roll_ms / P * 1e3},
+            # per serial step: one launch's time over the points it steps (the
+            # pipelined iterate launches the rollout in chunks of ILQG_PIPE_CHUNK points)
+            "rollout": {"bound": "latency", "avg_launch_ms": roll_ms, "points_per_launch": roll_pts,
+                        "us_per_step": roll_ms / roll_pts * 1e3},
             "fd_sweep": {"bound": "fp32-valu", "flops_per_launch": fd_pts * hf["fd_point"]["flops"],
                          "avg_launch_ms": fd_ms, "achieved_tflops": fd_tf, "peak_tflops": FP32_PEAK_TFS,
                          "frac": fd_tf / FP32_PEAK_TFS,

@@ -289,12 +289,11 @@ struct ilqg_solver {
   int ngroups = 1;
   bool grp_join = true;  // the next grouped iterate waits for the solver's stream first
   hipStream_t grp_roll[kMaxGroups] = {}, grp_fd[kMaxGroups] = {};
-  hipEvent_t grp_sel[kMaxGroups] = {}, grp_done[kMaxGroups] = {}, grp_zero[kMaxGroups] = {},
-            grp_fdend[kMaxGroups] = {};
-  // ILQG_GROUP_BW (default 1, read by set_groups): each group's recursion as a
-  // launch of its own beside its sweep (riccati_mw.h, one lane per matrix
-  // entry) where the model has that kernel; 0: streamed inside the fused sweep
-  bool grp_mw = false;
+  hipEvent_t grp_sel[kMaxGroups] = {}, grp_done[kMaxGroups] = {};
+  // Each group's recursion streams inside its own fused sweep launch: no
+  // consumer ever spin-waits on a producer in another launch or stream (round 5
+  // ran it as a launch of its own beside the sweep, which broke the rule below
+  // and measured slower; removed in round 6).
   DevBuf grp_sync;  // one hand-off block per group
   size_t grp_sync_stride = 0;
   int grp_xcd = 0;  // ILQG_GROUP_XCD: 1 a whole XCD per group rollout, 0 spread over every XCD (default)
@@ -364,10 +363,8 @@ struct ilqg_solver {
       if (grp_fd[g]) (void)hipStreamDestroy(grp_fd[g]);
       if (grp_sel[g]) (void)hipEventDestroy(grp_sel[g]);
       if (grp_done[g]) (void)hipEventDestroy(grp_done[g]);
-      if (grp_zero[g]) (void)hipEventDestroy(grp_zero[g]);
-      if (grp_fdend[g]) (void)hipEventDestroy(grp_fdend[g]);
       grp_roll[g] = grp_fd[g] = nullptr;
-      grp_sel[g] = grp_done[g] = grp_zero[g] = grp_fdend[g] = nullptr;
+      grp_sel[g] = grp_done[g] = nullptr;
     }
     grp_sync.release();
     ngroups = 1;
@@ -975,6 +972,39 @@ static hipError_t rollout_launch(ilqg_solver* s, const SeedRange& r, RollChunk c
   }, r.st);
 }
 
+// the pipelined rollout's chunks in launch order, (lo, hi) point ranges
+// descending from P - 1 (the rollout runs n = N .. 0, inc/ilqr.h:120): C
+// points each (flat), or C halving toward the end (ILQG_PIPE_FLAT=0: a small
+// last chunk's sweep takes about one team's latency)
+static void pipe_chunks(int P, int C, bool flat, std::vector<std::pair<int, int>>& out) {
+  out.clear();
+  for (int hi = P - 1, n; hi >= 0; hi -= n) {
+    const int rem = hi + 1;
+    n = rem >= 2 * C ? C : (rem + 1) / 2;
+    if (n < 1) n = 1;
+    if (flat) n = C;
+    out.emplace_back(hi - n + 1 > 0 ? hi - n + 1 : 0, hi);
+  }
+}
+
+// Which of `world` ranks differentiates each point when one seed's FD sweep
+// is sharded behind the pipelined rollout (flat chunks of C points): chunk c
+// (launch order) goes to rank c % world, except the last kShardTail chunks --
+// the sweep the recursion waits for once the rollout ends -- whose points
+// [0, T) are dealt in contiguous blocks, rank r taking [T r / world,
+// T (r + 1) / world).  Every rank sweeps behind the rollout as the one-GPU
+// pipeline does, and the tail's latency is split world ways.
+static constexpr int kShardTail = 2;
+static void point_owners(int P, int C, int world, int* owner) {
+  std::vector<std::pair<int, int>> ch;
+  pipe_chunks(P, C, true, ch);
+  const int nch = (int)ch.size(), tail = std::min(kShardTail, nch);
+  const int T = ch[nch - tail].second + 1;
+  for (int c = 0; c < nch; c++)
+    for (int p = ch[c].first; p <= ch[c].second; p++)
+      owner[p] = c < nch - tail ? c % world : (int)((long)p * world / T);
+}
+
 // iterate() with one candidate per seed and the unfused sweep: the rollout in
 // chunks of pipe_chunk points (descending, as the rollout runs), and behind
 // each chunk, on fd_stream, the FD sweep of the points it finished -- every
@@ -983,29 +1013,38 @@ static hipError_t rollout_launch(ilqg_solver* s, const SeedRange& r, RollChunk c
 // it; then selection / setDInit and the recursion once every record is in.
 // The same launches' work as ilqg_forward + ilqg_fd_sweep + ilqg_backward:
 // the same bits (tests/test_gpu_parity.py::test_pipelined_iterate).
-static int iterate_pipelined(ilqg_solver* s) {
+//
+// Point sharding (one seed's sweep over `world` ranks, BASELINE.json
+// configs[4]): every rank runs the whole rollout and differentiates, behind
+// each chunk, only the points it owns (point_owner); the records of the other
+// points come from the other ranks (an all-gather by the caller), then
+// ilqg_backward.  `backward` false stops after selection with the solver's
+// stream behind every sweep launch.
+static int iterate_pipelined(ilqg_solver* s, int rank = 0, int world = 1, bool backward = true) {
   const ilqg_model* m = s->model;
   const SeedRange r = whole(s);
   const int P = s->P, C = s->pipe_chunk;
   int ev = 0;
-  // chunks of C points, halving toward the end (the last chunks' sweeps are
-  // what the recursion waits for: a small chunk's sweep takes about one
-  // team's latency)
-  for (int hi = P - 1, n; hi >= 0; hi -= n) {
-    const int rem = hi + 1;
-    n = rem >= 2 * C ? C : (rem + 1) / 2;
-    if (n < 1) n = 1;
-    if (s->pipe_flat) n = C;
-    const int lo = hi - n + 1 > 0 ? hi - n + 1 : 0;
+  std::vector<std::pair<int, int>> chunks;
+  pipe_chunks(P, C, s->pipe_flat, chunks);
+  std::vector<int> owner(P, 0);
+  if (world > 1) point_owners(P, C, world, owner.data());
+  for (const auto& c : chunks) {
+    const int lo = c.first, hi = c.second;
     RollChunk ch;
     ch.n_hi = hi;
     ch.n_lo = lo;
     HIPCHK(rollout_launch(s, r, ch));
+    // this rank's points of the chunk: all of them, none, or one contiguous run
+    int plo = hi + 1, phi = lo - 1;
+    for (int p = lo; p <= hi; p++)
+      if (owner[p] == rank) plo = std::min(plo, p), phi = std::max(phi, p);
+    if (plo > phi) continue;
     HIPCHK(hipEventRecord(s->pipe_ev[ev], s->stream));
     hipStream_t fs = s->fd_stream[ev % s->nfd];
     HIPCHK(hipStreamWaitEvent(fs, s->pipe_ev[ev], 0));
     ev++;
-    HIPCHK(s->timed(3, [&] { return fd_range_launch(s, lo, hi - lo + 1, fs); }, fs));
+    HIPCHK(s->timed(3, [&] { return fd_range_launch(s, plo, phi - plo + 1, fs); }, fs));
   }
   // selection + setDInit (one candidate: the rollout wrote the nominal trajectory)
   const TrajDev nom = s->tview(s->traj), di = s->tview(s->dinit);
@@ -1019,7 +1058,33 @@ static int iterate_pipelined(ilqg_solver* s) {
     HIPCHK(hipStreamWaitEvent(s->stream, s->pipe_ev[ev], 0));
     ev++;
   }
+  if (!backward) {
+    s->grp_join = true;
+    return ILQG_OK;
+  }
   return ilqg_backward(s);
+}
+
+int ilqg_forward_sharded(ilqg_solver* s, int rank, int world) {
+  if (!s || !s->initialized) return fail(ILQG_ERR_ARG, "solver not initialised");
+  if (world < 1 || rank < 0 || rank >= world) return fail(ILQG_ERR_ARG, "rank outside [0, world)");
+  if (s->pipe_chunk <= 0 || !s->pipe_flat || s->fused)
+    return fail(ILQG_ERR_UNSUPPORTED, "point sharding rides the pipelined iterate (one candidate per seed, the "
+                                      "unfused sweep: fp32 FD or the MFMA recursion, flat chunks)");
+  return iterate_pipelined(s, rank, world, false);
+}
+
+int ilqg_solver_point_owners(ilqg_solver* s, int world, int* owner) {
+  if (!s || !owner || world < 1) return fail(ILQG_ERR_ARG, "bad argument");
+  if (s->pipe_chunk <= 0 || !s->pipe_flat) return fail(ILQG_ERR_UNSUPPORTED, "no pipelined iterate on this solver");
+  point_owners(s->P, s->pipe_chunk, world, owner);
+  return ILQG_OK;
+}
+
+int ilqg_point_owners(int npoint, int chunk, int world, int* owner) {
+  if (npoint < 1 || chunk < 1 || world < 1 || !owner) return fail(ILQG_ERR_ARG, "bad argument");
+  point_owners(npoint, chunk, world, owner);
+  return ILQG_OK;
 }
 
 int ilqg_forward(ilqg_solver* s) {
@@ -1242,34 +1307,11 @@ static int iterate_groups(ilqg_solver* s) {
     if (g > 0) HIPCHK(hipStreamWaitEvent(r.st, s->grp_sel[g - 1], 0));
     HIPCHK(forward_range(s, r));
     HIPCHK(hipEventRecord(s->grp_sel[g], r.st));
-    const hipStream_t rs = r.st;
     r.st = s->grp_fd[g];
     HIPCHK(hipStreamWaitEvent(r.st, s->grp_sel[g], 0));
-    if (s->grp_mw) {
-      // the sweep alone on the sweep stream and, on the rollout stream (the
-      // group's XCD idles until its next rollout), the one-lane-per-entry
-      // recursion streaming the sweep's records as they are announced
-      HIPCHK(fused_zero(s, r));
-      HIPCHK(hipEventRecord(s->grp_zero[g], r.st));
-      HIPCHK(s->timed(3, [&] { return fused_launch(s, r, 0, false); }, r.st));
-      HIPCHK(hipEventRecord(s->grp_fdend[g], r.st));
-      HIPCHK(hipStreamWaitEvent(rs, s->grp_zero[g], 0));
-      const ilqg_model* m = s->model;
-      const HostModel& h = m->host;
-      const size_t s0 = r.s0, P = s->P, nx = s->nx;
-      HIPCHK(s->timed(4, [&] {
-        return launch_backward_mw(m->dm, r.ns, s->P, s->opts.mu, s->deriv.as<double>() + s0 * P * s->Dp, s->Dp,
-                                  toff(s->tview(s->traj), s0 * P, h), s->K.as<double>() + s0 * P * h.nu * nx,
-                                  s->k.as<double>() + s0 * P * h.nu, s->V.as<double>() + s0 * nx * nx,
-                                  s->v.as<double>() + s0 * nx, s->flags(), r.sync + 4 + (size_t)r.ns * P,
-                                  (unsigned)(1 + s->nut + 2 * h.nv), s->fault.as<unsigned>() + 2 * g, rs);
-      }, rs));
-      HIPCHK(hipStreamWaitEvent(rs, s->grp_fdend[g], 0));
-      HIPCHK(hipEventRecord(s->grp_done[g], rs));
-    } else {
-      HIPCHK(s->timed(5, [&] { return fused_launch(s, r, 1); }, r.st));
-      HIPCHK(hipEventRecord(s->grp_done[g], r.st));
-    }
+    // the sweep with the group's recursion streamed behind it: one launch
+    HIPCHK(s->timed(5, [&] { return fused_launch(s, r, 1); }, r.st));
+    HIPCHK(hipEventRecord(s->grp_done[g], r.st));
   }
   for (int g = 0; g < G; g++) HIPCHK(hipStreamWaitEvent(s->stream, s->grp_done[g], 0));
   s->vinit_pending = false;
@@ -1481,7 +1523,6 @@ int ilqg_solver_set_groups(ilqg_solver* s, int ngroups) {
   // default: the lowest mask bits (the group's rollout spread over every XCD):
   // measured ahead of a whole XCD per group (profiles/r05_seed_groups.txt)
   s->grp_xcd = getenv_int("ILQG_GROUP_XCD", 0);
-  s->grp_mw = getenv_int("ILQG_GROUP_BW", 1) != 0 && backward_mw_supported(h.nq, h.nv, h.nu);
   const bool masked = getenv_int("ILQG_GROUP_MASK", 1) != 0 && G * k < nxcd;
   s->grp_rcus = masked ? k * per : 0;
   auto rolls = [&](int g, int c) {  // CU c in group g's rollout set
@@ -1507,8 +1548,6 @@ int ilqg_solver_set_groups(ilqg_solver* s, int ngroups) {
     if (e != hipSuccess) return bail(e, "hipStreamCreate");
     e = hipEventCreateWithFlags(&s->grp_sel[g], hipEventDisableTiming);
     if (e == hipSuccess) e = hipEventCreateWithFlags(&s->grp_done[g], hipEventDisableTiming);
-    if (e == hipSuccess) e = hipEventCreateWithFlags(&s->grp_zero[g], hipEventDisableTiming);
-    if (e == hipSuccess) e = hipEventCreateWithFlags(&s->grp_fdend[g], hipEventDisableTiming);
     if (e != hipSuccess) return bail(e, "hipEventCreate");
   }
   const size_t ntm = (size_t)s->nut + 2 * (size_t)h.nv;
@@ -1523,6 +1562,12 @@ int ilqg_solver_get_groups(ilqg_solver* s, int* ngroups, int* rollout_cus) {
   if (!s || !ngroups) return fail(ILQG_ERR_ARG, "bad argument");
   *ngroups = s->ngroups;
   if (rollout_cus) *rollout_cus = s->ngroups > 1 ? s->grp_rcus : 0;
+  return ILQG_OK;
+}
+
+int ilqg_solver_join_stream(ilqg_solver* s) {
+  if (!s) return fail(ILQG_ERR_ARG, "null solver");
+  s->grp_join = true;
   return ILQG_OK;
 }
 

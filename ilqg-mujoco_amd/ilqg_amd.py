@@ -67,6 +67,8 @@ EXPORTS = [
     "ilqg_solver_set_riccati", "ilqg_selftest_div", "ilqg_solver_set_fd_precision",
     "ilqg_solver_set_mu", "ilqg_solver_get_deriv_point", "ilqg_solver_debug_plant_schedule",
     "ilqg_fd_sweep_range", "ilqg_solver_device_deriv", "ilqg_solver_set_groups", "ilqg_solver_get_groups",
+    "ilqg_solver_join_stream", "ilqg_source_sha", "ilqg_forward_sharded", "ilqg_point_owners",
+    "ilqg_solver_point_owners",
 ]
 KERNELS = ("rollout", "select", "fd_centre", "fd_cols", "backward", "fd_backward")
 
@@ -75,23 +77,26 @@ _lib = None
 
 def source_sha() -> str:
     """sha256 (16 hex digits) of the device/host sources the library is built
-    from (csrc/**, Makefile): names the kernel code a measurement belongs to
-    without git (the GPU box has no .git)"""
-    import hashlib
-    h = hashlib.sha256()
-    root = os.path.dirname(os.path.abspath(__file__))
-    files = [os.path.join(root, "Makefile")]
-    for d, _, fs in sorted(os.walk(os.path.join(root, "csrc"))):
-        files += [os.path.join(d, f) for f in sorted(fs) if f.endswith((".h", ".hip", ".cpp", ".map"))]
-    for f in files:
-        h.update(os.path.relpath(f, root).encode())
-        with open(f, "rb") as fh:
-            h.update(fh.read())
-    return h.hexdigest()[:16]
+    from (csrc/**, Makefile; srcsha.py): names the kernel code a measurement
+    belongs to without git (the GPU box has no .git)"""
+    from srcsha import source_sha as _sha
+    return _sha(_HERE)
+
+
+def library_sha(path: str = None) -> str:
+    """the source digest compiled into a built library (ilqg_source_sha)"""
+    L = ctypes.CDLL(path or LIB_PATH)
+    try:
+        f = L.ilqg_source_sha
+    except AttributeError:
+        return None
+    f.restype = ctypes.c_char_p
+    return f().decode()
 
 
 def lib() -> ctypes.CDLL:
-    """Load the HIP library (fails loudly if it was not built)."""
+    """Load the HIP library (fails loudly if it was not built, or was built
+    from other sources than the ones beside it)."""
     global _lib
     if _lib is None:
         if not os.path.exists(LIB_PATH):
@@ -106,6 +111,12 @@ def lib() -> ctypes.CDLL:
                 t.cuda.is_available()
             except Exception:
                 pass
+        # provenance: the digest compiled into the library must be the digest
+        # of the sources beside it (a stale prebuilt .so is refused, not measured)
+        built, here = library_sha(LIB_PATH), source_sha()
+        if built != here:
+            raise IlqgError(f"{LIB_PATH} was built from sources {built}, but the sources here are {here}: "
+                            "rebuild with `make -C ilqg-mujoco_amd`")
         L = ctypes.CDLL(LIB_PATH)
         L.ilqg_last_error.restype = ctypes.c_char_p
         L.ilqg_solver_stream.restype = ctypes.c_void_p
@@ -133,6 +144,16 @@ def _f64(a, shape=None) -> Optional[np.ndarray]:
     if shape is not None:
         a = a.reshape(shape)
     return a
+
+
+def point_owners(npoint: int, chunk: int, world: int) -> np.ndarray:
+    """owner rank of every trajectory point when one seed's FD sweep is sharded
+    over `world` ranks behind a pipelined rollout of `chunk`-point chunks
+    (ilqg_point_owners: host logic, no device)"""
+    out = np.zeros(npoint, dtype=np.int32)
+    _check(lib().ilqg_point_owners(int(npoint), int(chunk), int(world), out.ctypes.data_as(_c_int_p)),
+           "point_owners")
+    return out
 
 
 def device_count() -> int:
@@ -411,6 +432,19 @@ class ILQR:
         share of a point-sharded sweep): ilqg_fd_sweep_range"""
         _check(lib().ilqg_fd_sweep_range(self._h, int(p0), int(np_)), "fd_sweep_range")
 
+    def forward_sharded(self, rank: int, world: int):
+        """one rank's share of a point-sharded, pipelined iteration
+        (ilqg_forward_sharded): the whole rollout, the FD sweep of the points
+        this rank owns behind each rollout chunk (point_owners), selection;
+        the caller gathers the other records, then riccati_pass()"""
+        _check(lib().ilqg_forward_sharded(self._h, int(rank), int(world)), "forward_sharded")
+
+    def point_owners(self, world: int) -> np.ndarray:
+        """owner rank of every point under forward_sharded (ilqg_solver_point_owners)"""
+        out = np.zeros(self.P, dtype=np.int32)
+        _check(lib().ilqg_solver_point_owners(self._h, int(world), out.ctypes.data_as(_c_int_p)), "point_owners")
+        return out
+
     def device_deriv(self):
         """(device pointer, record stride in doubles) of the resident FD records [S][P][stride]"""
         p = ctypes.POINTER(ctypes.c_double)()
@@ -467,6 +501,12 @@ class ILQR:
         the next group's rollout, each on CU-masked streams; the same bits as
         the ungrouped iterate.  1 restores it."""
         _check(lib().ilqg_solver_set_groups(self._h, int(ngroups)), "set_groups")
+
+    def join_stream(self):
+        """the next iterate()'s seed groups wait for everything enqueued on the
+        solver's stream so far -- call it after work of your own there (the
+        RCCL cost all-gather) and before the next iterate()"""
+        _check(lib().ilqg_solver_join_stream(self._h), "join_stream")
 
     @property
     def groups(self) -> int:

@@ -58,8 +58,23 @@ class CostExchange:
             return self.glob
         return self.local
 
+    def _solver_after_exchange(self):
+        """the solver's next launches wait for the gather + argmin: its stream
+        waits on torch's, and seed groups (whose streams otherwise wait on the
+        solver's stream only for the solver's own work) join it, so the next
+        rollout cannot overwrite the costs while the collective still reads them"""
+        if self.solver is None or not self.local.is_cuda:
+            return
+        cur = torch.cuda.current_stream(self.local.device)
+        sst = self.solver.stream
+        if sst and sst != cur.cuda_stream:
+            torch.cuda.ExternalStream(sst, device=self.local.device).wait_stream(cur)
+        self.solver.join_stream()
+
     def __call__(self) -> torch.Tensor:
-        return torch.argmin(self.gather())
+        best = torch.argmin(self.gather())
+        self._solver_after_exchange()
+        return best
 
 
 def broadcast_winner_control(best: int, ctrl_first: torch.Tensor, seeds_per_rank: int, world: int,
@@ -90,11 +105,15 @@ def first_controls_view(solver, nu: int) -> torch.Tensor:
 # ---- point sharding of one seed's FD sweep (cfg 5: one humanoid seed on 8 GPUs)
 # The FD sweep is independent across the N+1 trajectory points
 # (src/mjderivative.cpp:212-255 runs once per point, inc/ilqr.h:153-154).  Every
-# rank runs the (serial, deterministic) rollout itself, differentiates its
-# contiguous block of points, and one all-gather of the fp64 records gives
-# every rank all of them; every rank then runs the recursion (identical inputs,
-# identical K / k: no broadcast).  Exchange per iteration: S (N+1) Dp doubles
-# (humanoid H = 200: 201 x 2112 x 8 B = 3.4 MB).
+# rank runs the (serial, deterministic) rollout itself, differentiates the
+# points it owns, and one all-gather of the fp64 records gives every rank all
+# of them; every rank then runs the recursion (identical inputs, identical
+# K / k: no broadcast).  Ownership on the GPU follows the pipelined rollout
+# (ilqg_point_owners: chunks dealt round-robin, the last chunks' points split
+# over every rank, so each rank differentiates behind the rollout); the
+# default for other callers is contiguous blocks (point_range).  Exchange per
+# iteration: world x S x max-owned x Dp doubles (humanoid H = 200, 8 ranks:
+# about 3.4 MB).
 
 def point_range(rank: int, world: int, P: int):
     """(p0, np) of the contiguous block of points `rank` differentiates: blocks
@@ -104,30 +123,48 @@ def point_range(rank: int, world: int, P: int):
     return p0, min(P, p0 + chunk) - p0
 
 
+def block_owners(world: int, P: int):
+    """owner rank of every point under point_range's contiguous blocks"""
+    import numpy as np
+    own = np.zeros(P, dtype=np.int32)
+    for r in range(world):
+        p0, n = point_range(r, world, P)
+        own[p0:p0 + n] = r
+    return own
+
+
 class RecordExchange:
-    """all-gather every rank's block of FD records so that every rank holds the
-    records of all points.
+    """all-gather every rank's FD records so that every rank holds the records
+    of all points.
 
     records: the [S, P, stride] fp64 record array (on the GPU, a zero-copy view
     of the solver's resident records, ilqg_solver_device_deriv; on CPU any
-    tensor -- the gloo tests); rank / world / group: the point-sharding group.
+    tensor -- the gloo tests); rank / world / group: the point-sharding group;
+    owner: the owner rank of every point (default: contiguous blocks).
     solver: the ILQR writing `records`; torch's stream waits on its launch
     stream before the gather, and the solver's stream waits on torch's after
     it (the recursion reads what the gather wrote)."""
 
-    def __init__(self, records: torch.Tensor, rank: int, world: int, group=None, solver=None):
+    def __init__(self, records: torch.Tensor, rank: int, world: int, group=None, solver=None, owner=None):
+        import numpy as np
         S, P, D = records.shape
         self.records, self.rank, self.world, self.group, self.solver = records, rank, world, group, solver
-        self.chunk = -(-P // world)
-        self.p0, self.np = point_range(rank, world, P)
-        self.send = torch.zeros(S, self.chunk, D, dtype=records.dtype, device=records.device)
-        self.recv = torch.empty(world, S, self.chunk, D, dtype=records.dtype, device=records.device)
+        self.owner = np.asarray(block_owners(world, P) if owner is None else owner, dtype=np.int64)
+        if self.owner.shape != (P,) or self.owner.min() < 0 or self.owner.max() >= world:
+            raise ValueError("owner: one rank in [0, world) per point")
+        self.idx = [torch.as_tensor(np.nonzero(self.owner == r)[0], device=records.device) for r in range(world)]
+        self.nown = int(self.idx[rank].numel())
+        self.nmax = max(int(i.numel()) for i in self.idx)
+        self.send = torch.zeros(S, self.nmax, D, dtype=records.dtype, device=records.device)
+        self.recv = torch.empty(world, S, self.nmax, D, dtype=records.dtype, device=records.device)
 
     @classmethod
     def for_solver(cls, solver, rank: int, world: int, group=None):
+        """the solver's resident records, owned as its pipelined sharded
+        iteration (ILQR.forward_sharded) differentiates them"""
         ptr, stride = solver.device_deriv()
         rec = device_view(ptr, solver.S * solver.P * stride).view(solver.S, solver.P, stride)
-        return cls(rec, rank, world, group, solver)
+        return cls(rec, rank, world, group, solver, owner=solver.point_owners(world))
 
     def _solver_stream(self):
         if self.solver is None or not self.records.is_cuda:
@@ -136,23 +173,49 @@ class RecordExchange:
         return torch.cuda.ExternalStream(sst, device=self.records.device) if sst else None
 
     def exchange(self):
-        """every rank's block -> every rank's `records` (rank order = point order)"""
+        """every rank's points -> every rank's `records`"""
         ext = self._solver_stream()
         cur = torch.cuda.current_stream(self.records.device) if self.records.is_cuda else None
         if ext is not None and ext.cuda_stream != cur.cuda_stream:
             cur.wait_stream(ext)
-        self.send[:, :self.np] = self.records[:, self.p0:self.p0 + self.np]
+        self.send[:, :self.nown] = self.records.index_select(1, self.idx[self.rank])
         if self.world > 1:
             dist.all_gather_into_tensor(self.recv.view(-1), self.send.view(-1), group=self.group)
         else:
             self.recv[0].copy_(self.send)
-        P = self.records.shape[1]
         for r in range(self.world):
-            p0, n = point_range(r, self.world, P)
+            n = int(self.idx[r].numel())
             if n and r != self.rank:
-                self.records[:, p0:p0 + n] = self.recv[r, :, :n]
+                self.records.index_copy_(1, self.idx[r], self.recv[r, :, :n])
         if ext is not None and ext.cuda_stream != cur.cuda_stream:
             ext.wait_stream(cur)
+
+
+def trajectory_digest(tensors) -> torch.Tensor:
+    """an exact digest of fp64 tensors (their bit patterns, summed as int64 with
+    wrap-around, weighted by position): equal trajectories give equal digests,
+    and any bit that differs changes it with overwhelming likelihood"""
+    acc = None
+    for t in tensors:
+        b = t.reshape(-1).contiguous().view(torch.int64)
+        w = torch.arange(1, b.numel() + 1, dtype=torch.int64, device=b.device) * 2 + 1
+        d = torch.stack([b.sum(), (b * w).sum()])
+        acc = d if acc is None else acc * 31 + d
+    return acc
+
+
+def check_same_trajectory(tensors, world: int, group=None):
+    """point sharding splices every rank's records into every other rank's
+    recursion, which is right only if every rank rolled out the same
+    trajectory bit for bit: all-gather the digests and raise on a mismatch"""
+    d = trajectory_digest(tensors)
+    if world > 1:
+        allg = torch.empty(world * d.numel(), dtype=d.dtype, device=d.device)
+        dist.all_gather_into_tensor(allg, d, group=group)
+        allg = allg.view(world, -1)
+        if not bool((allg == allg[0]).all()):
+            raise RuntimeError(f"point sharding: the ranks' rollouts differ (trajectory digests {allg.tolist()})")
+    return d
 
 
 def max_over_ranks(x: float, world: int, device) -> float:

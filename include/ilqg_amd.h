@@ -146,6 +146,25 @@ int ilqg_backward(ilqg_solver* s);  /* initV + Riccati n = 1..N (inc/ilqr.h:100-
    written into the buffer ilqg_solver_device_deriv exposes (an all-gather),
    ilqg_backward then runs the recursion over all of them. */
 int ilqg_fd_sweep_range(ilqg_solver* s, int p0, int np);
+/* One seed's iteration point-sharded over `world` ranks, pipelined
+   (BASELINE.json configs[4]: one humanoid seed on 8 GPUs).  Every rank runs
+   the whole rollout (forwardPass, inc/ilqr.h:116-130, in the pipelined
+   iterate's chunks) and, behind each chunk, calcMJDerivatives
+   (src/mjderivative.cpp:212-255) at the points it owns (point_owners), then
+   selection / setDInit (inc/ilqr.h:110-113); the solver's stream is left
+   behind every sweep launch.  The caller then gathers the other ranks'
+   records into ilqg_solver_device_deriv's buffer and calls ilqg_backward.
+   ILQG_ERR_UNSUPPORTED unless the solver pipelines its iterate (one candidate
+   per seed, the unfused sweep: fp32 FD or the MFMA recursion).  world = 1 is
+   ilqg_iterate without the backward pass. */
+int ilqg_forward_sharded(ilqg_solver* s, int rank, int world);
+/* owner[p] (p = 0 .. npoint-1, 0 = terminal) = the rank that differentiates
+   point p under ilqg_forward_sharded: the pipelined rollout's chunks of
+   `chunk` points (launch order: descending from npoint - 1) dealt round-robin,
+   the last two chunks' points in contiguous blocks over every rank.  Pure host
+   logic (no device).  solver_point_owners: the same for a solver's chunking. */
+int ilqg_point_owners(int npoint, int chunk, int world, int* owner);
+int ilqg_solver_point_owners(ilqg_solver* s, int world, int* owner);
 int ilqg_iterate(ilqg_solver* s);   /* forwardPass; setDInit(dArray[N]); backwardPass (inc/ilqr.h:179-186) */
 /* waits for every launch; returns ILQG_ERR_HIP once if a fused sweep's
    hand-off wait timed out since the last call (the report is cleared by it) */
@@ -226,8 +245,9 @@ int ilqg_solver_set_fd_precision(ilqg_solver* s, int prec);
    for bit); only the overlap between independent seeds changes.  Work enqueued
    on the solver's stream after ilqg_iterate waits for every group; the groups
    wait for work on that stream only when it came through this API (ilqg_forward,
-   ilqg_fd_sweep, ilqg_backward, set_stream, ...) -- synchronise work of your
-   own before the next ilqg_iterate.  The seeds of MahanFathi/iLQG-MuJoCo's
+   ilqg_fd_sweep, ilqg_backward, set_stream, join_stream ...) -- work of your
+   own enqueued there (a collective reading the costs) must be followed by
+   ilqg_solver_join_stream before the next ilqg_iterate.  The seeds of MahanFathi/iLQG-MuJoCo's
    driver are independent (one ILQR per MPC problem, inc/ilqr.h:52-71), so
    the reference has no counterpart call.  ILQG_ERR_UNSUPPORTED unless the fused
    sweep is in use (fp64 FD, exact recursion, cooperative model); 1 restores
@@ -235,6 +255,15 @@ int ilqg_solver_set_fd_precision(ilqg_solver* s, int prec);
    rollout mask (0: unmasked). */
 int ilqg_solver_set_groups(ilqg_solver* s, int ngroups);
 int ilqg_solver_get_groups(ilqg_solver* s, int* ngroups, int* rollout_cus);
+/* the next ilqg_iterate's seed groups wait for everything enqueued on the
+   solver's stream up to now (work of the caller's own, e.g. the RCCL cost
+   all-gather, which reads the buffers the next rollout writes); without
+   groups every launch is on that stream anyway and this is a no-op */
+int ilqg_solver_join_stream(ilqg_solver* s);
+/* sha256 prefix (16 hex digits) of the sources this library was built from
+   (csrc/**, Makefile; the same digest as ilqg_amd.source_sha()): the host
+   refuses a library whose digest differs from the sources beside it */
+const char* ilqg_source_sha(void);
 /* device pointer to the per-seed selected-candidate cost (nseed doubles), for
    an in-stream collective (RCCL all-gather) without a host round trip */
 int ilqg_solver_device_costs(ilqg_solver* s, double** dptr);

@@ -61,6 +61,31 @@ def test_device_entry_points_fail_without_gpu(ia):
         ia.ILQR(m, st, 10, ia.PENDULUM_COST)
 
 
+def test_library_carries_source_digest(ia):
+    """binary provenance: the library in the tree was built from the sources
+    beside it (the digest compiled in equals srcsha.py's of csrc/** + Makefile)"""
+    lib = ia.lib()
+    lib.ilqg_source_sha.restype = ctypes.c_char_p
+    assert lib.ilqg_source_sha().decode() == ia.source_sha()
+    assert re.fullmatch(r"[0-9a-f]{16}", ia.source_sha())
+
+
+def test_stale_library_is_refused(tmp_path):
+    """a library whose compiled-in digest differs from the sources (a stale
+    prebuilt .so pushed beside newer sources) is refused with IlqgError before
+    anything runs on it"""
+    src = tmp_path / "stale.c"
+    src.write_text('const char* ilqg_source_sha(void) { return "0123456789abcdef"; }\n'
+                   'int ilqg_version(void) { return 999; }\n')
+    so = tmp_path / "libstale.so"
+    subprocess.run(["gcc", "-shared", "-fPIC", "-o", str(so), str(src)], check=True)
+    code = ("import sys; sys.path.insert(0, %r); import ilqg_amd as ia\n"
+            "try:\n    ia.lib()\nexcept ia.IlqgError as e:\n    print('REFUSED', e)\nelse:\n    print('LOADED')\n") % PKG
+    r = subprocess.run(["python3", "-c", code], env=dict(os.environ, ILQG_LIB=str(so)), capture_output=True,
+                       text=True, timeout=120)
+    assert "REFUSED" in r.stdout and "0123456789abcdef" in r.stdout, r.stdout + r.stderr
+
+
 def test_model_sizes_and_blob(ia):
     m = ia.Model.load(model_path("hopper"))
     b = m.blob()

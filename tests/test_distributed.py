@@ -206,12 +206,15 @@ def test_winner_broadcast_on_subgroup_gloo(tmp_path):
 
 
 # ---- point sharding of one seed's FD sweep (cfg 5's single humanoid seed on
-# N GPUs): every rank rolls out the same trajectory, differentiates its block
-# of points, all-gathers the records (RecordExchange) and runs the recursion.
+# N GPUs): every rank rolls out the same trajectory, differentiates the points
+# it owns, all-gathers the records (RecordExchange) and runs the recursion.
 # The FD engine here is the oracle (the product has no CPU path); the host
-# logic -- point blocks, the gather into every rank's record array, the
+# logic -- the ownership map the GPU's pipelined sharded iterate uses
+# (ilqg_point_owners: rollout chunks dealt round-robin, the last two chunks'
+# points in contiguous blocks), the gather into every rank's record array, the
 # recursion over the gathered records -- is the one the GPU run uses.
-H_PT = 4  # 5 points: blocks of 3 + 2 (world 2) and 2 + 2 + 1 (world 3)
+H_PT = 4  # 5 points; chunks of 1: owners [0,1,0,1,0] (world 2), [0,1,2,1,0] (world 3)
+PT_CHUNK = 1
 
 
 def _humanoid_oracle():
@@ -244,20 +247,22 @@ def _worker_points(rank, world, port, outdir):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
-        from seed_shard import RecordExchange, point_range
+        from seed_shard import RecordExchange
         ora, om, il = _humanoid_oracle()
+        import ilqg_amd as ia
         P = H_PT + 1
         D = om.D
         stride = D + 3  # padded records, as the solver's [S][P][Dp]
         rec = torch.full((1, P, stride), float("nan"), dtype=torch.float64)
-        p0, n = point_range(rank, world, P)
-        for p in range(p0, p0 + n):
+        owner = ia.point_owners(P, PT_CHUNK, world)
+        mine = [p for p in range(P) if owner[p] == rank]
+        for p in mine:
             rec[0, p, :D] = torch.from_numpy(ora.calc_derivatives(om, il_state(om, il, p), "ora_cost_desc_fn"))
-        RecordExchange(rec, rank, world).exchange()
+        RecordExchange(rec, rank, world, owner=owner).exchange()
         il.backward_from_records(rec[0, :, :D].numpy())
         a = il.arrays()
         np.savez(os.path.join(outdir, f"p{rank}.npz"), rec=rec[0, :, :D].numpy().copy(), K=a["K"], k=a["k"],
-                 V=a["V"], v=a["v"], p0=p0, n=n)
+                 V=a["V"], v=a["v"], mine=np.array(mine, dtype=np.int64))
     finally:
         dist.destroy_process_group()
 
@@ -265,19 +270,52 @@ def _worker_points(rank, world, port, outdir):
 @pytest.mark.parametrize("world", [2, 3])
 def test_point_sharded_fd_gloo(tmp_path, world):
     """one humanoid seed (cfg 5), H = 4, its FD sweep point-sharded over
-    `world` gloo ranks: every rank ends with the 1-rank records, K, k, V, v
-    bit for bit, and the blocks tile the trajectory"""
+    `world` gloo ranks with the GPU path's interleaved ownership: every rank
+    ends with the 1-rank records, K, k, V, v bit for bit, and the owned point
+    sets partition the trajectory"""
     mp.spawn(_worker_points, args=(world, _free_port(), str(tmp_path)), nprocs=world, join=True)
     ora, om, il = _humanoid_oracle()
     il.backward_pass()
     ref = il.arrays()
     r = [np.load(tmp_path / f"p{i}.npz") for i in range(world)]
-    assert [int(x["p0"]) for x in r] == sorted(int(x["p0"]) for x in r)
-    assert sum(int(x["n"]) for x in r) == H_PT + 1
+    owned = sorted(int(p) for x in r for p in x["mine"])
+    assert owned == list(range(H_PT + 1))
+    assert any(np.any(np.diff(x["mine"]) > 1) for x in r)  # interleaved, not blocks
     for x in r:
         assert np.array_equal(x["rec"], ref["deriv"])
         for key in ("K", "k", "V", "v"):
             assert np.array_equal(x[key], ref[key]), key
+
+
+def test_point_owners_follow_the_pipeline():
+    """ilqg_point_owners (the map ilqg_forward_sharded differentiates by):
+    every rollout chunk but the last two belongs wholly to rank c % world (so
+    every rank sweeps behind the rollout), the last two chunks' points are
+    split in contiguous blocks over every rank, world 1 owns everything; at
+    cfg 5's size (P = 201, chunks of 10) over 8 ranks"""
+    sys.path.insert(0, os.path.join(ROOT, "ilqg-mujoco_amd"))
+    import ilqg_amd as ia
+    for P, C in ((201, 10), (5, 1), (5, 2), (501, 10), (10, 10), (1, 1)):
+        chunks = []
+        hi = P - 1
+        while hi >= 0:
+            chunks.append((max(hi - C + 1, 0), hi))
+            hi -= C
+        for world in (1, 2, 3, 8):
+            own = ia.point_owners(P, C, world)
+            assert own.shape == (P,) and own.min() >= 0 and own.max() < world
+            if world == 1:
+                assert not own.any()
+                continue
+            tail = min(2, len(chunks))
+            for c, (lo, hi) in enumerate(chunks[:len(chunks) - tail]):
+                assert (own[lo:hi + 1] == c % world).all(), (P, C, world, c)
+            T = chunks[len(chunks) - tail][1] + 1
+            assert (np.diff(own[:T]) >= 0).all()  # contiguous blocks, ascending ranks
+            if T >= world:
+                assert set(own[:T].tolist()) == set(range(world))
+    own = ia.point_owners(201, 10, 8)
+    assert np.bincount(own[:11], minlength=8).max() <= 2  # the tail, 11 points over 8 ranks
 
 
 def test_point_range_tiles():

@@ -541,6 +541,54 @@ def test_fd_sweep_range_blocks(ia, ora, name, prec):
     exact(k, k_full, "k")
 
 
+@pytest.mark.parametrize("world", [3, 8])
+def test_forward_sharded_interleaved(ia, ora, world, monkeypatch):
+    """ilqg_forward_sharded (cfg 5 on N GPUs, one rank's share of the
+    pipelined, point-sharded iteration), every rank played in turn on one GPU:
+    rank r's call writes exactly the records of the points point_owners gives
+    it (the others stay as they were: NaN here), all ranks together write the
+    whole pipelined sweep's records, and the recursion over them gives the
+    unsharded iteration's gains -- over two iterations (humanoid, fp32 FD,
+    MFMA recursion, chunks of 5 points over H = 40: interleaved ownership)"""
+    import workloads
+    import torch
+    from seed_shard import RecordExchange
+    assert torch.cuda.is_available()  # torch's HIP runtime first (ilqg_amd.lib)
+    monkeypatch.setenv("ILQG_PIPE_CHUNK", "5")
+    m = ia.Model.load(workloads.model_file("humanoid"))
+    dmain, H = m.reset_state(1), 40
+    dmain.qpos[0, 2] = 1.4
+    P = H + 1
+    solvers = []
+    for _ in range(2):
+        g = ia.ILQR(m, dmain, H, ia.HUMANOID_COST)
+        g.set_fd_precision("f32")
+        g.set_riccati("mfma")
+        solvers.append(g)
+    ref, sh = solvers
+    owner = sh.point_owners(world)
+    assert np.array_equal(owner, ia.point_owners(P, 5, world))
+    assert any(np.any(np.diff(np.nonzero(owner == r)[0]) > 1) for r in range(world))  # interleaved
+    for it in range(2):
+        ref.iterate()
+        ref.synchronize()
+        D_ref = ref.deriv()
+        sh.set_deriv(np.full_like(D_ref, np.nan))
+        for r in range(world):
+            sh.forward_sharded(r, world)
+            sh.synchronize()
+            D = sh.deriv().reshape(P, -1)
+            done = np.isin(owner, np.arange(r + 1))
+            exact(D[done], D_ref.reshape(P, -1)[done], f"iteration {it}: ranks 0..{r}'s points")
+            assert np.isnan(D[~done]).all(), f"iteration {it}: rank {r} wrote points it does not own"
+        RecordExchange.for_solver(sh, 0, 1).exchange()  # one rank holds them all: a no-op gather
+        sh.riccati_pass()
+        sh.synchronize()
+        exact(sh.traj().qpos, ref.traj().qpos, f"iteration {it}: trajectory")
+        for a, b, what in zip(sh.gains(), ref.gains(), ("K", "k")):
+            exact(a, b, f"iteration {it}: {what}")
+
+
 @pytest.mark.parametrize("name,prec,chunk", [("humanoid", "f32", 7), ("humanoid", "f64", 5), ("hopper", "f64", 16)])
 def test_pipelined_iterate(ia, ora, name, prec, chunk, monkeypatch):
     """ilqg_iterate with one candidate per seed and the unfused sweep rolls out
@@ -581,7 +629,7 @@ def test_pipelined_iterate(ia, ora, name, prec, chunk, monkeypatch):
             exact(out[chunk][0][s * P:(s + 1) * P], il.traj()["qpos"], f"seed {s} qpos vs oracle")
 
 
-@pytest.mark.parametrize("G", [2, 3])
+@pytest.mark.parametrize("G", [2, 3, 4])
 def test_seed_groups_bitexact(ia, ora, G):
     """ilqg_solver_set_groups: iterate() software-pipelines the seeds as G
     ranges (per group: rollout + selection on an XCD-masked stream, the fused
@@ -613,6 +661,42 @@ def test_seed_groups_bitexact(ia, ora, G):
         out[grp] = (t.qpos, t.qvel, t.ctrl, g.deriv(), *g.gains(), *g.value(), *g.costs())
     for a, b, what in zip(out[1], out[G], ("qpos", "qvel", "ctrl", "deriv", "K", "k", "V", "v", "costs", "sel")):
         exact(b, a, what)
+
+
+@pytest.mark.parametrize("G", [2, 4])
+def test_seed_groups_cost_exchange(ia, ora, G):
+    """The bench's loop with seed groups: iterate(), then the cost exchange
+    (CostExchange: argmin over the device costs on torch's stream, which is the
+    solver's) and a torch copy of the selected costs, every iteration, with no
+    host synchronisation in between.  The exchange joins the groups
+    (ilqg_solver_join_stream), so no group's next rollout/selection overwrites
+    the costs while torch still reads them: every iteration's copy and best
+    seed equal the ungrouped run's (G = 4 over 4 seeds: one seed a group)."""
+    import torch
+    import workloads
+    from seed_shard import CostExchange, device_view
+    m, _ = setup(ia, ora, "hopper", ia.HOPPER_COST)
+    S, H = 4, 60
+    dmain = workloads.hopper_dmain(m, S, sigma=0.01)
+    out = {}
+    for grp in (1, G):
+        g = ia.ILQR(m, dmain, H, ia.HOPPER_COST, alphas=workloads.LINESEARCH_ALPHAS[:4], select="min_cost")
+        stream = torch.cuda.Stream()
+        g.set_stream(stream.cuda_stream)
+        g.set_groups(grp)
+        ex = CostExchange(device_view(g.device_costs_ptr(), S), 1, solver=g)
+        seen, best = [], []
+        with torch.cuda.stream(stream):
+            for _ in range(5):
+                g.iterate()
+                best.append(ex())
+                seen.append(ex.local.clone())
+        torch.cuda.synchronize()
+        g.synchronize()
+        out[grp] = (torch.stack(seen).cpu().numpy(), torch.stack(best).cpu().numpy())
+        g.set_groups(1)
+    exact(out[G][0], out[1][0], "selected costs read by torch after every iterate")
+    exact(out[G][1], out[1][1], "best seed per iterate")
 
 
 def test_bench_workload_bitexact(ia, ora):
