@@ -20,6 +20,21 @@ using namespace coopf;
 constexpr int TEAM32 = TEAM_SIZE;
 constexpr int FD32_NITER = 30;   // mjderivative.cpp:37
 constexpr int FD32_NWARMUP = 3;  // mjderivative.cpp:38
+// The physics pipeline inlined at every call site of these kernels.  Left to
+// the inliner's size heuristic, forward_skip stayed an outlined call, and a
+// call takes the model (MT, a ~1 KB struct of sizes and pointers) and the
+// layouts by reference: the kernel copied them into scratch memory (1,040 B a
+// lane) and every model field the physics read was a load from it.  Inlined,
+// the fields are kernel arguments again (0 scratch; VGPRs 248 -> 139 in
+// k_fd_cols32<DevModelNV<27>>).  ILQG_FD32_INL=0 restores the call (A/B).
+#ifndef ILQG_FD32_INL
+#define ILQG_FD32_INL 1
+#endif
+#if ILQG_FD32_INL
+#define FD32_INL [[clang::always_inline]]
+#else
+#define FD32_INL
+#endif
 
 // LDS: [workspace floats][coop floats][workspace ints][coop ints]; the model
 // image is read from global memory
@@ -85,8 +100,9 @@ __global__ __launch_bounds__(TEAM32) void k_fd_centre32(DevModel mg, WsLayout L,
   Team T = make_team32(L, C);
   const int pt = blockIdx.x;
   load_state32(m, L, T, tr, pt, pt / P, qfrc_applied, xfrc_applied);
-  forward_skip(m, L, C, X, T, STAGE_NONE, FD32_NITER, 0.0);
-  for (int rep = 1; rep < FD32_NWARMUP; rep++) forward_skip(m, L, C, X, T, STAGE_VEL, FD32_NITER, 0.0);
+  // every physics call inlined (FD32_INL): see k_fd_cols32
+  FD32_INL forward_skip(m, L, C, X, T, STAGE_NONE, FD32_NITER, 0.0);
+  for (int rep = 1; rep < FD32_NWARMUP; rep++) FD32_INL forward_skip(m, L, C, X, T, STAGE_VEL, FD32_NITER, 0.0);
   FOR_T(i, m.nv) warm_c[(size_t)pt * m.nv + i] = T.w[L.warm + i];
   // the centre cost on the fp32 state, as the perturbed costs below see it
   if (T.tid == 0) cost_c[pt] = step_cost32(m, cost, T.w + L.qpos, T.w + L.qvel, T.w + L.ctrl);
@@ -154,7 +170,7 @@ __global__ __launch_bounds__(TEAM32) void k_fd_cols32(DevModel mg, WsLayout L, c
   }
   FOR_T(j, nv) warm[j] = (float)wc[j];
   TSYNC();
-  forward_skip(m, L, C, X, T, STAGE_NONE, FD32_NITER, 0.0);
+  FD32_INL forward_skip(m, L, C, X, T, STAGE_NONE, FD32_NITER, 0.0);
   FOR_T(j, nv) temp[j] = qacc[j];
   // qpos undo before the minus side (mjderivative.cpp:184): the fp32 centre state
   if (kind == 2) FOR_T(k, m.nq) qpos[k] = (float)tr.qpos[(size_t)pt * m.nq + k];
@@ -165,7 +181,7 @@ __global__ __launch_bounds__(TEAM32) void k_fd_cols32(DevModel mg, WsLayout L, c
   }
   FOR_T(j, nv) warm[j] = (float)wc[j];
   TSYNC();
-  forward_skip(m, L, C, X, T, skip_minus, FD32_NITER, 0.0);
+  FD32_INL forward_skip(m, L, C, X, T, skip_minus, FD32_NITER, 0.0);
   FOR_T(j, nv) {
     const float v = (temp[j] - qacc[j]) / (2 * eps);
     if (kind == 0) dr[2 * nv * nv + i + j * nu] = v;

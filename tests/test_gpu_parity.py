@@ -544,49 +544,53 @@ def test_fd_sweep_range_blocks(ia, ora, name, prec):
 @pytest.mark.parametrize("world", [3, 8])
 def test_forward_sharded_interleaved(ia, ora, world, monkeypatch):
     """ilqg_forward_sharded (cfg 5 on N GPUs, one rank's share of the
-    pipelined, point-sharded iteration), every rank played in turn on one GPU:
-    rank r's call writes exactly the records of the points point_owners gives
-    it (the others stay as they were: NaN here), all ranks together write the
-    whole pipelined sweep's records, and the recursion over them gives the
-    unsharded iteration's gains -- over two iterations (humanoid, fp32 FD,
-    MFMA recursion, chunks of 5 points over H = 40: interleaved ownership)"""
+    pipelined, point-sharded iteration), `world` ranks played by `world`
+    solvers on one GPU: rank r's call writes exactly the records of the points
+    point_owners gives it (the others stay as they were: NaN here), every rank
+    rolls out the same trajectory, the owned records together are the
+    unsharded pipelined sweep's, and the recursion over the gathered records
+    gives the unsharded iteration's gains on every rank -- over two iterations
+    (humanoid, fp32 FD, MFMA recursion, chunks of 5 points over H = 40:
+    interleaved ownership)"""
     import workloads
     import torch
-    from seed_shard import RecordExchange
     assert torch.cuda.is_available()  # torch's HIP runtime first (ilqg_amd.lib)
     monkeypatch.setenv("ILQG_PIPE_CHUNK", "5")
     m = ia.Model.load(workloads.model_file("humanoid"))
     dmain, H = m.reset_state(1), 40
     dmain.qpos[0, 2] = 1.4
     P = H + 1
-    solvers = []
-    for _ in range(2):
+
+    def solver():
         g = ia.ILQR(m, dmain, H, ia.HUMANOID_COST)
         g.set_fd_precision("f32")
         g.set_riccati("mfma")
-        solvers.append(g)
-    ref, sh = solvers
-    owner = sh.point_owners(world)
+        return g
+    ref, ranks = solver(), [solver() for _ in range(world)]
+    owner = ranks[0].point_owners(world)
     assert np.array_equal(owner, ia.point_owners(P, 5, world))
     assert any(np.any(np.diff(np.nonzero(owner == r)[0]) > 1) for r in range(world))  # interleaved
     for it in range(2):
         ref.iterate()
         ref.synchronize()
-        D_ref = ref.deriv()
-        sh.set_deriv(np.full_like(D_ref, np.nan))
-        for r in range(world):
-            sh.forward_sharded(r, world)
-            sh.synchronize()
-            D = sh.deriv().reshape(P, -1)
-            done = np.isin(owner, np.arange(r + 1))
-            exact(D[done], D_ref.reshape(P, -1)[done], f"iteration {it}: ranks 0..{r}'s points")
-            assert np.isnan(D[~done]).all(), f"iteration {it}: rank {r} wrote points it does not own"
-        RecordExchange.for_solver(sh, 0, 1).exchange()  # one rank holds them all: a no-op gather
-        sh.riccati_pass()
-        sh.synchronize()
-        exact(sh.traj().qpos, ref.traj().qpos, f"iteration {it}: trajectory")
-        for a, b, what in zip(sh.gains(), ref.gains(), ("K", "k")):
-            exact(a, b, f"iteration {it}: {what}")
+        D_ref = ref.deriv().reshape(P, -1)
+        gathered = np.full_like(D_ref, np.nan)
+        for r, g in enumerate(ranks):
+            g.set_deriv(np.full_like(D_ref, np.nan))
+            g.forward_sharded(r, world)
+            g.synchronize()
+            D = g.deriv().reshape(P, -1)
+            mine = owner == r
+            exact(D[mine], D_ref[mine], f"iteration {it}: rank {r}'s points")
+            assert np.isnan(D[~mine]).all(), f"iteration {it}: rank {r} wrote points it does not own"
+            exact(g.traj().qpos, ref.traj().qpos, f"iteration {it}: rank {r}'s trajectory")
+            gathered[mine] = D[mine]
+        for r, g in enumerate(ranks):
+            g.set_deriv(gathered)  # the all-gather's result on every rank
+            g.riccati_pass()
+            g.synchronize()
+            for a, b, what in zip(g.gains(), ref.gains(), ("K", "k")):
+                exact(a, b, f"iteration {it}: rank {r}'s {what}")
 
 
 @pytest.mark.parametrize("name,prec,chunk", [("humanoid", "f32", 7), ("humanoid", "f64", 5), ("hopper", "f64", 16)])

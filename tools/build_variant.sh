@@ -3,6 +3,8 @@
 # -D flags, linked with the standard objects (A/B runs via ILQG_LIB=...).
 #   tools/build_variant.sh NAME TU(kernels_rollout|kernels_fd|riccati) "-DFLAG=0 ..."
 set -e
+# (run `make -C ilqg-mujoco_amd` first: a variant carries the sources' digest, build/srcsha.o,
+# which ilqg_amd.lib() checks)
 cd "$(dirname "$0")/../ilqg-mujoco_amd"
 name=$1; tu=$2; defs=$3
 ROCM=/opt/rocm
@@ -14,5 +16,5 @@ for o in kernels_fd kernels_fd32 kernels_rollout riccati; do
   if [ "$o" = "$tu" ]; then objs="$objs build/var/${tu}_$name.o"; else objs="$objs build/$o.o"; fi
 done
 $ROCM/bin/hipcc $FLAGS -shared -Wl,--version-script=csrc/exports.map -Wl,-Bsymbolic -o lib/libilqg_amd_$name.so \
-  $objs build/capi.o build/mjcf.o build/setconst.o
+  $objs build/capi.o build/mjcf.o build/setconst.o build/srcsha.o
 echo "built lib/libilqg_amd_$name.so"

@@ -11,7 +11,7 @@
 #   bench                default bench line (with the CPU baseline)
 #   ab=NAME[,ENV=V...]   REPS (default 3) bench lines, 20 steps, no CPU leg;
 #                        ENV=V pairs may include ILQG_LIB=...
-#   cfg5[=ENV=V,...]     REPS cfg-5 humanoid bench lines
+#   cfg5[=NAME,ENV=V...] REPS cfg-5 humanoid bench lines (ENV may include ILQG_LIB=...)
 #   prof                 rocprofv3 kernel-trace stats + FETCH/WRITE PMC passes
 #   stamps[=MODEL]       stage stamps on the diagnostic build
 #   timeline             fused-sweep timeline on the diagnostic build
@@ -56,11 +56,11 @@ for step in "$@"; do
       summ $f "$name#$r"
     done ;;
   cfg5)
-    envs=${arg//,/ }
+    name=${arg%%,*}; name=${name:-default}; envs=""; [[ $arg == *,* ]] && envs=${arg#*,}; envs=${envs//,/ }
     for r in $(seq 1 $REPS); do
-      f=$OUT/cfg5_$r.json
-      timeout -k 10 400 env $envs python bench.py --workload humanoid_cfg5 --no-cpu-baseline --steps 3 > $f 2> $f.err || fail cfg5 $f.err
-      summ $f "cfg5#$r"
+      f=$OUT/cfg5_${name}_$r.json
+      timeout -k 10 400 env $envs python bench.py --workload humanoid_cfg5 --no-cpu-baseline --steps 5 > $f 2> $f.err || fail cfg5 $f.err
+      summ $f "cfg5 $name#$r"
     done ;;
   prof)
     timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/trace -o run -- $PCMD \
