@@ -37,6 +37,12 @@
 
 /* line-search constants of the restated Newton solver */
 #define ORA_LS_ITER 50
+#ifdef ORA_LS_STUDY /* tools/ls_study (a study build; liboracle.so never defines it) */
+void ora_ls_study_begin(int ne, const double* Jv, const double* jar, const double* D, double g1, double g2,
+                        double d1, double d2, double gtol);
+void ora_ls_study_iter(int it, int bisect, double lo, double hi, double alpha, double d1, double d2);
+void ora_ls_study_end(void);
+#endif
 #define ORA_LS_TOL 0.01
 
 /* ------------------------------------------------------------------------- */
@@ -1277,14 +1283,25 @@ static mjtNum linesearch(const mjModel* m, mjData* d, const mjtNum* search, cons
   LS_EVAL(0.0);
   if (d1 >= 0) return 0;
   gtol = ORA_LS_TOL * fabs(d1);
+#ifdef ORA_LS_STUDY /* tools/ls_study: the line search's iterations, observed (never in liboracle.so) */
+  ora_ls_study_begin(ne, Jv, jar, d->efc_D, g1, g2, d1, d2, gtol);
+#endif
   for (int it = 0; it < ORA_LS_ITER; it++) {
     mjtNum anew = alpha - d1 / d2;
-    if (hi >= 0 && !(anew > lo && anew < hi)) anew = 0.5 * (lo + hi);
+    int bis = 0;
+    if (hi >= 0 && !(anew > lo && anew < hi)) anew = 0.5 * (lo + hi), bis = 1;
     alpha = anew;
     LS_EVAL(alpha);
+#ifdef ORA_LS_STUDY
+    ora_ls_study_iter(it, bis, lo, hi, alpha, d1, d2);
+#endif
+    (void)bis;
     if (fabs(d1) < gtol) break;
     if (d1 < 0) lo = alpha; else hi = alpha;
   }
+#ifdef ORA_LS_STUDY
+  ora_ls_study_end();
+#endif
 #undef LS_EVAL
   return alpha;
 }
