@@ -449,6 +449,12 @@ bool SolverCore::deriv_current(int n, const mjData* d) const {
          !memcmp(d->ctrl, &I.ctrl[(size_t)n * I.nu], sizeof(mjtNum) * I.nu);
 }
 
+bool SolverCore::traj_current(mjData* const* dArray) const {
+  for (int n = 0; n < p_->P; n++)
+    if (!deriv_current(n, dArray[n])) return false;
+  return true;
+}
+
 void SolverCore::riccati(mjtNum mu, mjtNum* K, mjtNum* k, mjtNum* V, mjtNum* v) {
   Impl& I = *p_;
   check(ilqg_solver_set_mu(I.s, mu), "ILQR mu");

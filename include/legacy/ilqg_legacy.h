@@ -84,6 +84,8 @@ class SolverCore {
   // whether the last sweep's record of point n is the linearisation at d's
   // current state (dArray[n] unchanged since the sweep)
   bool deriv_current(int n, const mjData* d) const;
+  // deriv_current at every point: dArray unchanged since the last sweep
+  bool traj_current(mjData* const* dArray) const;
 
  private:
   void push_traj(mjData* const* dArray);

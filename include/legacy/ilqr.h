@@ -15,7 +15,9 @@
 // default, or whatever an override sets) seed the device recursion
 // (ilqg_solver_set_value).  backwardPass runs the FD sweep over every point
 // first (the sweep does not depend on V), so the default initV reads the
-// terminal record the sweep already formed instead of launching its own FD.
+// terminal record the sweep already formed instead of launching its own FD;
+// if an override changes any dArray[n] the sweep is run again, as the
+// reference would differentiate the changed state.
 //
 // Unlike the reference, every ILQR instance owns its own state (the
 // reference's function-static references in backwardPass, inc/ilqr.h:137-140,
@@ -138,6 +140,10 @@ class ILQR {
   void backwardPass() {
     core_.sweep(dArray);
     initV();
+    // the reference differentiates dArray[n] inside its loop, after initV
+    // (inc/ilqr.h:142-154): an initV override that changed any point since the
+    // sweep gets those points differentiated again at their new state
+    if (!core_.traj_current(dArray)) core_.sweep(dArray);
     core_.riccati(mu, K[0].data(), k[0].data(), V->data(), v->data());
     differentiator->setMJData(dArray[N]);
     mju_copy(differentiator->deriv, core_.deriv(N), Differentiator<nv, nu>::kD);

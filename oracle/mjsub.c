@@ -43,6 +43,9 @@ void ora_ls_study_begin(int ne, const double* Jv, const double* jar, const doubl
 void ora_ls_study_iter(int it, int bisect, double lo, double hi, double alpha, double d1, double d2);
 void ora_ls_study_end(void);
 #endif
+#ifdef ORA_NT_STUDY
+void ora_nt_study_iter(int ne, const double* jar, const double* Jv, double alpha, const int* state);
+#endif
 #define ORA_LS_TOL 0.01
 
 /* ------------------------------------------------------------------------- */
@@ -1329,6 +1332,9 @@ static void solver_newton(const mjModel* m, mjData* d, int maxiter, mjtNum tol) 
     chol_solve(nv, H, grad, search);
     for (int j = 0; j < nv; j++) search[j] = -search[j];
     alpha = linesearch(m, d, search, Ma, jar, Mv, Jv);
+#ifdef ORA_NT_STUDY /* tools/ls_study: would the active set at alpha = 1 predict the next factor's? */
+    ora_nt_study_iter(ne, jar, Jv, alpha, d->efc_state);
+#endif
     if (alpha == 0) break;
     for (int j = 0; j < nv; j++) d->qacc[j] += alpha * search[j];
     for (int j = 0; j < nv; j++) Ma[j] += alpha * Mv[j];

@@ -316,6 +316,15 @@ class OILQR:
                         ("k", _dp), ("mu", ctypes.c_double)]
         ctypes.cast(self.s, ctypes.POINTER(S)).contents.mu = float(mu)
 
+    def point(self, n: int) -> "OData":
+        """dArray[n] (the oracle's own mjData, not a copy: writes change the trajectory)"""
+        class S(ctypes.Structure):
+            _fields_ = [("m", ctypes.c_void_p), ("N", ctypes.c_int), ("nv", ctypes.c_int), ("nu", ctypes.c_int),
+                        ("nx", ctypes.c_int), ("D", ctypes.c_int), ("d", ctypes.c_void_p),
+                        ("dArray", ctypes.POINTER(ctypes.c_void_p))]
+        st = ctypes.cast(self.s, ctypes.POINTER(S)).contents
+        return OData(self.model, handle=st.dArray[n])
+
     def backward_from_records(self, deriv):
         """backwardPass (initV + the recursion, inc/ilqr.h:100-107,133-176) over
         the given FD records (P x D) instead of the oracle's own sweep"""

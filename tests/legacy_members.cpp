@@ -10,6 +10,8 @@
 //                                      prints K, k, V, v and the trajectory as hex
 //   legacy_members model.xml mu X N    N iterate() of a plain ILQR whose public mu
 //                                      was set to X first (inc/ilqr.h:65,166); same output
+//   legacy_members model.xml mutate    one iterate() of a subclass whose initV changes
+//                                      dArray[N/2] after the default; same output
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -44,6 +46,20 @@ class FixedTerminal : public ILQR<nv, nu, N> {
       (*this->v)(0, j) = j - 1.5;
       for (int i = 0; i < 2 * nv; i++) (*this->V)(i, j) = (i == j ? 0.5 * (i + 1) : 0.0) + 0.125 * (i + j);
     }
+  }
+};
+
+// the default terminal value, then a later point changed (qvel[0] of
+// dArray[N / 2] += 1e-3): the recursion must differentiate that point at its
+// new state, as the reference's loop would (inc/ilqr.h:142-154)
+template <int nv, int nu, int N>
+class MutatingTerminal : public ILQR<nv, nu, N> {
+ public:
+  using Base = ILQR<nv, nu, N>;
+  MutatingTerminal(mjModel* m, mjData* d, stepCostFn_t& fn) : Base(m, d, fn) {}
+  void initV() override {
+    Base::initV();
+    this->dArray[N / 2]->qvel[0] += 1e-3;
   }
 };
 
@@ -166,6 +182,15 @@ int initv(mjModel* m, mjData* d0, int iters) {
   return 0;
 }
 
+int mutate(mjModel* m, mjData* d0) {
+  stepCostFn_t fn = stepCost;
+  MutatingTerminal<kNv, kNu, kN> il(m, d0, fn);
+  il.setDInit(d0);
+  il.iterate();
+  dump(m, il);
+  return 0;
+}
+
 int mu(mjModel* m, mjData* d0, mjtNum value, int iters) {
   stepCostFn_t fn = stepCost;
   ILQR<kNv, kNu, kN> il(m, d0, fn);
@@ -179,7 +204,7 @@ int mu(mjModel* m, mjData* d0, mjtNum value, int iters) {
 
 int main(int argc, const char** argv) {
   if (argc < 3) {
-    fprintf(stderr, "usage: legacy_members model.xml members | initv [iters] | mu value [iters]\n");
+    fprintf(stderr, "usage: legacy_members model.xml members | initv [iters] | mu value [iters] | mutate\n");
     return 2;
   }
   mj_activate("mjkey.txt");
@@ -191,6 +216,7 @@ int main(int argc, const char** argv) {
   for (int i = 0; i < 10; i++) mj_step(m, d);  // inverted_pendulum.cpp:12-13
   int rc = !strcmp(argv[2], "members") ? members(m, d)
            : !strcmp(argv[2], "mu")    ? mu(m, d, argc > 3 ? atof(argv[3]) : 1000.0, argc > 4 ? atoi(argv[4]) : 1)
+           : !strcmp(argv[2], "mutate") ? mutate(m, d)
                                        : initv(m, d, argc > 3 ? atoi(argv[3]) : 1);
   mj_deleteData(d);
   mj_deleteModel(m);

@@ -197,6 +197,36 @@ def test_initv_override_drives_recursion(ora, iters):
 
 
 @pytest.mark.gpu
+def test_initv_override_changing_a_point(ora):
+    """an initV override that changes a later point (dArray[N/2]->qvel[0] +=
+    1e-3 after the default initV): the reference differentiates dArray[n]
+    inside its loop, after initV (inc/ilqr.h:142-154), so the recursion sees
+    the changed state -- the legacy backwardPass re-sweeps when an override
+    changed the trajectory.  K, k, V, v and the trajectory bit-exact against
+    the oracle's backwardPass run on the changed trajectory"""
+    import ilqg_amd as ia
+    r = subprocess.run([MEMBERS, model_path("inverted_pendulum"), "mutate"], capture_output=True, text=True,
+                       timeout=600)
+    assert r.returncode == 0, r.stderr
+    got = _hex_rows(r.stdout)
+    m = ia.Model.load(model_path("inverted_pendulum"))
+    om = ora.OModel(m.blob())
+    d = om.make_data()
+    d.step(10)
+    N = 20
+    il = ora.OILQR(om, d, N, cost_fn="ora_cost_pendulum")
+    il.set_dinit(d)
+    il.forward_pass()  # iterate(): forwardPass; setDInit(dArray[N]); backwardPass
+    il.set_dinit(il.point(N))
+    il.point(N // 2).arr("qvel")[0] += 1e-3  # what the override does after the default initV
+    il.backward_pass()
+    a, t = il.arrays(), il.traj()
+    assert np.array_equal(got["K"], a["K"]) and np.array_equal(got["k"], a["k"])
+    assert np.array_equal(got["V"][0], a["V"]) and np.array_equal(got["v"][0], a["v"])
+    assert np.array_equal(got["qvel"], t["qvel"]) and np.array_equal(got["ctrl"], t["ctrl"])
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("iters", [1, 2])
 def test_legacy_mu_is_live(ora, iters):
     """the public ILQR::mu (inc/ilqr.h:65) is read by every backward pass

@@ -6,11 +6,15 @@ every rank runs ilqg_forward_sharded(rank, N) (the whole pipelined rollout,
 the FD sweep of its own points behind each chunk), one RCCL all-gather of the
 fp64 records, then the recursion.  The 8-GPU run is the driver's to launch,
 so this probe times, on one GPU, exactly what one rank executes per iteration
-except the all-gather: forward_sharded(rank, world) + riccati_pass() -- the
-recursion reading whatever records the buffer holds (a full iteration ran
-first, so they are real records of a neighbouring trajectory; the recursion's
-time does not depend on their values).  The all-gather of 3.4 MB over xGMI is
-added as a stated estimate, not measured.
+except the all-gather: forward_sharded(rank, world) + riccati_pass().
+
+The records of the points the rank does not own must be the right ones for
+the recursion's time to be representative, so every timed iteration rolls out
+the SAME trajectory: the gains are zeroed before it (outside the timed region;
+with K = 0, k = 0 the rollout u = u* reproduces the nominal trajectory bit
+for bit, inc/ilqr.h:126), and a full iteration beforehand differentiated
+every point of that trajectory.  world = 1 times ilqg_iterate the same way.
+The all-gather (3.4 MB over xGMI) is not measured here.
 
   python3 tools/cfg5_shard_probe.py [world ...]    (default: 1 2 4 8)
 """
@@ -19,9 +23,11 @@ import os
 import sys
 import time
 
+import numpy as np
+
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "ilqg-mujoco_amd"))
-import torch  # noqa: E402,F401  (torch's HIP runtime first)
+import torch  # noqa: E402  (torch's HIP runtime first)
 import ilqg_amd as ia  # noqa: E402
 import workloads  # noqa: E402
 
@@ -36,8 +42,14 @@ for world in worlds:
         g = ia.ILQR(m, st, H, ia.HUMANOID_COST)
         g.set_riccati("mfma")
         g.set_fd_precision("f32")
-        g.iterate()
+        g.iterate()  # a first update: the trajectory below is an iterate's, not the passive one
         g.synchronize()
+        K, k = g.gains()
+        Kz, kz = np.zeros_like(K), np.zeros_like(k)
+        g.set_gains(Kz, kz)
+        g.iterate()  # every point of the fixed trajectory differentiated
+        g.synchronize()
+        q0 = g.traj().qpos.copy()
 
         def one():
             if world == 1:
@@ -45,18 +57,21 @@ for world in worlds:
             else:
                 g.forward_sharded(rank, world)
                 g.riccati_pass()
-        one()
-        g.synchronize()
+        tot = 0.0
         g.set_timing(True)
         g.timing()
-        t0 = time.perf_counter()
         for _ in range(STEPS):
+            g.set_gains(Kz, kz)
+            g.synchronize()
+            t0 = time.perf_counter()
             one()
-        g.synchronize()
-        dt = (time.perf_counter() - t0) / STEPS
-        kt = {k: {"avg_ms": round(v[0] / v[1], 3), "launches_per_it": v[1] / STEPS} for k, v in g.timing().items()
-              if v[1]}
+            g.synchronize()
+            tot += time.perf_counter() - t0
+        assert np.array_equal(g.traj().qpos, q0), "the fixed trajectory moved"
+        dt = tot / STEPS
+        kt = {k_: {"avg_ms": round(v[0] / v[1], 3), "launches_per_it": v[1] / STEPS}
+              for k_, v in g.timing().items() if v[1]}
         own = int((g.point_owners(world) == rank).sum()) if world > 1 else H + 1
-        print(json.dumps({"world": world, "rank": rank, "points_owned": own, "ms_per_iter": dt * 1e3,
-                          "it_per_s": 1 / dt, "kernels": kt}), flush=True)
+        print(json.dumps({"world": world, "rank": rank, "points_owned": own, "ms_per_iter": round(dt * 1e3, 3),
+                          "it_per_s": round(1 / dt, 3), "kernels": kt}), flush=True)
         del g
