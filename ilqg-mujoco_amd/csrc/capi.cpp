@@ -277,6 +277,7 @@ struct ilqg_solver {
   int nfd = 3;  // ILQG_PIPE_STREAMS (1 .. 4), read at creation
   std::vector<hipEvent_t> pipe_ev;
   DevBuf carry[5];  // the chunked rollout's state between launches, [S][...]
+  bool pipe_ready = false;  // pipe_setup done (fd_stream, pipe_ev, carry)
   // seed groups (ilqg_solver_set_groups): the seeds as G contiguous ranges,
   // software-pipelined.  Group g has a rollout stream (CU-masked to an XCD of
   // its own: one rollout workgroup per CU) and a sweep stream (every CU but the
@@ -733,48 +734,10 @@ int ilqg_solver_create(const ilqg_model* mc, const ilqg_solver_opts* o, const il
   s->pipe_chunk = getenv_int("ILQG_PIPE_CHUNK", 10);
   s->pipe_flat = getenv_int("ILQG_PIPE_FLAT", 1) != 0;
   s->nfd = std::min(std::max(getenv_int("ILQG_PIPE_STREAMS", 3), 1), (int)ilqg_solver::kFdStreams);
-  if (s->A == 1 && s->pipe_chunk > 0 && s->pipe_chunk < (int)P) {
-    // the sweep streams leave CUs to the rollout: a rollout chunk's workgroup
-    // (the humanoid's: 147 KB of LDS, a CU to itself) waited up to 13 ms for
-    // sweep teams to free a whole CU (rocprofv3 kernel trace); one CU per seed,
-    // spread over the chip, is never given to the sweep
-    int ncu = 0;
-    e = hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, o->device);
-    if (e != hipSuccess) return fail_free(e, "hipDeviceGetAttribute");
-    // (ILQG_PIPE_KEEP: how many; ILQG_PIPE_LOW: 1 the lowest-numbered mask
-    // bits, which KFD deals round-robin over the XCDs (bit c -> XCD c % 8), so
-    // ncu / 8 of them are four CUs on every XCD; 2 the CUs of one XCD (bits
-    // c % 8 == 0), an L2 of the rollout's own; 0 spread evenly by bit).
-    // Default: the lowest ncu / 8: cfg 5 rollout chunks 212 -> 177 us per step
-    // beside the sweep (profiles/r05_cfg5_pipeline.txt)
-    const int keep = std::min(getenv_int("ILQG_PIPE_KEEP", std::max((int)S, ncu / 8)), ncu / 4);
-    const int low = getenv_int("ILQG_PIPE_LOW", 1);
-    const int nxcd = (ncu >= 64 && ncu % 8 == 0) ? 8 : 1;
-    std::vector<uint32_t> fmask((ncu + 31) / 32, 0);
-    for (int c = 0, j = 0; c < ncu; c++) {
-      bool r;
-      if (low == 1) r = c < keep;
-      else if (low == 2) r = j < keep && c % nxcd == 0;
-      else r = j < keep && (long)c * keep / ncu >= j;  // spread evenly by bit
-      if (r) j++;
-      else fmask[c / 32] |= 1u << (c % 32);
-    }
-    for (int f = 0; f < s->nfd; f++) {
-      hipStream_t& fs = s->fd_stream[f];
-      e = keep > 0 ? hipExtStreamCreateWithCUMask(&fs, (uint32_t)fmask.size(), fmask.data())
-                   : hipStreamCreateWithFlags(&fs, hipStreamNonBlocking);
-      if (e != hipSuccess) return fail_free(e, "hipStreamCreate");
-    }
-    for (int f = 0; f < 5; f++) ALLOC(s->carry[f], S * fld[f] * 8);
-    const int nch = ((int)P + s->pipe_chunk - 1) / s->pipe_chunk + 32 + ilqg_solver::kFdStreams;
-    s->pipe_ev.resize(nch, nullptr);
-    for (auto& ev : s->pipe_ev) {
-      e = hipEventCreateWithFlags(&ev, hipEventDisableTiming);
-      if (e != hipSuccess) return fail_free(e, "hipEventCreate");
-    }
-  } else {
-    s->pipe_chunk = 0;
-  }
+  // the pipeline's streams, events and carry buffers are created by the first
+  // pipelined iterate (pipe_setup): most solvers never take that path, and the
+  // box gives a process 4 hardware queues
+  if (!(s->A == 1 && s->pipe_chunk > 0 && s->pipe_chunk < (int)P)) s->pipe_chunk = 0;
   ALLOC(s->warm_c, S * P * h.nv * 8);
   ALLOC(s->cost_c, S * P * 8);
   ALLOC(s->V, S * s->nx * s->nx * 8);
@@ -972,6 +935,62 @@ static hipError_t rollout_launch(ilqg_solver* s, const SeedRange& r, RollChunk c
   }, r.st);
 }
 
+// the pipelined iterate's resources (ILQG_PIPE_STREAMS sweep streams CU-masked
+// away from the rollout's CUs, the chunk events, the carried state), created
+// on first use
+static hipError_t pipe_setup(ilqg_solver* s) {
+  if (s->pipe_ready) return hipSuccess;
+  const HostModel& h = s->model->host;
+  const size_t S = s->S, P = s->P;
+  const size_t fld[5] = {1, (size_t)h.nq, (size_t)h.nv, (size_t)h.nv, (size_t)h.nu};
+  // the sweep streams leave CUs to the rollout: a rollout chunk's workgroup
+  // (the humanoid's: 147 KB of LDS, a CU to itself) waited up to 13 ms for
+  // sweep teams to free a whole CU (rocprofv3 kernel trace); one CU per seed,
+  // spread over the chip, is never given to the sweep
+  int ncu = 0;
+  hipError_t e = hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, s->opts.device);
+  if (e != hipSuccess) return e;
+  // (ILQG_PIPE_KEEP: how many; ILQG_PIPE_LOW: 1 the lowest-numbered mask
+  // bits, which KFD deals round-robin over the XCDs (bit c -> XCD c % 8), so
+  // ncu / 8 of them are four CUs on every XCD; 2 the CUs of one XCD (bits
+  // c % 8 == 0), an L2 of the rollout's own; 0 spread evenly by bit).
+  // Default: the lowest ncu / 8: cfg 5 rollout chunks 212 -> 177 us per step
+  // beside the sweep (profiles/r05_cfg5_pipeline.txt)
+  const int keep = std::min(getenv_int("ILQG_PIPE_KEEP", std::max((int)S, ncu / 8)), ncu / 4);
+  const int low = getenv_int("ILQG_PIPE_LOW", 1);
+  const int nxcd = (ncu >= 64 && ncu % 8 == 0) ? 8 : 1;
+  std::vector<uint32_t> fmask((ncu + 31) / 32, 0);
+  for (int c = 0, j = 0; c < ncu; c++) {
+    bool r;
+    if (low == 1) r = c < keep;
+    else if (low == 2) r = j < keep && c % nxcd == 0;
+    else r = j < keep && (long)c * keep / ncu >= j;  // spread evenly by bit
+    if (r) j++;
+    else fmask[c / 32] |= 1u << (c % 32);
+  }
+  for (int f = 0; f < s->nfd; f++) {
+    hipStream_t& fs = s->fd_stream[f];
+    if (fs) continue;  // (a retry after a failed setup)
+    e = keep > 0 ? hipExtStreamCreateWithCUMask(&fs, (uint32_t)fmask.size(), fmask.data())
+                 : hipStreamCreateWithFlags(&fs, hipStreamNonBlocking);
+    if (e != hipSuccess) return e;
+  }
+  for (int f = 0; f < 5; f++) {
+    if (s->carry[f].p) continue;
+    e = s->carry[f].alloc(S * fld[f] * 8);
+    if (e != hipSuccess) return e;
+  }
+  const int nch = ((int)P + s->pipe_chunk - 1) / s->pipe_chunk + 32 + ilqg_solver::kFdStreams;
+  s->pipe_ev.resize(nch, nullptr);
+  for (auto& ev : s->pipe_ev) {
+    if (ev) continue;
+    e = hipEventCreateWithFlags(&ev, hipEventDisableTiming);
+    if (e != hipSuccess) return e;
+  }
+  s->pipe_ready = true;
+  return hipSuccess;
+}
+
 // the pipelined rollout's chunks in launch order, (lo, hi) point ranges
 // descending from P - 1 (the rollout runs n = N .. 0, inc/ilqr.h:120): C
 // points each (flat), or C halving toward the end (ILQG_PIPE_FLAT=0: a small
@@ -1024,6 +1043,7 @@ static int iterate_pipelined(ilqg_solver* s, int rank = 0, int world = 1, bool b
   const ilqg_model* m = s->model;
   const SeedRange r = whole(s);
   const int P = s->P, C = s->pipe_chunk;
+  HIPCHK(pipe_setup(s));
   int ev = 0;
   std::vector<std::pair<int, int>> chunks;
   pipe_chunks(P, C, s->pipe_flat, chunks);

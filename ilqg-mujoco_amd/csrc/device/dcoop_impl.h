@@ -3176,9 +3176,24 @@ __device__ inline real linesearch_rows(int ne, real g1, real g2, real jr, real j
 // after a compile-time-model solve (nothing reads them after the solve today;
 // a future consumer such as a contact-force cost or sensor must add the
 // write-back).
+// ILQG_SPEC_H (three-wave rollout, step_dual_split): the Newton Hessian factor
+// of the active set a full step (alpha = 1) would give is built by wave 2,
+// idle through phase 5, while the primary runs the line search; when the
+// step's active set changed and equals that set, the primary loads the factor
+// instead of building it (the factor is a function of qM, J, D and the set
+// alone: the same bits).  The oracle over the bench's rollouts: 64-77 % of the
+// rebuilds are such sets (tools/ls_study/nt_run.py).  Hand-off words:
+// T.ci[C.ibc + 1] the primary's iteration token sid * 128 + k (jr, jv of the
+// iteration in the Newton scratch), sid * 128 + 127 at the end of its solve;
+// T.ci[C.ibc + 2] the token whose factor wave 2 left at s_newton + 4 nv (the
+// warm start's factor slot, free once loaded), its active set in T.c[C.bc + 6].
+#ifndef ILQG_SPEC_H
+#define ILQG_SPEC_H 1
+#endif
+constexpr int SPEC_DONE = 127;
 template <int NV>
 __device__ inline void fwd_constraint_u(const auto& m, const auto& L, const auto& C, const Team& T, int maxiter,
-                                        real tol, bool dual) {
+                                        real tol, bool dual, int spec_sid = 0) {
 #ifdef ILQG_STAMPS
   const unsigned long long tnt_ = __builtin_amdgcn_s_memtime();
 #endif
@@ -3254,12 +3269,25 @@ __device__ inline void fwd_constraint_u(const auto& m, const auto& L, const auto
   int iter = 0;
   CNT_ADD(9, 1ull);
   STAMP(10);
+  const bool specH = ILQG_SPEC_H && spec_sid > 0 && maxiter < SPEC_DONE;
+  int* f_it = T.ci + C.ibc + 1;
+  int* f_h = T.ci + C.ibc + 2;
   while (iter < maxiter) {
     real sv[NV], Mv[NV];
     chol_solve_u<NV>(Hf, rd, grad, sv);
     STAMP(14);
     gatheru(Mv, dotu(Mr, sv));
     const real jv = row ? dotu(Jr, sv) : 0.0;
+    // the full step's active set, and the iteration's rows for wave 2
+    unsigned long long m1 = 0;
+    if (specH) {
+      m1 = __ballot(row && jr + jv < 0);
+      if (row) {
+        jar_l[r] = jr;
+        jar_l[ne + r] = jv;
+      }
+      wave_signal(f_it, spec_sid * 128 + iter + 1);
+    }
     STAMP(15);
     real alpha = 0;
     if (!(sqrt(dotu(sv, sv)) < MINVAL)) {
@@ -3302,11 +3330,21 @@ __device__ inline void fwd_constraint_u(const auto& m, const auto& L, const auto
     // the factor is a function of (qM, J, D, active set) alone: rebuilt only
     // when the active set changed since it was computed (the same bits)
     if (mask != hmask) {
-      hessian_factor_u<NV>(qM, J, T.w + L.efc_D, mask, r, Hf, rd);
+      bool got = false;
+      if (specH && mask == m1) {
+        // wave 2 built this set's factor (this iteration's token)
+        wave_wait(f_h, spec_sid * 128 + iter);
+        if ((unsigned long long)__double_as_longlong((double)T.c[C.bc + 6]) == mask) {
+          factor_load_u<NV>(sn + 4 * NV, Hf, rd);
+          got = true;
+        }
+      }
+      if (!got) hessian_factor_u<NV>(qM, J, T.w + L.efc_D, mask, r, Hf, rd);
       hmask = mask;
     }
     STAMP(19);
   }
+  if (specH) wave_signal(f_it, spec_sid * 128 + SPEC_DONE);
   if (row) jar_l[r] = jr;
   real* qa_l = T.w + L.qacc;
   real* wm_l = T.w + L.warm;
@@ -3380,14 +3418,57 @@ __device__ inline void newton_warm_prep_u(const auto& m, const auto& L, const au
   TSYNC();
 }
 
+// wave 2's side of ILQG_SPEC_H (see fwd_constraint_u): for each iteration the
+// primary announces, the factor of the active set its rows give at alpha = 1,
+// into the warm start's factor slot, announced with that iteration's token;
+// ends when the primary's solve does
+template <int NV>
+__device__ inline void newton_spec_helper(const auto& L, const auto& C, const Team& T, int sid) {
+  const int ne = T.iw[L.nefc];
+  real* sn = T.w + L.s_newton;
+  const real* jar_l = sn + 4 * NV + NV * NV;
+  const int r = T.tid;
+  const bool row = r < ne;
+  const int* f_it = T.ci + C.ibc + 1;
+  int* f_h = T.ci + C.ibc + 2;
+  int seen = sid * 128;
+  for (int guard = 0; guard < (1 << 22); guard++) {
+    const int tok = __builtin_amdgcn_readfirstlane(
+        __hip_atomic_load(f_it, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP));
+    if (tok >= sid * 128 + SPEC_DONE) break;
+    if (tok <= seen) {
+      __builtin_amdgcn_s_sleep(1);
+      continue;
+    }
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+    seen = tok;
+    const real jr = row ? jar_l[r] : 0.0, jv = row ? jar_l[ne + r] : 0.0;
+    const unsigned long long m1 = __ballot(row && jr + jv < 0);
+    real Hf[NV][NV], rd[NV];
+    hessian_factor_u<NV>(T.w + L.qM, T.w + L.efc_J, T.w + L.efc_D, m1, r, Hf, rd);
+    (void)rd;
+    if (r < NV * NV) {
+      const int i = r / NV, j = r % NV;
+      real hv = 0;
+      sfor<0, NV>(SLAM(ii) {
+        sfor<0, SK(ii) + 1>(SLAM(cc) { hv = r == SK(ii) * NV + SK(cc) ? Hf[SK(ii)][SK(cc)] : hv; });
+      });
+      if (j <= i) sn[4 * NV + r] = hv;
+    }
+    if (r == 0) T.c[C.bc + 6] = __longlong_as_double((long long)m1);
+    wave_signal(f_h, tok);
+  }
+}
+
 // dual: the primary wave of a two-wave team whose helper runs newton_warm_prep
 // concurrently; exactly one __syncthreads (after the smooth start's cost)
 __device__ inline void fwd_constraint_fast(const auto& m, const auto& L, const auto& C, const auto& X,
-                                           const Team& T, int maxiter, real tol, bool dual = false) {
+                                           const Team& T, int maxiter, real tol, bool dual = false,
+                                           int spec_sid = 0) {
   using MT = std::remove_cvref_t<decltype(m)>;
   if constexpr (StaticModel<MT>) {
     if constexpr (MT::nv <= RMAX) {
-      fwd_constraint_u<MT::nv>(m, L, C, T, maxiter, tol, dual);
+      fwd_constraint_u<MT::nv>(m, L, C, T, maxiter, tol, dual, spec_sid);
       return;
     }
   }
@@ -4304,6 +4385,13 @@ __device__ inline void step_dual_split(const auto& m, const auto& L, const auto&
   STAMPC(52);
   const int ne5 = T.iw[L.nefc];
   const bool spec = ne5 > 0 && ne5 <= TEAM_SIZE && m.nv <= RMAX;
+  // ILQG_SPEC_H: wave 2 builds the primary's Newton factors ahead (fwd_constraint_u)
+  using MT5 = std::remove_cvref_t<decltype(m)>;
+  constexpr bool spec_h_ok = [] {
+    if constexpr (StaticModel<MT5>) return ILQG_SPEC_H && MT5::nv <= RMAX && MT5::opt_iterations < SPEC_DONE;
+    else return false;
+  }();
+  const bool spec_h = spec_h_ok && spec;
   // the acceleration stage beside the helpers' phase-4 work (the factor of M
   // handed over by wave 2 as soon as it is formed), or in phase 5
   using MT4 = std::remove_cvref_t<decltype(m)>;
@@ -4370,7 +4458,7 @@ __device__ inline void step_dual_split(const auto& m, const auto& L, const auto&
     if (!acc_done) fwd_acceleration(m, L, X, T, true);
     if constexpr (!split3) STAMP(7);
     if (spec) {
-      fwd_constraint_fast(m, L, C, X, T, m.opt_iterations, m.opt_tolerance, true);
+      fwd_constraint_fast(m, L, C, X, T, m.opt_iterations, m.opt_tolerance, true, spec_h ? sid : 0);
     } else {
       phase_sync();
       fwd_constraint(m, L, C, X, T, m.opt_iterations, m.opt_tolerance);
@@ -4384,6 +4472,10 @@ __device__ inline void step_dual_split(const auto& m, const auto& L, const auto&
     if (B && !bad) late();
     // wave 2: the factor of M + h D, read by the integrator in phase 6
     if (!B && euler_late) euler_factor_rows(m, L, X, T);
+    // wave 2: the Newton factors of the full steps' active sets (ILQG_SPEC_H)
+    if constexpr (spec_h_ok) {
+      if (!B && spec_h) newton_spec_helper<MT5::nv>(L, C, T, sid);
+    }
     STAMPB(38);
   }
   phase_sync();

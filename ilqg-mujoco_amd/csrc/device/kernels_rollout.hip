@@ -160,7 +160,8 @@ __device__ inline void rollout_body(const auto& m, const auto& L, const auto& C,
   };
   if (wave >= 0) {
     // the step ids of the two-wave hand-off flags (step_dual_split) start above 0
-    if (threadIdx.x == 0) T.ci[C.ibc + 3] = T.ci[C.ibc + 4] = T.ci[C.ibc + 6] = T.ci[C.ibc + 7] = 0;
+    if (threadIdx.x == 0)
+      T.ci[C.ibc + 1] = T.ci[C.ibc + 2] = T.ci[C.ibc + 3] = T.ci[C.ibc + 4] = T.ci[C.ibc + 6] = T.ci[C.ibc + 7] = 0;
     __syncthreads();
   }
   for (int n = nhi; n >= nlo; n--) {
