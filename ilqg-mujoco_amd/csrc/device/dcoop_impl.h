@@ -3191,6 +3191,16 @@ __device__ inline real linesearch_rows(int ne, real g1, real g2, real jr, real j
 #define ILQG_SPEC_H 1
 #endif
 constexpr int SPEC_DONE = 127;
+#ifndef ILQG_EULER_EARLY
+#define ILQG_EULER_EARLY 1
+#endif
+// ILQG_SPEC_SMOOTH (opt-in): wave 2 also builds the smooth start's factor at
+// the phase's start (used when the solve starts from qacc_smooth).  Measured
+// slower: the factor can start only when phase 5 does (qacc_smooth is phase 4's
+// output), and the primary then waits for it (profiles/r06_ab_spec_smooth.txt)
+#ifndef ILQG_SPEC_SMOOTH
+#define ILQG_SPEC_SMOOTH 0
+#endif
 template <int NV>
 __device__ inline void fwd_constraint_u(const auto& m, const auto& L, const auto& C, const Team& T, int maxiter,
                                         real tol, bool dual, int spec_sid = 0) {
@@ -3224,8 +3234,11 @@ __device__ inline void fwd_constraint_u(const auto& m, const auto& L, const auto
   const real cost_smooth = lane_sum_mask(0.0, acts ? 0.5 * Di * jb * jb : -0.0, ms);
   real jw, cost_warm, Ma[NV];
   unsigned long long mw;
+  const bool specH = ILQG_SPEC_H && spec_sid > 0 && maxiter < SPEC_DONE;
   if (dual) {
-    __syncthreads();  // the helper's newton_warm_prep is in LDS
+    // the helper's newton_warm_prep is in LDS (the three-wave schedule ran it
+    // in the previous phase: no barrier here then)
+    if (!specH) __syncthreads();
     jw = row ? jar_l[r] : 0.0;
     mw = (unsigned long long)__double_as_longlong((double)T.c[C.bc + 5]);
     ldu(Ma, sn);
@@ -3262,14 +3275,22 @@ __device__ inline void fwd_constraint_u(const auto& m, const auto& L, const auto
     const real f = (row && jr < 0) ? -Di * jr : 0.0;
     sfor<0, NV>(SLAM(jj) { p[SK(jj)] = Jr[SK(jj)] * f; });
     lane_sums_mask(qc, p, mask);
-    hessian_factor_u<NV>(qM, J, T.w + L.efc_D, mask, r, Hf, rd);
+    bool got = false;
+    if (ILQG_SPEC_SMOOTH && specH && use_smooth) {
+      // the smooth start's factor: wave 2 built it at the phase's start (token sid * 128)
+      wave_wait(T.ci + C.ibc + 2, spec_sid * 128);
+      if ((unsigned long long)__double_as_longlong((double)T.c[C.bc + 7]) == mask) {
+        factor_load_u<NV>(T.c + C.buf6, Hf, rd);
+        got = true;
+      }
+    }
+    if (!got) hessian_factor_u<NV>(qM, J, T.w + L.efc_D, mask, r, Hf, rd);
   }
   sfor<0, NV>(SLAM(jj) { grad[SK(jj)] = (Ma[SK(jj)] - qfs[SK(jj)]) - qc[SK(jj)]; });
   unsigned long long hmask = mask;
   int iter = 0;
   CNT_ADD(9, 1ull);
   STAMP(10);
-  const bool specH = ILQG_SPEC_H && spec_sid > 0 && maxiter < SPEC_DONE;
   int* f_it = T.ci + C.ibc + 1;
   int* f_h = T.ci + C.ibc + 2;
   while (iter < maxiter) {
@@ -3431,6 +3452,34 @@ __device__ inline void newton_spec_helper(const auto& L, const auto& C, const Te
   const bool row = r < ne;
   const int* f_it = T.ci + C.ibc + 1;
   int* f_h = T.ci + C.ibc + 2;
+  // store the factor Hf (lower triangle, row-major nv x nv) at dst, its set in *ms_dst
+  auto publish = [&](real* dst, real* ms_dst, const real (&Hf)[NV][NV], unsigned long long set) {
+    if (r < NV * NV) {
+      const int i = r / NV, j = r % NV;
+      real hv = 0;
+      sfor<0, NV>(SLAM(ii) {
+        sfor<0, SK(ii) + 1>(SLAM(cc) { hv = r == SK(ii) * NV + SK(cc) ? Hf[SK(ii)][SK(cc)] : hv; });
+      });
+      if (j <= i) dst[r] = hv;
+    }
+    if (r == 0) *ms_dst = __longlong_as_double((long long)set);
+  };
+  if (ILQG_SPEC_SMOOTH) {
+    // the smooth start's factor (fwd_constraint_u: jb = J qacc_smooth - aref,
+    // the active set of jb < 0), in case the solve starts there; qacc_smooth is
+    // the primary's phase-4 output, the rows wave 1's
+    real Jr[NV], qas[NV];
+    sfor<0, NV>(SLAM(jj) { Jr[SK(jj)] = row ? T.w[L.efc_J + r * NV + SK(jj)] : 0.0; });
+    ldu(qas, T.w + L.qacc_smooth);
+    const real aref = row ? T.w[L.efc_aref + r] : 0.0;
+    const real jb = row ? dotu(Jr, qas) - aref : 0.0;
+    const unsigned long long ms = __ballot(row && jb < 0);
+    real Hf[NV][NV], rd[NV];
+    hessian_factor_u<NV>(T.w + L.qM, T.w + L.efc_J, T.w + L.efc_D, ms, r, Hf, rd);
+    (void)rd;
+    publish(T.c + C.buf6, T.c + C.bc + 7, Hf, ms);
+    wave_signal(f_h, sid * 128);
+  }
   int seen = sid * 128;
   for (int guard = 0; guard < (1 << 22); guard++) {
     const int tok = __builtin_amdgcn_readfirstlane(
@@ -3447,15 +3496,7 @@ __device__ inline void newton_spec_helper(const auto& L, const auto& C, const Te
     real Hf[NV][NV], rd[NV];
     hessian_factor_u<NV>(T.w + L.qM, T.w + L.efc_J, T.w + L.efc_D, m1, r, Hf, rd);
     (void)rd;
-    if (r < NV * NV) {
-      const int i = r / NV, j = r % NV;
-      real hv = 0;
-      sfor<0, NV>(SLAM(ii) {
-        sfor<0, SK(ii) + 1>(SLAM(cc) { hv = r == SK(ii) * NV + SK(cc) ? Hf[SK(ii)][SK(cc)] : hv; });
-      });
-      if (j <= i) sn[4 * NV + r] = hv;
-    }
-    if (r == 0) T.c[C.bc + 6] = __longlong_as_double((long long)m1);
+    publish(sn + 4 * NV, T.c + C.bc + 6, Hf, m1);
     wave_signal(f_h, tok);
   }
 }
@@ -4388,7 +4429,7 @@ __device__ inline void step_dual_split(const auto& m, const auto& L, const auto&
   // ILQG_SPEC_H: wave 2 builds the primary's Newton factors ahead (fwd_constraint_u)
   using MT5 = std::remove_cvref_t<decltype(m)>;
   constexpr bool spec_h_ok = [] {
-    if constexpr (StaticModel<MT5>) return ILQG_SPEC_H && MT5::nv <= RMAX && MT5::opt_iterations < SPEC_DONE;
+    if constexpr (StaticModel<MT5>) return ILQG_SPEC_H && split3 && MT5::nv <= RMAX && MT5::opt_iterations < SPEC_DONE;
     else return false;
   }();
   const bool spec_h = spec_h_ok && spec;
@@ -4465,7 +4506,9 @@ __device__ inline void step_dual_split(const auto& m, const auto& L, const auto&
     }
     STAMP(8);
   } else {
-    phase_sync();  // the primary's barrier inside its Newton start
+    // the primary's barrier inside its Newton start (none in the ILQG_SPEC_H
+    // schedule: wave 1's warm start is from phase 4)
+    if (!spec_h) phase_sync();
     // `late` (the caller's work after `pre` that no phase reads: parking the
     // prefetched record) runs here, where wave 1 has slack, so its loads have
     // landed long before
@@ -4578,13 +4621,18 @@ __device__ inline void step_dual(const auto& m, const auto& L, const auto& C, co
   // barrier inside the phase, on both waves)
   const int ne5 = T.iw[L.nefc];
   const bool spec = ne5 > 0 && ne5 <= TEAM_SIZE && m.nv <= RMAX;
+  // ILQG_EULER_EARLY: without the warm-start hand-off (the generic solver:
+  // nv > 8 or > 64 rows, the humanoid) nothing needs the barrier inside this
+  // phase, and the helper starts the Euler factor of M + h D (112k cycles a
+  // humanoid step) beside the primary's acceleration stage instead of after it
+  const bool mid_sync = spec || !ILQG_EULER_EARLY;
   if (A) {
     fwd_acceleration(m, L, X, T);
     STAMP(7);
     if (spec) {
       fwd_constraint_fast(m, L, C, X, T, m.opt_iterations, m.opt_tolerance, true);
     } else {
-      phase_sync();
+      if (mid_sync) phase_sync();
       fwd_constraint(m, L, C, X, T, m.opt_iterations, m.opt_tolerance);
     }
     STAMP(8);
@@ -4601,7 +4649,7 @@ __device__ inline void step_dual(const auto& m, const auto& L, const auto& C, co
       if (!done_u) newton_warm_prep(m, L, C, T);
     }
     STAMPB(30);
-    phase_sync();
+    if (mid_sync) phase_sync();
     if (eul) euler_prefactor(m, L, C, X, T);
     // `late` (the caller's work no phase reads: the next point's record into
     // its second buffer) where the helper waits for the constraint solve
