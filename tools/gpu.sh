@@ -12,6 +12,9 @@
 #   ab=NAME[,ENV=V...]   REPS (default 3) bench lines, 20 steps, no CPU leg;
 #                        ENV=V pairs may include ILQG_LIB=...
 #   cfg5[=NAME,ENV=V...] REPS cfg-5 humanoid bench lines (ENV may include ILQG_LIB=...)
+#   cfg5cpu              one cfg-5 bench line with its CPU baseline (cfg5_bench.json)
+#   cfg5trace            rocprofv3 kernel trace of a short cfg-5 bench (the pipeline's timeline)
+#   resources            tools/resource_report.py of the library (no GPU)
 #   prof                 rocprofv3 kernel-trace stats + FETCH/WRITE PMC passes
 #   stamps[=MODEL]       stage stamps on the diagnostic build
 #   timeline             fused-sweep timeline on the diagnostic build
@@ -62,6 +65,18 @@ for step in "$@"; do
       timeout -k 10 400 env $envs python bench.py --workload humanoid_cfg5 --no-cpu-baseline --steps 5 > $f 2> $f.err || fail cfg5 $f.err
       summ $f "cfg5 $name#$r"
     done ;;
+  cfg5cpu)
+    timeout -k 10 600 python bench.py --workload humanoid_cfg5 --steps 5 > $OUT/cfg5_bench.json 2> $OUT/cfg5_bench.err \
+      || fail cfg5cpu $OUT/cfg5_bench.err
+    summ $OUT/cfg5_bench.json "cfg5 (with cpu_baseline)" ;;
+  cfg5trace)
+    timeout -k 10 600 rocprofv3 --kernel-trace --output-format csv -d $OUT/cfg5trace -o run -- \
+      python3 bench.py --workload humanoid_cfg5 --steps 2 --warmup 1 --no-cpu-baseline \
+      > $OUT/cfg5trace.json 2> $OUT/cfg5trace.err || fail cfg5trace $OUT/cfg5trace.err
+    echo "cfg5trace ok" ;;
+  resources)
+    python3 tools/resource_report.py > $OUT/resource_usage.txt || fail resources
+    echo "resources ok" ;;
   prof)
     timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/trace -o run -- $PCMD \
       > $OUT/trace.json 2> $OUT/trace.err || fail trace $OUT/trace.err
