@@ -289,6 +289,12 @@ struct ilqg_solver {
   static constexpr int kMaxGroups = 4;
   int ngroups = 1;
   bool grp_join = true;  // the next grouped iterate waits for the solver's stream first
+  // ilqg_solver_join_stream with candidates (A > 1): only the groups' selections
+  // (which rewrite the selected costs, the nominal trajectory and setDInit) wait
+  // for the caller's work on the solver's stream, so the next rollouts still
+  // start behind their own sweeps (the pipeline survives the cost exchange)
+  bool grp_sel_join = false;
+  hipEvent_t grp_ext = nullptr;
   hipStream_t grp_roll[kMaxGroups] = {}, grp_fd[kMaxGroups] = {};
   hipEvent_t grp_sel[kMaxGroups] = {}, grp_done[kMaxGroups] = {};
   // Each group's recursion streams inside its own fused sweep launch: no
@@ -364,6 +370,7 @@ struct ilqg_solver {
       if (grp_fd[g]) (void)hipStreamDestroy(grp_fd[g]);
       if (grp_sel[g]) (void)hipEventDestroy(grp_sel[g]);
       if (grp_done[g]) (void)hipEventDestroy(grp_done[g]);
+      if (g == 0 && grp_ext) (void)hipEventDestroy(grp_ext), grp_ext = nullptr;
       grp_roll[g] = grp_fd[g] = nullptr;
       grp_sel[g] = grp_done[g] = nullptr;
     }
@@ -895,7 +902,7 @@ static TrajDev toff(TrajDev t, size_t pts, const HostModel& h) {
 // rollout of every (seed, alpha) candidate of the range, then selection + setDInit
 static hipError_t rollout_launch(ilqg_solver* s, const SeedRange& r, RollChunk ch);
 static hipError_t fd_range_launch(ilqg_solver* s, int p0, int np, hipStream_t st);
-static hipError_t forward_range(ilqg_solver* s, const SeedRange& r) {
+static hipError_t forward_range(ilqg_solver* s, const SeedRange& r, hipEvent_t before_select = nullptr) {
   const ilqg_model* m = s->model;
   const HostModel& h = m->host;
   const size_t s0 = r.s0, P = s->P, A = s->A, nx = s->nx;
@@ -909,6 +916,10 @@ static hipError_t forward_range(ilqg_solver* s, const SeedRange& r) {
   double* cc = s->cost_cand.as<double>() + s0 * A;
   hipError_t e = rollout_launch(s, r, RollChunk{});
   if (e != hipSuccess) return e;
+  if (before_select) {
+    e = hipStreamWaitEvent(r.st, before_select, 0);
+    if (e != hipSuccess) return e;
+  }
   return s->timed(1, [&] {
     return launch_select(m->dm, r.ns, s->A, s->P, s->opts.select_mode, multi ? 1 : 0, cc, s->sel.as<int>() + s0,
                          s->cost_sel.as<double>() + s0, outv, nom, di, r.st);
@@ -1318,6 +1329,13 @@ static int iterate_groups(ilqg_solver* s) {
   if (s->grp_join) {
     for (int g = 0; g < G; g++) HIPCHK(hipEventRecord(s->grp_done[g], s->stream));
     s->grp_join = false;
+    s->grp_sel_join = false;
+  }
+  hipEvent_t sel_wait = nullptr;
+  if (s->grp_sel_join) {
+    HIPCHK(hipEventRecord(s->grp_ext, s->stream));
+    sel_wait = s->grp_ext;
+    s->grp_sel_join = false;
   }
   for (int g = 0; g < G; g++) {
     const int s0 = s->S * g / G, s1 = s->S * (g + 1) / G;
@@ -1325,7 +1343,7 @@ static int iterate_groups(ilqg_solver* s) {
                 reinterpret_cast<unsigned*>(static_cast<char*>(s->grp_sync.p) + g * s->grp_sync_stride), g};
     HIPCHK(hipStreamWaitEvent(r.st, s->grp_done[g], 0));
     if (g > 0) HIPCHK(hipStreamWaitEvent(r.st, s->grp_sel[g - 1], 0));
-    HIPCHK(forward_range(s, r));
+    HIPCHK(forward_range(s, r, sel_wait));
     HIPCHK(hipEventRecord(s->grp_sel[g], r.st));
     r.st = s->grp_fd[g];
     HIPCHK(hipStreamWaitEvent(r.st, s->grp_sel[g], 0));
@@ -1568,6 +1586,7 @@ int ilqg_solver_set_groups(ilqg_solver* s, int ngroups) {
     if (e != hipSuccess) return bail(e, "hipStreamCreate");
     e = hipEventCreateWithFlags(&s->grp_sel[g], hipEventDisableTiming);
     if (e == hipSuccess) e = hipEventCreateWithFlags(&s->grp_done[g], hipEventDisableTiming);
+    if (e == hipSuccess && g == 0) e = hipEventCreateWithFlags(&s->grp_ext, hipEventDisableTiming);
     if (e != hipSuccess) return bail(e, "hipEventCreate");
   }
   const size_t ntm = (size_t)s->nut + 2 * (size_t)h.nv;
@@ -1587,7 +1606,11 @@ int ilqg_solver_get_groups(ilqg_solver* s, int* ngroups, int* rollout_cus) {
 
 int ilqg_solver_join_stream(ilqg_solver* s) {
   if (!s) return fail(ILQG_ERR_ARG, "null solver");
-  s->grp_join = true;
+  // with candidates the rollout writes only the candidate buffers, so the
+  // selection is the first launch that rewrites what the caller may read;
+  // with one candidate the rollout rewrites the nominal trajectory itself
+  if (s->ngroups > 1 && s->A > 1 && s->grp_ext) s->grp_sel_join = true;
+  else s->grp_join = true;
   return ILQG_OK;
 }
 
