@@ -71,14 +71,6 @@ hipError_t launch_select(const DevModel& m, int S, int A, int P, int mode, int c
 hipError_t launch_backward(const DevModel& m, int S, int P, double mu, const double* deriv, int Ds, TrajDev tr,
                            double* K, double* k, double* V, double* v, RicFlags fl, hipStream_t st);
 size_t backward_lds_bytes(int nv, int nu);
-// the same recursion, bit for bit, with one lane per matrix entry (riccati_mw.h:
-// hopper 6/3, pendulum 2/1, nq == nv): a multi-wave workgroup per seed.
-// done != nullptr: streamed behind a concurrent FD sweep launch (seed groups),
-// record p read once done[s P + p] >= target (handoff.h), waits bounded by fault
-bool backward_mw_supported(int nq, int nv, int nu);
-hipError_t launch_backward_mw(const DevModel& m, int S, int P, double mu, const double* deriv, int Ds, TrajDev tr,
-                              double* K, double* k, double* V, double* v, RicFlags fl, const unsigned* done,
-                              unsigned target, unsigned* fault, hipStream_t st);
 // the same recursion with the matrix products on the fp64 matrix cores
 // (riccati_mfma.h): one 4-wave workgroup per seed; agrees with the oracle to
 // rounding (the product sums run in the matrix core's order)

@@ -41,7 +41,6 @@ __device__ unsigned long long g_bstamp_cnt[16];
 
 #include "riccati.h"
 #include "riccati_mfma.h"
-#include "riccati_mw.h"
 #include "dsmall.h"
 
 namespace ilqg {
@@ -64,26 +63,6 @@ __global__ __launch_bounds__(BW_THREADS) void k_backward(DevModel m, int nq, int
   extern __shared__ double sh[];
   backward_seed<NV_, NU_>(m, nq, nv_rt, nu_rt, P, dt, mu, deriv, Ds, tr, Kg, kg, Vg, vg, blockIdx.x, threadIdx.x, sh,
                           nullptr, 0u, nullptr, fl);
-}
-
-template <int NV, int NU>
-__global__ __launch_bounds__((RicMw<NV, NU>::THREADS)) void k_backward_mw(DevModel m, int P, double dt, double mu,
-                                                                       const double* deriv, int Ds, TrajDev tr,
-                                                                       double* Kg, double* kg, double* Vg, double* vg,
-                                                                       const unsigned* done, unsigned target,
-                                                                       unsigned* fault, RicFlags fl) {
-  extern __shared__ double sh[];
-  backward_seed_mw<NV, NU>(m, P, dt, mu, deriv, Ds, tr, Kg, kg, Vg, vg, blockIdx.x, threadIdx.x, sh, done, target,
-                           fault, fl);
-}
-
-template <int NV, int NU>
-void launch_mw_t(const DevModel& m, int S, int P, double mu, const double* deriv, int Ds, TrajDev tr, double* K,
-                 double* k, double* V, double* v, RicFlags fl, const unsigned* done, unsigned target, unsigned* fault,
-                 hipStream_t st) {
-  using R = RicMw<NV, NU>;
-  hipLaunchKernelGGL((k_backward_mw<NV, NU>), dim3(S), dim3(R::THREADS), R::bytes, st, m, P, m.opt_timestep, mu,
-                     deriv, Ds, tr, K, k, V, v, done, target, fault, fl);
 }
 
 template <int NV, int NU>
@@ -136,31 +115,8 @@ hipError_t launch_backward_mfma(const DevModel& m, int S, int P, double mu, cons
   return hipGetLastError();
 }
 
-bool backward_mw_supported(int nq, int nv, int nu) {
-  return nq == nv && ((nv == 6 && nu == 3) || (nv == 2 && nu == 1));
-}
-
-hipError_t launch_backward_mw(const DevModel& m, int S, int P, double mu, const double* deriv, int Ds, TrajDev tr,
-                              double* K, double* k, double* V, double* v, RicFlags fl, const unsigned* done,
-                              unsigned target, unsigned* fault, hipStream_t st) {
-  if (!backward_mw_supported(m.nq, m.nv, m.nu)) return hipErrorInvalidValue;
-  if (m.nv == 6) launch_mw_t<6, 3>(m, S, P, mu, deriv, Ds, tr, K, k, V, v, fl, done, target, fault, st);
-  else launch_mw_t<2, 1>(m, S, P, mu, deriv, Ds, tr, K, k, V, v, fl, done, target, fault, st);
-  return hipGetLastError();
-}
-
 hipError_t launch_backward(const DevModel& m, int S, int P, double mu, const double* deriv, int Ds, TrajDev tr,
                            double* K, double* k, double* V, double* v, RicFlags fl, hipStream_t st) {
-  // ILQG_BW_MW=1: the register-formulation sizes on the one-lane-per-entry
-  // kernel (riccati_mw.h; the seed groups' streaming recursion).  Off by
-  // default: standalone it measured 3.8 us a hopper step against the one-wave
-  // kernel's 3.55 (profiles/r05_seed_groups.txt)
-  static const int mw = [] {
-    const char* e = getenv("ILQG_BW_MW");
-    return (e && e[0] == '1') ? 1 : 0;
-  }();
-  if (mw && backward_mw_supported(m.nq, m.nv, m.nu))
-    return launch_backward_mw(m, S, P, mu, deriv, Ds, tr, K, k, V, v, fl, nullptr, 0u, nullptr, st);
   if (m.nu > 32) return hipErrorInvalidValue;  // LDLT scratch bound
   const size_t lds = backward_lds_bytes(m.nv, m.nu);
   if (lds > 160 * 1024) return hipErrorInvalidValue;

@@ -81,7 +81,7 @@ for what, fn, rd, rls in (("rollout (1 seed)", g.forward_pass, L.ilqg_debug_stam
             if cnt[i]:
                 print(f"  {W2[i]:24s} calls {cnt[i]:6d}  cycles/call {acc[i]/cnt[i]:9.0f}  share {acc[i]/tot2:6.1%}")
 
-# ilqg_backward on the hopper: the one-lane-per-entry recursion (riccati_mw.h)
+# ilqg_backward on the hopper: the one-wave recursion (riccati.h)
 BN = ["A Vs col, T1, v(prev), w", "B T3, Mm, col", "C LDLT, k, K col, ABK, y", "D T4, T6", "E Vn, z, record"]
 if MFMA:
     g.set_riccati("mfma")
