@@ -47,6 +47,7 @@ struct CostDev {
 struct RicFlags {
   int layout;  // 0 reference, 1 corrected
   int vinit;   // 1: V0 / v0 are read from V / v instead of initV's (inc/ilqr.h:100-107)
+  int ldlt_lds = 0;  // k_backward_mfma<21>: 1 the LDS-resident LDLT instead of ldlt_factor_reg_t, 2 its pivot replay forced (ILQG_LDLT_REG)
 };
 __host__ __device__ inline int rec_src(int e, int nv, int nu, int layout) {
   if (!layout) return e;
@@ -72,7 +73,7 @@ hipError_t launch_backward(const DevModel& m, int S, int P, double mu, const dou
                            double* K, double* k, double* V, double* v, RicFlags fl, hipStream_t st);
 size_t backward_lds_bytes(int nv, int nu);
 // the same recursion with the matrix products on the fp64 matrix cores
-// (riccati_mfma.h): one 4-wave workgroup per seed; agrees with the oracle to
+// (riccati_mfma.h): one 8-wave workgroup per seed; agrees with the oracle to
 // rounding (the product sums run in the matrix core's order)
 hipError_t launch_backward_mfma(const DevModel& m, int S, int P, double mu, const double* deriv, int Ds, TrajDev tr,
                                 double* K, double* k, double* V, double* v, RicFlags fl, hipStream_t st);

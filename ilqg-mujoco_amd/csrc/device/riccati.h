@@ -310,6 +310,127 @@ __device__ inline void ldlt_factor_wave_t(double* mat, int* transp, double* temp
     wave_sync();
   });
 }
+__device__ __forceinline__ double readlane_f64(double x, int l) {
+  return __longlong_as_double((long long)readlane_u64((unsigned long long)__double_as_longlong(x), l));
+}
+// ldlt_factor_wave_t's factor with the matrix in registers, one row per lane.
+// ldlt_factor's pivot scan reads the diagonal entries of rows k..n-1, which no
+// earlier column has updated (entry (k, k) is updated at step k), so the pivot
+// sequence is a function of the input's diagonal alone: it is replayed first
+// (lane q holds the key of the row at position q; ldlt_factor_wave_t's scan and
+// row swaps on the keys), which also yields the rows' final order -- perm,
+// what ldlt_perm derives from transp.  Lane i then holds row perm[i] of the
+// (lower-triangle) symmetric input in that order and forms column k with
+// ldlt_factor's operations in ldlt_factor's order: temp[j] = D[j] L(k, j)
+// (lane k's products, read across the wave with v_readlane), the row's dot
+// product with temp ascending from +0, its subtraction from the input entry,
+// the division by the updated diagonal.  The factor is the same bit for bit
+// (tests/test_gpu_parity.py::test_ldlt_reg_matches_lds); a NaN or an all-zero
+// diagonal (ldlt_factor's early exit) takes ldlt_factor_wave_t + ldlt_perm.
+// Writes the lower triangle and diagonal of mat, transp and perm.
+// (replay: the replay even without equal keys, for the test)
+template <int N>
+__device__ inline void ldlt_factor_reg_t(double* mat, int* transp, int* perm, double* temp, int lane,
+                                         bool replay = false) {
+  static_assert(N >= 1 && N <= 32, "one wavefront, n <= 32");
+  const int li = lane < N ? lane : N - 1;
+  const double dg = fabs(mat[li + li * N]);
+  const unsigned long long key0 = lane < N ? (unsigned long long)__double_as_longlong(dg) : 0ull;
+  if (__ballot(lane < N && dg != dg) != 0ull || __ballot(lane < N && dg > 0) == 0ull) {
+    ldlt_factor_wave_t<N>(mat, transp, temp, lane);
+    ldlt_perm(N, transp, perm, lane);
+    return;
+  }
+  // the pivot sequence.  Distinct keys: the scan picks the largest remaining
+  // key whatever the rows' positions, so the order is the rows by |diagonal|
+  // descending -- each lane counts the keys above its own.  Equal keys (the
+  // first in the current order wins, and the swaps reorder the rest): the scan
+  // and its swaps replayed on the keys, lane q holding position q's row and key.
+  int rank = 0;
+  bool tie = false;
+  rreg::sf<0, N>([&](auto jj) __attribute__((always_inline)) {
+    constexpr int j = decltype(jj)::value;
+    const double dj = fabs(mat[j + j * N]);
+    rank += dj > dg ? 1 : 0;
+    tie = tie || (lane < N && lane != j && dj == dg);
+  });
+  int pos;
+  if (__ballot(tie) == 0ull && !replay) {
+    if (lane < N) perm[rank] = lane;
+    wave_sync();
+    pos = lane < N ? perm[lane] : 0;
+  } else {
+    pos = lane < N ? lane : 0;
+    unsigned long long ky = key0;
+    rreg::sf<0, N>([&](auto kk) __attribute__((always_inline)) {
+      constexpr int k = decltype(kk)::value;
+      const bool in = lane >= k && lane < N;
+      unsigned long long key = in ? ky : 0ull;
+      key = umax_ror<8>(key);
+      key = umax_ror<4>(key);
+      key = umax_ror<2>(key);
+      key = umax_ror<1>(key);
+      const unsigned long long m0 = readlane_u64(key, 0), m1 = readlane_u64(key, 16);
+      const unsigned long long kmax = m1 > m0 ? m1 : m0;
+      const unsigned long long hit = __ballot(in && ky == kmax);
+      const int big = kmax != 0ull ? (int)__builtin_ctzll(hit) : k;
+      if (big != k) {
+        const unsigned long long kb = readlane_u64(ky, big), kk0 = readlane_u64(ky, k);
+        const int pb = __builtin_amdgcn_readlane(pos, big), pk = __builtin_amdgcn_readlane(pos, k);
+        if (lane == k) {
+          ky = kb;
+          pos = pb;
+        } else if (lane == big) {
+          ky = kk0;
+          pos = pk;
+        }
+      }
+    });
+    if (lane < N) perm[lane] = pos;
+  }
+  // row pos of the symmetric input, columns in the final order (all reads issue
+  // before the first write below)
+  double a[N];
+  rreg::sf<0, N>([&](auto cc) __attribute__((always_inline)) {
+    constexpr int c = decltype(cc)::value;
+    const int pc = __builtin_amdgcn_readlane(pos, c);
+    const int hi = pos > pc ? pos : pc, lo = pos > pc ? pc : pos;
+    a[c] = mat[hi + lo * N];
+  });
+  // the column loop is one basic block (no stores, no branches), so the
+  // scheduler can start column k's dot products beside column k-1's division
+  double l[N], dl[N];  // L(i, j); D[j] L(i, j)
+  double dd = 0;       // lane i: D[i]
+  rreg::sf<0, N>([&](auto kk) __attribute__((always_inline)) {
+    constexpr int k = decltype(kk)::value;
+    double v = a[k];
+    if constexpr (k > 0) {
+      double si = 0;
+      rreg::sf<0, k>([&](auto jj) __attribute__((always_inline)) {
+        constexpr int j = decltype(jj)::value;
+        si += l[j] * readlane_f64(dl[j], k);
+      });
+      v -= si;
+    }
+    const double d = readlane_f64(v, k);
+    dd = lane == k ? d : dd;
+    if constexpr (N - k - 1 > 0) {
+      const double lk = fabs(d) > 0 ? v / d : v;
+      l[k] = lk;
+      dl[k] = d * lk;
+    }
+  });
+  // column j of lane i: L(i, j) below the diagonal; the lanes above it write
+  // their (unused) values into the upper triangle, which nothing reads; the
+  // diagonal last
+  if (lane < N) {
+    rreg::sf<0, N - 1>([&](auto jj) __attribute__((always_inline)) {
+      constexpr int j = decltype(jj)::value;
+      mat[lane + j * N] = l[j];
+    });
+    mat[lane + lane * N] = dd;
+  }
+}
 // a zero the compiler cannot see through, produced after v: L reads addressed
 // with it cannot be hoisted above v's computation (left free, the scheduler
 // issues all N^2 reads of an unrolled solve at once and the kernel spills)
@@ -319,12 +440,16 @@ __device__ __forceinline__ int zero_after(double v) {
   return z;
 }
 template <int N>
-__device__ inline void ldlt_solve_reg_t(const double* Lm, const int* perm, double* x, bool active) {
+__device__ inline void ldlt_solve_reg_t(const double* Lm, const int* perm, const double* src, double* x, bool dbl,
+                                        bool active) {
   const double tol = 2.2250738585072014e-308;
   double r[N];
+  // the right-hand side src (2 src when dbl: the caller's doubling, exact),
+  // solved into x
   rreg::sf<0, N>([&](auto ii) __attribute__((always_inline)) {
     constexpr int i = decltype(ii)::value;
-    r[i] = active ? x[perm[i]] : 0.0;
+    const double b = active ? src[perm[i]] : 0.0;
+    r[i] = dbl ? 2 * b : b;
   });
   // forward substitution column by column: r[i] -= L(i, j) r[j] for i > j --
   // each r[i] still receives its subtractions in ascending j, ldlt_solve's
@@ -350,6 +475,63 @@ __device__ inline void ldlt_solve_reg_t(const double* Lm, const int* perm, doubl
     rreg::sf<i + 1, N>([&](auto jj) __attribute__((always_inline)) {
       constexpr int j = decltype(jj)::value;
       r[i] -= Lc[j + i * N] * r[j];
+    });
+  });
+  rreg::sf<0, N>([&](auto ii) __attribute__((always_inline)) {
+    constexpr int i = decltype(ii)::value;
+    if (active) x[perm[i]] = r[i];
+  });
+}
+
+// x, copied once dep is computed (the copy cannot move above dep)
+__device__ __forceinline__ double copy_after(double x, double dep) {
+  double y;
+  asm volatile("v_mov_b64 %0, %1" : "=v"(y) : "v"(x), "v"(dep));
+  return y;
+}
+// ldlt_solve_reg_t with the factor read across the wave instead of from LDS:
+// lane i holds row i of the factor (L(i, j), j < i, and D(i)) in registers,
+// loaded once, and every use of L(i, j) is a v_readlane of lane i's register j
+// into scalar registers -- no LDS load, so no LDS latency, on the
+// substitutions' dependent chain.  The same operations in the same order.
+template <int N>
+__device__ inline void ldlt_solve_bcast_t(const double* Lm, const int* perm, const double* src, double* x, bool dbl,
+                                          bool active, int lane) {
+  const double tol = 2.2250738585072014e-308;
+  const int li = lane < N ? lane : 0;
+  double Lr[N];  // row li of the factor (its upper part unused)
+  rreg::sf<0, N>([&](auto jj) __attribute__((always_inline)) {
+    constexpr int j = decltype(jj)::value;
+    Lr[j] = Lm[li + j * N];
+  });
+  double r[N];
+  rreg::sf<0, N>([&](auto ii) __attribute__((always_inline)) {
+    constexpr int i = decltype(ii)::value;
+    const double b = active ? src[perm[i]] : 0.0;
+    r[i] = dbl ? 2 * b : b;
+  });
+  // (column j's reads are issued once r[j - 1] is final, row i's once r[i + 2]
+  // is: left free, the scheduler hoists every read into scalar registers and
+  // spills them -- as zero_after does for ldlt_solve_reg_t's LDS reads)
+  rreg::sf<0, N>([&](auto jj) __attribute__((always_inline)) {
+    constexpr int j = decltype(jj)::value;
+    const double Lc = j > 0 ? copy_after(Lr[j], r[j > 0 ? j - 1 : 0]) : Lr[j];
+    rreg::sf<j + 1, N>([&](auto ii) __attribute__((always_inline)) {
+      constexpr int i = decltype(ii)::value;
+      r[i] -= readlane_f64(Lc, i) * r[j];
+    });
+  });
+  rreg::sf<0, N>([&](auto ii) __attribute__((always_inline)) {
+    constexpr int i = decltype(ii)::value;
+    const double d = readlane_f64(Lr[i], i);
+    r[i] = fabs(d) > tol ? r[i] / d : 0.0;
+  });
+  rreg::sf<0, N>([&](auto ii) __attribute__((always_inline)) {
+    constexpr int i = N - 1 - decltype(ii)::value;
+    const double Lc = i + 2 < N ? copy_after(Lr[i], r[i + 2 < N ? i + 2 : 0]) : Lr[i];
+    rreg::sf<i + 1, N>([&](auto jj) __attribute__((always_inline)) {
+      constexpr int j = decltype(jj)::value;
+      r[i] -= readlane_f64(Lc, j) * r[j];
     });
   });
   rreg::sf<0, N>([&](auto ii) __attribute__((always_inline)) {

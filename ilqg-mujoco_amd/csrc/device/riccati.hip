@@ -88,8 +88,8 @@ size_t backward_mfma_lds_bytes(int nv, int nu) {
 }
 bool backward_mfma_supported(int nv, int nu) {
   const int D = nv * (2 * nv + nu) + 2 * nv + nu;
-  // stage 5 solves one right-hand side per thread: nx + 1 <= THREADS
-  return nu <= rmfma::NU_MAX && D <= rmfma::MPF * rmfma::THREADS && 2 * nv + 1 <= rmfma::THREADS &&
+  // stage 5 solves one right-hand side per thread of its waves
+  return nu <= rmfma::NU_MAX && D <= rmfma::MPF * rmfma::THREADS && 2 * nv + 1 <= 64 * rmfma::SOLVE_WAVES &&
          backward_mfma_lds_bytes(nv, nu) <= 160 * 1024;
 }
 
@@ -102,6 +102,14 @@ hipError_t launch_backward_mfma(const DevModel& m, int S, int P, double mu, cons
     const char* e = getenv("ILQG_MFMA_T");
     return (e && e[0] == '0') ? 0 : 1;
   }();
+  // ILQG_LDLT_REG=0: the compile-time instance's LDLT on LDS (ldlt_factor_wave_t)
+  // instead of in registers (ldlt_factor_reg_t), the same factor; =2: the
+  // register path with its pivot replay forced (A/B and tests; read per launch
+  // so a test can compare them in one process)
+  {
+    const char* e = getenv("ILQG_LDLT_REG");
+    fl.ldlt_lds = (e && e[0] == '0') ? 1 : (e && e[0] == '2') ? 2 : 0;
+  }
   const void* kf = (ct && m.nu == 21) ? reinterpret_cast<const void*>(k_backward_mfma<21>)
                                       : reinterpret_cast<const void*>(k_backward_mfma<0>);
   hipError_t e = hipFuncSetAttribute(kf, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);

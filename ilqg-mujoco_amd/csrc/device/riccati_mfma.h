@@ -4,7 +4,7 @@
 // north star, for models whose nx x nx products dominate (humanoid: nx = 54,
 // nu = 21: 1.23 MFLOP per step).
 //
-// One workgroup of four wavefronts per seed; every matrix LDS-resident at an
+// One workgroup of eight wavefronts (two a SIMD) per seed; every matrix LDS-resident at an
 // odd leading dimension (the 16 lanes of an MFMA operand fetch walk a row or a
 // column: an odd stride keeps them on distinct banks).  Each product is a set
 // of 16x16 output tiles dealt round-robin to the waves; K advances 4 per
@@ -24,9 +24,17 @@
 namespace ilqg {
 namespace rmfma {
 
-constexpr int THREADS = 256;  // four wavefronts
+// eight wavefronts: two a SIMD, so one wave's LDS operand loads and barrier
+// waits overlap the other's MFMAs (cfg 5's recursion 9.0 -> 8.0 ms against
+// four, 7.9 -> 9.2 at sixteen, whose 128-VGPR budget spills:
+// profiles/r06_mfma_waves.txt); ILQG_MFMA_WAVES rebuilds another count (A/B)
+#ifndef ILQG_MFMA_WAVES
+#define ILQG_MFMA_WAVES 8
+#endif
+constexpr int THREADS = 64 * ILQG_MFMA_WAVES;
 constexpr int WAVES = THREADS / 64;
-constexpr int MPF = 16;  // record prefetch registers per thread: D <= 4096
+constexpr int SOLVE_WAVES = WAVES < 4 ? WAVES : 4;  // stage 5's waves
+constexpr int MPF = 4096 / THREADS;  // record prefetch registers per thread: D <= 4096
 constexpr int NU_MAX = 32;  // pivoted-LDLT permutation tables (static __shared__ below)
 constexpr size_t STATIC_LDS_BYTES = 2 * NU_MAX * sizeof(int);
 
@@ -35,11 +43,12 @@ typedef double d4 __attribute__((ext_vector_type(4)));
 // one 16x16 tile of C = sum_k a(i, k) b(k, j), i in [i0, i0+16), j in [j0, j0+16):
 // lane l supplies a(i0 + l%16, k0 + l/16) and b(k0 + l/16, j0 + l%16); result
 // entry q of lane l is C(i0 + l/16 + 4q, j0 + l%16)
+// (k from kb, a multiple of 4: the terms below kb are zero products)
 template <class GA, class GB>
-__device__ __forceinline__ d4 tile(int i0, int j0, int K, const GA& ga, const GB& gb, int lane) {
+__device__ __forceinline__ d4 tile(int i0, int j0, int K, const GA& ga, const GB& gb, int lane, int kb = 0) {
   const int r = lane & 15, kq = lane >> 4;
   d4 acc = {0.0, 0.0, 0.0, 0.0};
-  int k0 = 0;
+  int k0 = kb;
   // four K steps a block: the block's eight operand reads issue together, then
   // its four MFMAs (the same accumulation sequence as one step at a time)
   for (; k0 + 16 <= K; k0 += 16) {
@@ -63,11 +72,11 @@ __device__ __forceinline__ d4 tile(int i0, int j0, int K, const GA& ga, const GB
 // C (rows x cols) = A B over K, tiles dealt to the waves; out(i, j, value) stores
 template <class GA, class GB, class OUT>
 __device__ __forceinline__ void product(int rows, int cols, int K, const GA& ga, const GB& gb, const OUT& out,
-                                        int wave, int lane) {
+                                        int wave, int lane, int kb = 0) {
   const int mt = (rows + 15) / 16, nt = (cols + 15) / 16;
   for (int t = wave; t < mt * nt; t += WAVES) {
     const int i0 = (t % mt) * 16, j0 = (t / mt) * 16;
-    const d4 acc = tile(i0, j0, K, ga, gb, lane);
+    const d4 acc = tile(i0, j0, K, ga, gb, lane, kb);
     const int j = j0 + (lane & 15);
 #pragma unroll
     for (int q = 0; q < 4; q++) {
@@ -208,18 +217,21 @@ __device__ inline void backward_seed_mfma(const MD& m, int nq, int nv, int nu_rt
     for (int i = tid; i < nx; i += THREADS) Vs[i + i * LX] += mu;
     __syncthreads();
     BSTAMP(0);
-    // stage 2: T1 = B' Vs (nu x nx)
+    // stage 2: T1 = B' Vs (nu x nx); B's rows below nv are zero (B = [0; dt dB]):
+    // the products over them start at the last multiple of 4 at or below nv
+    // (whole MFMA k-steps of zero terms skipped, which add exact zeros)
+    const int kb = nv & ~3;
     product(
         nu, nx, nx, [&](int a, int k) { return (a < nu && k < nx) ? B[k + a * LX] : 0.0; },
         [&](int k, int j) { return (k < nx && j < nx) ? Vs[k + j * LX] : 0.0; },
-        [&](int a, int j, double x) { X1[a + j * LU] = x; }, wave, lane);
+        [&](int a, int j, double x) { X1[a + j * LU] = x; }, wave, lane, kb);
     __syncthreads();
     BSTAMP(1);
     // stage 3: Mm = -2 T1 B - 2 R ; T3 = T1 A ; w = v + 2 Vs c
     auto gT1 = [&](int a, int k) { return (a < nu && k < nx) ? X1[a + k * LU] : 0.0; };
     product(
         nu, nu, nx, gT1, [&](int k, int b) { return (k < nx && b < nu) ? B[k + b * LX] : 0.0; },
-        [&](int a, int b, double x) { Mm[a + b * nu] = -2 * x - 2 * (r[a] * r[b]); }, wave, lane);
+        [&](int a, int b, double x) { Mm[a + b * nu] = -2 * x - 2 * (r[a] * r[b]); }, wave, lane, kb);
     product(
         nu, nx, nx, gT1, [&](int k, int j) { return (k < nx && j < nx) ? A[k + j * LX] : 0.0; },
         [&](int a, int j, double x) { Y1[a + j * LU] = x; }, wave, lane);
@@ -230,9 +242,19 @@ __device__ inline void backward_seed_mfma(const MD& m, int nq, int nv, int nu_rt
     __syncthreads();
     BSTAMP(2);
     // stage 4: LDLT of Mm (wave 0); col = B'w + r beside it (wave 1)
+    // (and perm, the solves' gather order)
     if (wave == 0) {
-      if constexpr (NU_ > 0) ldlt_factor_wave_t<NU_>(Mm, trn, tmp, lane);
-      else ldlt_factor_wave(nu, Mm, trn, tmp, lane);
+      if constexpr (NU_ > 0) {
+        if (fl.ldlt_lds == 1) {
+          ldlt_factor_wave_t<NU_>(Mm, trn, tmp, lane);
+          ldlt_perm(nu, trn, perm, lane);
+        } else {
+          ldlt_factor_reg_t<NU_>(Mm, trn, perm, tmp, lane, fl.ldlt_lds == 2);
+        }
+      } else {
+        ldlt_factor_wave(nu, Mm, trn, tmp, lane);
+        ldlt_perm(nu, trn, perm, lane);
+      }
     }
     for (int a = tid - 64; a >= 0 && a < nu; a += THREADS) {
       const double sm = dot8(nx, [&](int kk) { return B[kk + a * LX]; }, [&](int kk) { return w[kk]; });
@@ -241,21 +263,32 @@ __device__ inline void backward_seed_mfma(const MD& m, int nq, int nv, int nu_rt
     __syncthreads();
     BSTAMP(3);
     // stage 5: K = ldlt.solve(2 T3) column-parallel (in place), k = ldlt.solve(B'w + r)
-    // (columns dealt over the four waves: one solve per lane, every SIMD busy;
-    // the vector in registers, ldlt_solve_reg)
-    if (wave == 0) ldlt_perm(nu, trn, perm, lane);
-    __syncthreads();
-    for (int j = lane * WAVES + wave; j < nx + 1; j += THREADS) {
+    // (columns dealt over SOLVE_WAVES waves, one a SIMD: one solve per lane,
+    // the vector in registers, ldlt_solve_reg; a second wave on a SIMD would
+    // issue the whole instruction stream again for its few columns -- 8 waves
+    // measured 26k cycles a step against 4's 16k)
+    // (NU_ > 0: the doubling of T3 and the copy of col folded into the solve's
+    // gather, the same values)
+#ifndef ILQG_SOLVE_STRIDE
+#define ILQG_SOLVE_STRIDE 1
+#endif
+    constexpr int SS = ILQG_SOLVE_STRIDE;  // the solving waves: every SS-th
+    if (wave % SS == 0 && wave / SS < SOLVE_WAVES) {
+      const int j = lane * SOLVE_WAVES + wave / SS;  // one column per thread: nx + 1 <= 64 SOLVE_WAVES (launch_backward_mfma)
       double* x = j < nx ? Y1 + j * LU : kl;
-      if (j < nx)
-        for (int a = 0; a < nu; a++) x[a] = 2 * x[a];
-      else
-        for (int a = 0; a < nu; a++) x[a] = col[a];
-    }
-    {
-      const int j = lane * WAVES + wave;  // one column per thread: nx + 1 <= THREADS (launch_backward_mfma)
-      if constexpr (NU_ > 0) ldlt_solve_reg_t<NU_>(Mm, perm, j < nx ? Y1 + j * LU : kl, j < nx + 1);
-      else ldlt_solve_reg(nu, Mm, perm, j < nx ? Y1 + j * LU : kl, j < nx + 1);
+      if constexpr (NU_ > 0) {
+#ifndef ILQG_SOLVE_BCAST
+#define ILQG_SOLVE_BCAST 1
+#endif
+        if constexpr (ILQG_SOLVE_BCAST) ldlt_solve_bcast_t<NU_>(Mm, perm, j < nx ? x : col, x, j < nx, j < nx + 1, lane);
+        else ldlt_solve_reg_t<NU_>(Mm, perm, j < nx ? x : col, x, j < nx, j < nx + 1);
+      } else {
+        if (j < nx)
+          for (int a = 0; a < nu; a++) x[a] = 2 * x[a];
+        else if (j == nx)
+          for (int a = 0; a < nu; a++) x[a] = col[a];
+        ldlt_solve_reg(nu, Mm, perm, x, j < nx + 1);
+      }
     }
     __syncthreads();
     BSTAMP(4);

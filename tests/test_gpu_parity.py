@@ -401,6 +401,34 @@ def test_riccati_mfma_step(ia, fixture):
     assert all(e <= 1e-12 for e in errs.values()), errs
 
 
+def test_ldlt_reg_matches_lds(ia, monkeypatch):
+    """The MFMA recursion's compile-time humanoid instance (nu = 21) factors
+    Quu in registers (riccati.h ldlt_factor_reg_t: the pivot sequence replayed
+    from the diagonal, one row per lane) or on LDS (ILQG_LDLT_REG=0,
+    ldlt_factor_wave_t), with its pivot order from ranks of distinct keys or
+    from the scan replayed (ILQG_LDLT_REG=2): the same operations in the same
+    order, so K, k, V, v agree bit for bit (cfg 5's state, H = 200, after two
+    iterations)"""
+    m = ia.Model.load(model_path("humanoid"))
+    st = m.reset_state(1)
+    st.qpos[0, 2] = 1.4
+    g = ia.ILQR(m, st, 200, ia.HUMANOID_COST)
+    g.set_riccati("mfma")
+    for _ in range(2):
+        g.iterate()
+    g.synchronize()
+    out = {}
+    for flag in ("0", "1", "2"):
+        monkeypatch.setenv("ILQG_LDLT_REG", flag)
+        g.riccati_pass()
+        g.synchronize()
+        out[flag] = g.gains() + g.value()
+    for flag in ("1", "2"):
+        for a, b, n in zip(out["0"], out[flag], ("K", "k", "V", "v")):
+            assert np.isfinite(a).all(), n
+            exact(b, a, f"{n} (ILQG_LDLT_REG={flag})")
+
+
 @pytest.mark.parametrize("env", [{}, {"ILQG_FUSED": "0"}, {"ILQG_PLAN": "1"}, {"ILQG_PLAN": "1", "ILQG_FD_HALVES": "1"},
                                  {"ILQG_FD_HALVES": "1"},
                                  {"ILQG_FD_SNAP": "0"}, {"ILQG_FD_HALVES": "1", "ILQG_FD_SNAP": "0"},

@@ -16,7 +16,7 @@
 #   cfg5trace            rocprofv3 kernel trace of a short cfg-5 bench (the pipeline's timeline)
 #   resources            tools/resource_report.py of the library (no GPU)
 #   prof                 rocprofv3 kernel-trace stats + FETCH/WRITE PMC passes
-#   stamps[=MODEL]       stage stamps on the diagnostic build
+#   stamps[=MODEL[:mfma]] stage stamps on the diagnostic build
 #   timeline             fused-sweep timeline on the diagnostic build
 #   sq                   SQ instruction-mix / stall counters (3 passes)
 set -o pipefail
@@ -86,8 +86,8 @@ for step in "$@"; do
       > $OUT/write.json 2> $OUT/write.err || fail write $OUT/write.err
     python3 tools/pmc_summary.py $OUT $OUT/pmc_traffic.json || fail pmc_summary ;;
   stamps)
-    m=${arg:-hopper}
-    timeout -k 10 300 env ILQG_LIB=$DIAG python3 tools/stamps.py $m > $OUT/stamps_$m.log 2>&1 || fail stamps $OUT/stamps_$m.log
+    m=${arg:-hopper}  # MODEL or MODEL:mfma (the backward section on the MFMA engine)
+    timeout -k 10 300 env ILQG_LIB=$DIAG python3 tools/stamps.py ${m//:/ } > $OUT/stamps_${m//:/_}.log 2>&1 || fail stamps $OUT/stamps_${m//:/_}.log
     echo "stamps $m ok" ;;
   timeline)
     timeout -k 10 300 env ILQG_LIB=$DIAG python3 -u tools/fused_timeline.py 8 > $OUT/timeline.log 2>&1 || fail timeline $OUT/timeline.log
