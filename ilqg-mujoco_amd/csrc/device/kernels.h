@@ -47,7 +47,7 @@ struct CostDev {
 struct RicFlags {
   int layout;  // 0 reference, 1 corrected
   int vinit;   // 1: V0 / v0 are read from V / v instead of initV's (inc/ilqr.h:100-107)
-  int ldlt_lds = 0;  // k_backward_mfma<21>: 1 the LDS-resident LDLT instead of ldlt_factor_reg_t, 2 its pivot replay forced (ILQG_LDLT_REG)
+  int ldlt_lds = 0;  // k_backward_mfma<27, 21>: 1 the LDS-resident LDLT instead of ldlt_factor_reg_t, 2 its pivot replay forced (ILQG_LDLT_REG)
 };
 __host__ __device__ inline int rec_src(int e, int nv, int nu, int layout) {
   if (!layout) return e;

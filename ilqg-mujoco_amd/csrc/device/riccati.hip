@@ -46,13 +46,13 @@ __device__ unsigned long long g_bstamp_cnt[16];
 namespace ilqg {
 namespace {
 
-template <int NU_>
+template <int NV_, int NU_>
 __global__ __launch_bounds__(rmfma::THREADS) void k_backward_mfma(DevModel m, int nq, int nv, int nu, int P, double dt,
                                                                   double mu, const double* deriv, int Ds, TrajDev tr,
                                                                   double* Kg, double* kg, double* Vg, double* vg,
                                                                   RicFlags fl) {
   extern __shared__ double sh[];
-  rmfma::backward_seed_mfma<NU_>(m, nq, nv, nu, P, dt, mu, deriv, Ds, tr, Kg, kg, Vg, vg, blockIdx.x, sh, fl);
+  rmfma::backward_seed_mfma<NV_, NU_>(m, nq, nv, nu, P, dt, mu, deriv, Ds, tr, Kg, kg, Vg, vg, blockIdx.x, sh, fl);
 }
 
 template <int NV_, int NU_>
@@ -97,7 +97,7 @@ hipError_t launch_backward_mfma(const DevModel& m, int S, int P, double mu, cons
                                 double* K, double* k, double* V, double* v, RicFlags fl, hipStream_t st) {
   if (!backward_mfma_supported(m.nv, m.nu)) return hipErrorInvalidValue;
   const size_t lds = rmfma::lds_doubles(m.nv, m.nu) * sizeof(double);  // dynamic part
-  // nu = 21 (the bundled humanoid): the compile-time instance (ILQG_MFMA_T=0: the generic one, A/B)
+  // nv = 27, nu = 21 (the bundled humanoid): the compile-time instance (ILQG_MFMA_T=0: the generic one, A/B)
   static const int ct = [] {
     const char* e = getenv("ILQG_MFMA_T");
     return (e && e[0] == '0') ? 0 : 1;
@@ -110,15 +110,19 @@ hipError_t launch_backward_mfma(const DevModel& m, int S, int P, double mu, cons
     const char* e = getenv("ILQG_LDLT_REG");
     fl.ldlt_lds = (e && e[0] == '0') ? 1 : (e && e[0] == '2') ? 2 : 0;
   }
-  const void* kf = (ct && m.nu == 21) ? reinterpret_cast<const void*>(k_backward_mfma<21>)
-                                      : reinterpret_cast<const void*>(k_backward_mfma<0>);
+#ifndef ILQG_MFMA_NV
+#define ILQG_MFMA_NV 0  // 27: nv a compile-time constant too (A/B: 6.78 against 6.34 ms, its VGPRs spill)
+#endif
+  const bool hum = ct && (ILQG_MFMA_NV == 0 || m.nv == ILQG_MFMA_NV) && m.nu == 21;
+  const void* kf = hum ? reinterpret_cast<const void*>(k_backward_mfma<ILQG_MFMA_NV, 21>)
+                       : reinterpret_cast<const void*>(k_backward_mfma<0, 0>);
   hipError_t e = hipFuncSetAttribute(kf, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   if (e != hipSuccess) return e;
-  if (ct && m.nu == 21)
-    hipLaunchKernelGGL(k_backward_mfma<21>, dim3(S), dim3(rmfma::THREADS), lds, st, m, m.nq, m.nv, m.nu, P,
+  if (hum)
+    hipLaunchKernelGGL((k_backward_mfma<ILQG_MFMA_NV, 21>), dim3(S), dim3(rmfma::THREADS), lds, st, m, m.nq, m.nv, m.nu, P,
                        m.opt_timestep, mu, deriv, Ds, tr, K, k, V, v, fl);
   else
-    hipLaunchKernelGGL(k_backward_mfma<0>, dim3(S), dim3(rmfma::THREADS), lds, st, m, m.nq, m.nv, m.nu, P,
+    hipLaunchKernelGGL((k_backward_mfma<0, 0>), dim3(S), dim3(rmfma::THREADS), lds, st, m, m.nq, m.nv, m.nu, P,
                        m.opt_timestep, mu, deriv, Ds, tr, K, k, V, v, fl);
   return hipGetLastError();
 }

@@ -117,13 +117,14 @@ __host__ __device__ inline size_t lds_doubles(int nv, int nu) {
 // Eigen-style LDLT with symmetric pivoting (oracle ora_ldlt_factor) and its
 // solve: riccati.h ldlt_factor_wave (one wavefront) / ldlt_solve (per column)
 // NU_ > 0: nu fixed at compile time (the humanoid's 21): the LDLT and its
-// solves fully unrolled (riccati.h ldlt_factor_wave_t / ldlt_solve_reg_t, the
-// same operations); 0: any nu <= NU_MAX
-template <int NU_, class MD>
-__device__ inline void backward_seed_mfma(const MD& m, int nq, int nv, int nu_rt, int P, double dt, double mu,
+// solves fully unrolled (riccati.h ldlt_factor_reg_t / ldlt_solve_bcast_t, the
+// same operations); 0: any nu <= NU_MAX.  NV_ > 0: nv fixed too (27).
+template <int NV_, int NU_, class MD>
+__device__ inline void backward_seed_mfma(const MD& m, int nq, int nv_rt, int nu_rt, int P, double dt, double mu,
                                           const double* deriv, int Ds, TrajDev tr, double* Kg, double* kg,
                                           double* Vg, double* vg, int s, double* sh, RicFlags fl) {
   const int nu = NU_ > 0 ? NU_ : nu_rt;
+  const int nv = NV_ > 0 ? NV_ : nv_rt;  // NV_ > 0: every loop bound and index a compile-time constant
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int nx = 2 * nv, D = nv * (2 * nv + nu) + 2 * nv + nu;
   const int LX = nx | 1, LU = nu | 1;
@@ -186,35 +187,36 @@ __device__ inline void backward_seed_mfma(const MD& m, int nq, int nv, int nu_rt
       }
     };
     const double* dn = dl;
-    // stage 1: symmetrise V, assemble A/B (differentiator.h:66-71,89-92), q, r, c
-    for (int e = tid; e < nx * nx; e += THREADS) {
-      const int i = e % nx, j = e / nx;
-      Vs[i + j * LX] = (V[i + j * LX] + V[j + i * LX]) / 2;
-      double val;
-      if (i < nv && j < nv) val = (i == j) ? 1 : 0;
-      else if (i < nv) val = (i == j - nv) ? dt : 0;
-      else if (j < nv) val = dn[(i - nv) + j * nv] * dt;
-      else val = ((i - nv) == (j - nv) ? 1 : 0) + dn[nv * nv + (i - nv) + (j - nv) * nv] * dt;
-      A[i + j * LX] = val;
-    }
-    for (int e = tid; e < nx * nu; e += THREADS) {
-      const int i = e % nx, j = e / nx;
-      B[i + j * LX] = (i < nv) ? 0 : dn[2 * nv * nv + (i - nv) + j * nv] * dt;
-    }
-    for (int i = tid; i < nx; i += THREADS) {
-      q[i] = dn[2 * nv * nv + nv * nu + i];
-      // c = x*_{n-1} (-) x*_n (inc/ilqr.h:154-157; tangent space for quaternion joints)
-      if (i < nv && nq != nv) {
-        c[i] = dev::state_diff_dof(m, i, tr.qpos + pp * nq, tr.qpos + pc * nq);
-      } else {
-        const double xp = i < nv ? tr.qpos[pp * nq + i] : tr.qvel[pp * nv + i - nv];
-        const double xc = i < nv ? tr.qpos[pc * nq + i] : tr.qvel[pc * nv + i - nv];
-        c[i] = xp - xc;
+    // stage 1: symmetrise V (+ mu I), assemble A/B (differentiator.h:66-71,89-92), q, r, c
+    // (columns dealt to the waves, rows to the lanes: no index division; q, c, r
+    // on the last wave, which has the fewest columns)
+    for (int j = wave; j < nx; j += WAVES)
+      for (int i = lane; i < nx; i += 64) {
+        const double sv = (V[i + j * LX] + V[j + i * LX]) / 2;
+        Vs[i + j * LX] = i == j ? sv + mu : sv;
+        double val;
+        if (i < nv && j < nv) val = (i == j) ? 1 : 0;
+        else if (i < nv) val = (i == j - nv) ? dt : 0;
+        else if (j < nv) val = dn[(i - nv) + j * nv] * dt;
+        else val = ((i - nv) == (j - nv) ? 1 : 0) + dn[nv * nv + (i - nv) + (j - nv) * nv] * dt;
+        A[i + j * LX] = val;
       }
+    for (int j = wave; j < nu; j += WAVES)
+      for (int i = lane; i < nx; i += 64) B[i + j * LX] = (i < nv) ? 0 : dn[2 * nv * nv + (i - nv) + j * nv] * dt;
+    if (wave == WAVES - 1) {
+      for (int i = lane; i < nx; i += 64) {
+        q[i] = dn[2 * nv * nv + nv * nu + i];
+        // c = x*_{n-1} (-) x*_n (inc/ilqr.h:154-157; tangent space for quaternion joints)
+        if (i < nv && nq != nv) {
+          c[i] = dev::state_diff_dof(m, i, tr.qpos + pp * nq, tr.qpos + pc * nq);
+        } else {
+          const double xp = i < nv ? tr.qpos[pp * nq + i] : tr.qvel[pp * nv + i - nv];
+          const double xc = i < nv ? tr.qpos[pc * nq + i] : tr.qvel[pc * nv + i - nv];
+          c[i] = xp - xc;
+        }
+      }
+      for (int a = lane; a < nu; a += 64) r[a] = dn[2 * nv * nv + nv * nu + nx + a];
     }
-    for (int a = tid; a < nu; a += THREADS) r[a] = dn[2 * nv * nv + nv * nu + nx + a];
-    __syncthreads();
-    for (int i = tid; i < nx; i += THREADS) Vs[i + i * LX] += mu;
     __syncthreads();
     BSTAMP(0);
     // stage 2: T1 = B' Vs (nu x nx); B's rows below nv are zero (B = [0; dt dB]):
@@ -232,13 +234,15 @@ __device__ inline void backward_seed_mfma(const MD& m, int nq, int nv, int nu_rt
     product(
         nu, nu, nx, gT1, [&](int k, int b) { return (k < nx && b < nu) ? B[k + b * LX] : 0.0; },
         [&](int a, int b, double x) { Mm[a + b * nu] = -2 * x - 2 * (r[a] * r[b]); }, wave, lane, kb);
+    // (T3's tiles dealt from wave 4 on: Mm's went to waves 0-3; w on the last wave)
     product(
         nu, nx, nx, gT1, [&](int k, int j) { return (k < nx && j < nx) ? A[k + j * LX] : 0.0; },
-        [&](int a, int j, double x) { Y1[a + j * LU] = x; }, wave, lane);
-    for (int i = tid; i < nx; i += THREADS) {
-      const double sm = dot8(nx, [&](int j) { return Vs[i + j * LX]; }, [&](int j) { return c[j]; });
-      w[i] = v[i] + 2 * sm;
-    }
+        [&](int a, int j, double x) { Y1[a + j * LU] = x; }, (wave + 4) % WAVES, lane);
+    if (wave == WAVES - 1)
+      for (int i = lane; i < nx; i += 64) {
+        const double sm = dot8(nx, [&](int j) { return Vs[i + j * LX]; }, [&](int j) { return c[j]; });
+        w[i] = v[i] + 2 * sm;
+      }
     __syncthreads();
     BSTAMP(2);
     // stage 4: LDLT of Mm (wave 0); col = B'w + r beside it (wave 1)
@@ -292,7 +296,15 @@ __device__ inline void backward_seed_mfma(const MD& m, int nq, int nv, int nu_rt
     }
     __syncthreads();
     BSTAMP(4);
-    prefetch();
+#ifndef ILQG_PF_STAGE
+#define ILQG_PF_STAGE 9
+#endif
+    // (issued at stage 6, the record loads' registers collided with the
+    // products' and the compiler waited for the loads there: vmcnt(0) before
+    // stage 6's first MFMA, every step.  Issued at stage 9 they are waited for
+    // at stage 10 -- the same 6.22-6.27 ms a launch as issuing them at stage 7,
+    // profiles/r06_mfma_waves.txt)
+    if constexpr (ILQG_PF_STAGE == 6) prefetch();
     // stage 6: ABK = A + B K ; T6 = K'R ; y = B k + c ; kR = k'R
     auto gK = [&](int a, int j) { return (a < nu && j < nx) ? Y1[a + j * LU] : 0.0; };
     product(
@@ -302,12 +314,15 @@ __device__ inline void backward_seed_mfma(const MD& m, int nq, int nv, int nu_rt
         nx, nu, nu, [&](int i, int a) { return (i < nx && a < nu) ? Y1[a + i * LU] : 0.0; },
         [&](int a, int b) { return (a < nu && b < nu) ? r[a] * r[b] : 0.0; },
         [&](int i, int b, double x) { X1[i + b * LX] = x; }, wave, lane);
-    for (int i = tid; i < nx; i += THREADS) {
-      const double sm = dot8(nu, [&](int a) { return B[i + a * LX]; }, [&](int a) { return kl[a]; });
-      y[i] = sm + c[i];
-    }
-    for (int b = tid; b < nu; b += THREADS)
-      kR[b] = dot8(nu, [&](int a) { return kl[a]; }, [&](int a) { return r[a] * r[b]; });
+    // (y on wave 0, kR on wave 1: every wave has dealt its tiles)
+    if (wave == 0)
+      for (int i = lane; i < nx; i += 64) {
+        const double sm = dot8(nu, [&](int a) { return B[i + a * LX]; }, [&](int a) { return kl[a]; });
+        y[i] = sm + c[i];
+      }
+    if (wave == 1)
+      for (int b = lane; b < nu; b += 64)
+        kR[b] = dot8(nu, [&](int a) { return kl[a]; }, [&](int a) { return r[a] * r[b]; });
     __syncthreads();
     BSTAMP(5);
     // stage 7: T4 = ABK' Vs (into A's buffer: A is dead)
@@ -337,22 +352,34 @@ __device__ inline void backward_seed_mfma(const MD& m, int nq, int nv, int nu_rt
     }
     __syncthreads();
     BSTAMP(7);
-    // stage 9: z = (2y)' V_new ; v_new (reads the NEW V, quirk Q14)
-    for (int j = tid; j < nx; j += THREADS)
-      z[j] = dot8(nx, [&](int i) { return 2 * y[i]; }, [&](int i) { return Vn[i + j * LX]; });
+    if constexpr (ILQG_PF_STAGE == 9) prefetch();
+    // stage 9: z = (2y)' V_new ; v_new (reads the NEW V, quirk Q14).  The
+    // terms of v_new that do not read z -- v' ABK and (2 kR)' K -- beside z on
+    // waves 1 and 2 (into w and c, dead since stages 4 and 6), the gains out
+    // on the others; then z' ABK and the sum, in the oracle's order
+    static_assert(WAVES >= 4, "stage 9 deals four roles to the waves");
+    if (wave == 0) {
+      for (int j = lane; j < nx; j += 64)
+        z[j] = dot8(nx, [&](int i) { return 2 * y[i]; }, [&](int i) { return Vn[i + j * LX]; });
+    } else if (wave == 1) {
+      for (int j = lane; j < nx; j += 64)
+        w[j] = dot8(nx, [&](int i) { return v[i]; }, [&](int i) { return ABK[i + j * LX]; });
+    } else if (wave == 2) {
+      for (int j = lane; j < nx; j += 64)
+        c[j] = dot8(nu, [&](int b) { return 2 * kR[b]; }, [&](int b) { return Y1[b + j * LU]; });
+    } else {
+      // gains out (Eigen col-major K[a + j nu])
+      for (int e = tid - 192; e < nu * nx; e += THREADS - 192) {
+        const int a = e % nu, j = e / nu;
+        Kg[pc * nu * nx + e] = Y1[a + j * LU];
+      }
+      for (int a = tid - 192; a < nu; a += THREADS - 192) kg[pc * nu + a] = kl[a];
+    }
     __syncthreads();
     for (int j = tid; j < nx; j += THREADS) {
       const double ta = dot8(nx, [&](int i) { return z[i]; }, [&](int i) { return ABK[i + j * LX]; });
-      const double tb = dot8(nx, [&](int i) { return v[i]; }, [&](int i) { return ABK[i + j * LX]; });
-      const double td = dot8(nu, [&](int b) { return 2 * kR[b]; }, [&](int b) { return Y1[b + j * LU]; });
-      vn[j] = ((ta + tb) + q[j]) + td;
+      vn[j] = ((ta + w[j]) + q[j]) + c[j];
     }
-    // gains out (Eigen col-major K[a + j nu])
-    for (int e = tid; e < nu * nx; e += THREADS) {
-      const int a = e % nu, j = e / nu;
-      Kg[pc * nu * nx + e] = Y1[a + j * LU];
-    }
-    for (int a = tid; a < nu; a += THREADS) kg[pc * nu + a] = kl[a];
     __syncthreads();
     BSTAMP(8);
     for (int i = tid; i < nx; i += THREADS) v[i] = vn[i];
