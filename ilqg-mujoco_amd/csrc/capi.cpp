@@ -735,10 +735,11 @@ int ilqg_solver_create(const ilqg_model* mc, const ilqg_solver_opts* o, const il
     }
   }
   ALLOC(s->fault, 2 * ilqg_solver::kMaxGroups * sizeof(unsigned));  // one fault block (handoff.h) per seed group
-  // chunks of 10 points to the end (flat): cfg 5 19.4 iterations/s against
-  // 18.3-18.4 with 8 and 17.7-17.8 with 16 and halving tail chunks
-  // (profiles/r05_cfg5_pipeline.txt)
-  s->pipe_chunk = getenv_int("ILQG_PIPE_CHUNK", 10);
+  // chunks of 7 points to the end (flat): cfg 5 21.53-21.59 iterations/s
+  // against 21.28-21.31 with 10, 21.51 with 9, 19.9 with 6, after round 6's
+  // faster fp32 sweep and recursion (round 5: 10 best, with halving tail
+  // chunks worse; profiles/r05_cfg5_pipeline.txt, r06_cfg5_chunks.txt)
+  s->pipe_chunk = getenv_int("ILQG_PIPE_CHUNK", 7);
   s->pipe_flat = getenv_int("ILQG_PIPE_FLAT", 1) != 0;
   s->nfd = std::min(std::max(getenv_int("ILQG_PIPE_STREAMS", 3), 1), (int)ilqg_solver::kFdStreams);
   // the pipeline's streams, events and carry buffers are created by the first
