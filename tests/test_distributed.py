@@ -292,10 +292,10 @@ def test_point_owners_follow_the_pipeline():
     every rollout chunk but the last two belongs wholly to rank c % world (so
     every rank sweeps behind the rollout), the last two chunks' points are
     split in contiguous blocks over every rank, world 1 owns everything; at
-    cfg 5's size (P = 201, chunks of 10) over 8 ranks"""
+    cfg 5's size (P = 201, chunks of 7, the default, and of 10) over 8 ranks"""
     sys.path.insert(0, os.path.join(ROOT, "ilqg-mujoco_amd"))
     import ilqg_amd as ia
-    for P, C in ((201, 10), (5, 1), (5, 2), (501, 10), (10, 10), (1, 1)):
+    for P, C in ((201, 7), (201, 10), (5, 1), (5, 2), (501, 10), (10, 10), (1, 1)):
         chunks = []
         hi = P - 1
         while hi >= 0:
@@ -316,6 +316,8 @@ def test_point_owners_follow_the_pipeline():
                 assert set(own[:T].tolist()) == set(range(world))
     own = ia.point_owners(201, 10, 8)
     assert np.bincount(own[:11], minlength=8).max() <= 2  # the tail, 11 points over 8 ranks
+    own = ia.point_owners(201, 7, 8)
+    assert np.bincount(own[:12], minlength=8).max() <= 2  # the tail, 12 points (chunks 11..5, 4..0) over 8 ranks
 
 
 def test_point_range_tiles():
